@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark: batched LFT backward sweeps/s (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (driver form, N > 1)
+
+A "step" is one pass of the hot path over one batch: the fused LFT sweep
+(stage + prefix compose + all-horizon query) of every problem plus the fused
+horizon argmin, with the (T*, J*) all-gather over RCCL when N > 1.  Inputs are
+synthetic Quadrotor-shaped blocks (s = n+1 = 13, m = 4, N = 100, fp64) resident
+in HBM before timing (configs[1] of BASELINE.json; per-GPU work fixed as N
+grows -> weak scaling).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_F64_TFLOPS = 78.6  # MI355X dense fp64 (vector == matrix), MI355X_MICROARCH.md / datasheet
+PEAK_HBM_GBS = 8000.0
+
+
+def lft_flops(N, s, m):
+    """Algorithmic FLOPs of one sweep."""
+    return N * (23 * s ** 3 + 2 * s * m * m + 2 * s * s * m) - 11 * s ** 3
+
+
+def lft_bytes(N, s, m, w=8):
+    """Algorithmic HBM bytes of one sweep."""
+    return w * (N * (3 * s * s + s * m) + m * m + s + N)
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle's NumPy restatement on the host cores (rank 0 only)
+# ---------------------------------------------------------------------------
+
+def _cpu_worker(args):
+    seed0, count, s, m, N = args
+    from oracle import hop_oracle as orc
+    t0 = time.perf_counter()
+    for i in range(count):
+        A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_problem(seed0 + i, s, m, N)
+        orc.lft_sweep(A, Bm, Q, Ri, z0, QT, N)
+    return count, time.perf_counter() - t0
+
+
+def cpu_baseline(s, m, N, per_core=640, cores=None):
+    import multiprocessing as mp
+    cores = cores or min(16, os.cpu_count() or 1)
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    os.environ["OMP_NUM_THREADS"] = "1"
+    ctx = mp.get_context("spawn")
+    jobs = [(10_000 + c * per_core, per_core, s, m, N) for c in range(cores)]
+    # warm the interpreters (imports) before the timed map
+    with ctx.Pool(cores) as pool:
+        pool.map(_cpu_worker, [(0, 1, s, m, 2)] * cores)
+        t0 = time.perf_counter()
+        res = pool.map(_cpu_worker, jobs)
+        wall = time.perf_counter() - t0
+    done = sum(r[0] for r in res)
+    return {"value": done / wall, "unit": "sweeps/s", "cores": cores, "kind": "port",
+            "sample": f"{done} synthetic sweeps (s={s}, m={m}, N={N}, fp64) of the NumPy "
+                      f"restatement oracle/hop_oracle.py, {cores} processes x 1 BLAS thread, "
+                      f"{wall:.1f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
+    ap.add_argument("--s", type=int, default=13)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--t-min", type=int, default=40)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from time_opt_ilqr_amd import build as hop_build
+    from time_opt_ilqr_amd import distributed as hd
+    from time_opt_ilqr_amd import engine, synth
+
+    rank, world, local = hd.env_rank_world()
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    if rank == 0:
+        hop_build.build(verbose=False)
+    if world > 1:
+        dist.barrier()
+    dtype = torch.float64 if args.dtype == "f64" else torch.float32
+    Bn, s, m, N = args.batch, args.s, args.m, args.N
+    lo, hi = hd.shard_bounds(Bn * world, rank, world)
+    A, Bm, Q, Ri, z0, QT = synth.device_batch(hi - lo, s, m, N, seed=1234 + lo, device=dev,
+                                               dtype=dtype)
+    t_min, t_max = min(args.t_min, N), N
+
+    def step():
+        r = engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
+        if world > 1:
+            hd.gather_selection(r.t_star, r.j_star, Bn * world)
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record()
+        r = engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
+        ev[i][1].record()
+        if world > 1:
+            hd.gather_selection(r.t_star, r.j_star, Bn * world)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    status_ok = int(r.status.abs().sum().item()) == 0 and bool(torch.isfinite(r.J).all())
+
+    if rank == 0:
+        total = Bn * world * K
+        value = total / elapsed
+        fl = lft_flops(N, s, m) * (hi - lo)
+        achieved = fl / (kern_ms * 1e-3) / 1e12
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            key = f"s{s}_m{m}_N{N}_B{hi - lo}_{args.dtype}"
+            if key in tj:
+                traffic = tj[key]["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            traffic = None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(s, m, N)
+        line = {
+            "metric": "batched iLQR backward sweeps/sec, Quadrotor n=13 N=100",
+            "value": value,
+            "unit": "sweeps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / K * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (device RNG, well-conditioned SPD blocks; SURVEY.md 8(d))",
+            "config": {"workload": f"LFT sweep + fused argmin, s={s} m={m} N={N}",
+                       "batch_per_gpu": Bn, "global_batch": Bn * world, "s": s, "m": m,
+                       "N": N, "t_min": t_min, "t_max": t_max, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_F64_TFLOPS,
+                         "traffic": traffic,
+                         "kernel": "lft_sweep_kernel", "kernel_ms": kern_ms,
+                         "flops_per_sweep": lft_flops(N, s, m),
+                         "alg_bytes_per_sweep": lft_bytes(N, s, m, 8 if dtype == torch.float64 else 4)},
+            "cpu_baseline": cpu,
+            "status_ok": status_ok,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

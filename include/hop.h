@@ -1,0 +1,148 @@
+/*
+ * hop.h -- C ABI of the MI355X (gfx950) horizon-selection engine (libhop_amd.so).
+ *
+ * Drop-in boundary for the hot path of dmmsjtu-umich/time-opt-ilqr: the batched
+ * LFT propagator, the horizon argmin and the Riccati gain/value passes.  The
+ * reference exposes these as Python functions (no FFI of its own); each entry
+ * point below names the reference function it replaces.  The Python mirror in
+ * time_opt_ilqr_amd/ (ctypes) and INTEGRATION.md show the binding.
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer (hipMalloc / torch.cuda tensor storage),
+ *    row-major, batch-major, contiguous unless a stride argument says otherwise.
+ *    Strides are in ELEMENTS; a batch stride of 0 broadcasts one block to all
+ *    problems.
+ *  - Launches are asynchronous on `stream` (hipStream_t, NULL = default stream);
+ *    the library never allocates, copies or synchronises on the hot path, so the
+ *    calls are graph-capturable.
+ *  - Return value: 0 = launched; <0 = rejected before launch (HOP_E_*), see
+ *    hop_last_error() for the message.
+ *  - Numerical outcomes are reported per problem in `status` (HOP_ST_* bits),
+ *    matching the reference's exception / return conventions:
+ *      HOP_ST_JITTER    chol_inv/chol_solve needed more than the first 1e-9 jitter
+ *      HOP_ST_LU        chol_inv exhausted its jitter tries and used the fallback
+ *      HOP_ST_NONFINITE a non-finite value (reference: FloatingPointError)
+ *      HOP_ST_FAIL      not PD after every try (reference: LinAlgError, or
+ *                       backward_pass_truncated's ok=False)
+ */
+#ifndef HOP_H
+#define HOP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HOP_ABI_VERSION 1
+
+#define HOP_OK 0
+#define HOP_E_ARG (-1)
+#define HOP_E_SIZE (-2)
+#define HOP_E_HIP (-3)
+
+#define HOP_ST_JITTER 1
+#define HOP_ST_LU 2
+#define HOP_ST_NONFINITE 4
+#define HOP_ST_FAIL 8
+
+#define HOP_MAX_DIM 16 /* augmented s = n+1 <= 16, m <= 16 */
+
+int hop_abi_version(void);
+const char* hop_last_error(void);
+
+/*
+ * hop_lft_sweep_f64 / _f32
+ * Replaces propagator_all_Jt_aug(A_aug, B_aug, Q_aug, R_list, z0, QT_aug_list,
+ *                                T_use, R_inv_cached)
+ *   /root/reference/horizon_selection.py:36-86 (legacy twin
+ *   ilqr_propagator.py:209-232), for a batch of independent problems.
+ *
+ *   A_aug  [batch][n_alloc][s][s]   Q_aug [batch][n_alloc][s][s]
+ *   B_aug  [batch][n_alloc][s][m]   QT_aug[batch][n_alloc][s][s] (QT[t-1] for horizon t)
+ *   R      r_is_inverse=1: R_inv_cached;  r_is_inverse=0: raw R_k, inverted per
+ *          step with chol_inv semantics.  Element (b,k) block at
+ *          R + b*r_batch_stride + k*r_step_stride ([m][m]).
+ *   z0     [batch or 1][s]  (z0_batch_stride = s or 0)
+ *   n_use  = T_use (<= n_alloc); n_use <= 0 launches nothing (reference returns [])
+ *   max_tries = chol_inv jitter tries (8 = utils.py; 4 = legacy ilqr_propagator.py)
+ *   J      [batch][n_use]  out: J[b][t-1] = 1/2 z0^T P0^(t) z0
+ *   status [batch]         out: HOP_ST_* bits
+ *   t_min/t_max: if t_max > 0 the argmin of solver.py:522 is fused and written
+ *          to t_star [batch] / j_star [batch] (both may be NULL otherwise).
+ *   dbg_efg [batch][n_use][3][s][s] nullable: E_k, F_k, G_k (stage blocks)
+ *   dbg_prefix [batch][n_use][3][s][s] nullable: Ebar_k, Fbar_k, Gbar_k
+ */
+int hop_lft_sweep_f64(const double* A_aug, const double* B_aug, const double* Q_aug,
+                      const double* R, int64_t r_batch_stride, int64_t r_step_stride,
+                      int32_t r_is_inverse, const double* QT_aug, const double* z0,
+                      int64_t z0_batch_stride, int64_t batch, int32_t n_alloc, int32_t n_use,
+                      int32_t s, int32_t m, int32_t max_tries, int32_t t_min, int32_t t_max,
+                      double* J, int32_t* status, int32_t* t_star, double* j_star,
+                      double* dbg_efg, double* dbg_prefix, void* stream);
+int hop_lft_sweep_f32(const float* A_aug, const float* B_aug, const float* Q_aug,
+                      const float* R, int64_t r_batch_stride, int64_t r_step_stride,
+                      int32_t r_is_inverse, const float* QT_aug, const float* z0,
+                      int64_t z0_batch_stride, int64_t batch, int32_t n_alloc, int32_t n_use,
+                      int32_t s, int32_t m, int32_t max_tries, int32_t t_min, int32_t t_max,
+                      float* J, int32_t* status, int32_t* t_star, float* j_star,
+                      float* dbg_efg, float* dbg_prefix, void* stream);
+
+/*
+ * hop_select_horizon_f64 / _f32
+ * Replaces T = int(np.argmin(J[T_min-1:T_max]) + T_min)
+ *   /root/reference/solver.py:522, 590, 613 (legacy ilqr_propagator.py:496, 547).
+ *   J [batch][ld] ; first minimiser wins, a NaN wins like np.argmin.
+ *   1 <= t_min <= t_max <= ld, else HOP_E_ARG (the reference would raise).
+ */
+int hop_select_horizon_f64(const double* J, int64_t batch, int32_t ld, int32_t t_min,
+                           int32_t t_max, int32_t* t_star, double* j_star, void* stream);
+int hop_select_horizon_f32(const float* J, int64_t batch, int32_t ld, int32_t t_min,
+                           int32_t t_max, int32_t* t_star, float* j_star, void* stream);
+
+/*
+ * hop_riccati_f64 / _f32
+ * mode 0 replaces backward_pass_truncated(A_list, B_list, X, U, xg, u_ref, Q, R,
+ *        alpha, T_star, lm_lambda, wrap_idx, extra_stage_cost)
+ *        /root/reference/solver.py:156-230 (legacy ilqr_propagator.py:375-400)
+ *        horizon[b] = T_star[b]; K/k written for steps 0..T*-1.
+ * mode 1 replaces value_expansions_and_gains_prefix(A_list, B_list, X, U, xg,
+ *        u_ref, Q, R, alpha, T_bar, S_right, lm_lambda, w_stage, wrap_idx,
+ *        extra_stage_cost, reg_max_tries)  /root/reference/horizon_selection.py:97-212
+ *        Arrays are indexed by i = t + S_right; horizon[b] = T_bar + S_right.
+ *
+ *   A [batch][n_alloc][n][n]  Bm [batch][n_alloc][n][m]
+ *   X [batch][n_alloc+1][n]   U  [batch][n_alloc][m]
+ *   xg [.][n], u_ref [.][m], Q [.][n][n], R [.][m][m], Qf [.][n][n]
+ *      (batch strides in elements; Qf = as_terminal_weight(alpha), utils.py:49-62)
+ *   qxx_extra [batch][n_alloc][n][n], qx_extra [batch][n_alloc][n],
+ *   c_extra [batch][n_alloc]: extra_stage_cost (c, cx, cxx) evaluated by the
+ *      caller at (X_k, U_k); all NULL when there is no extra cost.
+ *   lm [batch] (lm_lambda), w_stage (mode 1), wrap_mask bit i = wrap_idx has i.
+ *   Outputs: K [batch][n_alloc][m][n], k [batch][n_alloc][m];
+ *      nullable Vxx [batch][n_alloc+1][n][n], Vx [batch][n_alloc+1][n],
+ *      V0 [batch][n_alloc+1]; status [batch] (HOP_ST_FAIL = ok=False / raise).
+ */
+int hop_riccati_f64(const double* A, const double* Bm, const double* X, const double* U,
+                    const double* xg, int64_t xg_batch_stride, const double* u_ref,
+                    int64_t u_ref_batch_stride, const double* Q, int64_t q_batch_stride,
+                    const double* R, int64_t r_batch_stride, const double* Qf,
+                    int64_t qf_batch_stride, const double* qxx_extra, const double* qx_extra,
+                    const double* c_extra, const int32_t* horizon, const double* lm,
+                    double w_stage, uint32_t wrap_mask, int32_t mode, int32_t reg_max_tries,
+                    int64_t batch, int32_t n_alloc, int32_t n, int32_t m, double* K, double* k,
+                    double* Vxx, double* Vx, double* V0, int32_t* status, void* stream);
+int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float* U,
+                    const float* xg, int64_t xg_batch_stride, const float* u_ref,
+                    int64_t u_ref_batch_stride, const float* Q, int64_t q_batch_stride,
+                    const float* R, int64_t r_batch_stride, const float* Qf,
+                    int64_t qf_batch_stride, const float* qxx_extra, const float* qx_extra,
+                    const float* c_extra, const int32_t* horizon, const float* lm,
+                    float w_stage, uint32_t wrap_mask, int32_t mode, int32_t reg_max_tries,
+                    int64_t batch, int32_t n_alloc, int32_t n, int32_t m, float* K, float* k,
+                    float* Vxx, float* Vx, float* V0, int32_t* status, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HOP_H */

@@ -1,0 +1,487 @@
+"""CPU restatement of the horizon-selection hot path (TEST INFRASTRUCTURE ONLY).
+
+This module is the parity oracle for the MI355X engine in ``time_opt_ilqr_amd``.
+Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
+``bench.py`` may import it, and only as the checker / CPU baseline.  The product
+path never calls into this file.
+
+It restates, in batched NumPy, the algorithm of the reference
+(dmmsjtu-umich/time-opt-ilqr) for the rows of SURVEY.md section 8(a):
+
+  a1  LFT propagator J(t) for all t ......... horizon_selection.py:36-86
+  a2  chol_inv (jitter 1e-9, x10, 8 tries, LU) utils.py:69-93
+  a3  chol_solve (jitter, no fallback) ...... utils.py:96-120
+  a4  _sym .................................. utils.py:35-37
+  a5  augmented stage blocks ................ augmented.py:10-60
+  a6  augmented terminal blocks ............. augmented.py:63-87
+  a7  terminal weight / angle wrap .......... utils.py:49-62, 127-137
+  a8  argmin horizon selection .............. solver.py:522
+  a9  truncated Riccati pass (K, k) ......... solver.py:156-230
+  a10 value expansions (Vxx, Vx, V0, K, k) .. horizon_selection.py:97-212
+  a11 brute-force J(T) curve ................ solver.py:293-358
+
+Parity pinning: tests/golden/*.npz were produced by importing the reference
+itself in the build container (tests/golden/make_golden.py).  The tests in
+tests/test_oracle_golden.py check this restatement against those vectors.
+
+Status bits (shared with the C ABI, include/hop.h):
+  1 = jitter escalated past the first try
+  2 = LU fallback used (Cholesky failed for every jitter)
+  4 = non-finite input/output encountered
+  8 = not positive definite / solve failed (reference: LinAlgError or ok=False)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+ST_JITTER = 1
+ST_LU = 2
+ST_NONFINITE = 4
+ST_FAIL = 8
+
+JITTER0 = 1e-9
+
+
+# ---------------------------------------------------------------------------
+# a4 / a2 / a3 : small dense helpers
+# ---------------------------------------------------------------------------
+
+def sym(M):
+    """0.5 (M + M^T) -- utils.py:35-37."""
+    return 0.5 * (M + M.T)
+
+
+def spd_inverse(M, jitter=JITTER0, max_tries=8):
+    """Inverse of sym(M) + eps I following utils.py:69-93.
+
+    Returns (inverse, status).  The first attempt already carries eps=jitter;
+    every failed Cholesky multiplies eps by 10; after ``max_tries`` failures an
+    LU solve of (sym(M) + eps I) is used (status bit 2).
+    """
+    S = sym(np.asarray(M, dtype=np.float64))
+    if not np.isfinite(S).all():
+        return np.full_like(S, np.nan), ST_NONFINITE
+    eye = np.eye(S.shape[0])
+    eps = float(jitter)
+    flags = 0
+    for attempt in range(int(max_tries)):
+        try:
+            low = np.linalg.cholesky(S + eps * eye)
+        except np.linalg.LinAlgError:
+            eps *= 10.0
+            flags |= ST_JITTER
+            continue
+        # two LU-based triangular solves, as the reference does
+        half = np.linalg.solve(low, eye)
+        return np.linalg.solve(low.T, half), flags
+    try:
+        return np.linalg.solve(S + eps * eye, eye), flags | ST_LU
+    except np.linalg.LinAlgError:
+        return np.full_like(S, np.nan), flags | ST_LU | ST_FAIL
+
+
+def spd_solve(M, rhs, jitter=JITTER0, max_tries=8):
+    """(sym(M) + eps I)^{-1} rhs with utils.py:96-120 semantics -> (X, status)."""
+    S = sym(np.asarray(M, dtype=np.float64))
+    rhs = np.asarray(rhs, dtype=np.float64)
+    if not (np.isfinite(S).all() and np.isfinite(rhs).all()):
+        return None, ST_NONFINITE
+    eye = np.eye(S.shape[0])
+    eps = float(jitter)
+    flags = 0
+    for attempt in range(int(max_tries)):
+        try:
+            low = np.linalg.cholesky(S + eps * eye)
+            X = np.linalg.solve(low.T, np.linalg.solve(low, rhs))
+            if not np.isfinite(X).all():
+                raise FloatingPointError
+            return X, flags
+        except (np.linalg.LinAlgError, FloatingPointError):
+            eps *= 10.0
+            flags |= ST_JITTER
+    return None, flags | ST_FAIL
+
+
+# ---------------------------------------------------------------------------
+# a1 : LFT propagator (one problem)
+# ---------------------------------------------------------------------------
+
+def lft_sweep(A, Bm, Q, R_inv, z0, QT, N=None, R_list=None, want_efg=False,
+              want_prefix=False, max_tries=8):
+    """J[t-1] for t = 1..N (horizon_selection.py:36-86), one problem.
+
+    A, Q, QT : (>=N, s, s); Bm : (>=N, s, m); R_inv : (m, m) (cached inverse)
+    or None with R_list (N, m, m) (then each stage inverse is spd_inverse(R_k)).
+    Returns dict(J, status[, E, F, G][, Ebar, Fbar, Gbar]).
+    """
+    N = len(A) if N is None else int(N)
+    out = {"status": 0}
+    if N <= 0:
+        out["J"] = np.zeros(0)
+        return out
+    status = 0
+    s = A[0].shape[0]
+
+    def inv(M):
+        nonlocal status
+        X, st = spd_inverse(M, max_tries=max_tries)
+        status |= st
+        return X
+
+    if R_inv is None:
+        rinv = [inv(R_list[k]) for k in range(N)]
+    else:
+        rinv = [np.asarray(R_inv, dtype=np.float64)] * N
+
+    # stage blocks (independent per k)
+    Es, Fs, Gs = [], [], []
+    for k in range(N):
+        Ek = inv(Q[k])
+        Fk = Ek @ A[k].T
+        Gk = sym(A[k] @ Ek @ A[k].T + Bm[k] @ rinv[k] @ Bm[k].T)
+        Es.append(Ek)
+        Fs.append(Fk)
+        Gs.append(Gk)
+
+    # prefix composition; the query for horizon t only needs prefix t-1, so
+    # it is evaluated in the same forward pass (fused stage/compose/query).
+    J = np.zeros(N)
+    z0 = np.asarray(z0, dtype=np.float64).reshape(-1)
+    Eb, Fb, Gb = Es[0], Fs[0], Gs[0]
+    pre = []
+    for k in range(N):
+        if k > 0:
+            W = inv(Es[k] + Gb)
+            FbW = Fb @ W
+            Eb = sym(Eb - FbW @ Fb.T)
+            Fb = FbW @ Fs[k]
+            Gb = sym(Gs[k] - Fs[k].T @ W @ Fs[k])
+        if want_prefix:
+            pre.append((Eb, Fb, Gb))
+        Xt = inv(QT[k])
+        Wt = inv(Xt + Gb)
+        X0 = sym(Eb - Fb @ Wt @ Fb.T)
+        P0 = inv(X0)
+        J[k] = 0.5 * float(z0 @ P0 @ z0)
+    if not np.isfinite(J).all():
+        status |= ST_NONFINITE
+    out["J"] = J
+    out["status"] = status
+    if want_efg:
+        out["E"], out["F"], out["G"] = np.array(Es), np.array(Fs), np.array(Gs)
+    if want_prefix:
+        out["Ebar"] = np.array([p[0] for p in pre])
+        out["Fbar"] = np.array([p[1] for p in pre])
+        out["Gbar"] = np.array([p[2] for p in pre])
+    return out
+
+
+def lft_sweep_batch(A, Bm, Q, R_inv, z0, QT, N=None, max_tries=8):
+    """Loop of lft_sweep over a leading batch axis.  R_inv: (m,m) or (B,m,m)."""
+    Bn = A.shape[0]
+    N = A.shape[1] if N is None else int(N)
+    J = np.zeros((Bn, N))
+    st = np.zeros(Bn, dtype=np.int32)
+    R_inv = np.asarray(R_inv)
+    z0 = np.asarray(z0)
+    for b in range(Bn):
+        r = R_inv if R_inv.ndim == 2 else R_inv[b]
+        z = z0 if z0.ndim == 1 else z0[b]
+        o = lft_sweep(A[b], Bm[b], Q[b], r, z, QT[b], N, max_tries=max_tries)
+        J[b] = o["J"]
+        st[b] = o["status"]
+    return J, st
+
+
+# ---------------------------------------------------------------------------
+# a8 : horizon selection
+# ---------------------------------------------------------------------------
+
+def select_horizon(J, T_min, T_max):
+    """T* = first minimiser of J[T_min-1 : T_max] (+T_min) -- solver.py:522.
+
+    Works on (N,) or (B, N); NaN compares like np.argmin (NaN wins).
+    """
+    J = np.asarray(J)
+    win = J[..., int(T_min) - 1:int(T_max)]
+    idx = np.argmin(win, axis=-1)
+    Jstar = np.take_along_axis(win, np.expand_dims(idx, -1), -1)[..., 0]
+    return idx + int(T_min), Jstar
+
+
+# ---------------------------------------------------------------------------
+# a7 / a5 / a6 : host preparation
+# ---------------------------------------------------------------------------
+
+def wrap_angles(e, wrap_idx):
+    """utils.py:127-137: (a + pi) mod 2 pi - pi on the listed coordinates."""
+    if not wrap_idx:
+        return e
+    e = np.array(e, dtype=np.float64, copy=True)
+    for i in wrap_idx:
+        e[..., i] = np.remainder(e[..., i] + np.pi, 2.0 * np.pi) - np.pi
+    return e
+
+
+def terminal_weight(alpha, n):
+    """utils.py:49-62."""
+    a = np.asarray(alpha, dtype=np.float64)
+    if a.ndim == 0:
+        return float(a) * np.eye(n)
+    if a.ndim == 1:
+        if a.shape != (n,):
+            raise ValueError("terminal weight vector has wrong shape")
+        return np.diag(a)
+    if a.shape != (n, n):
+        raise ValueError("terminal weight matrix has wrong shape")
+    return sym(a)
+
+
+def augment_stage(A_list, B_list, a_res, X, U, xg, u_ref, Q, R, w, wrap_idx=None,
+                  q_reg=1e-9, rho_reg=1e-12, extra=None):
+    """augmented.py:10-60 with the affine residuals a_k = F(x_k,u_k) - x_{k+1}
+    supplied by the caller (the dynamics F stays on the host)."""
+    N = len(A_list)
+    n = X.shape[1]
+    m = U.shape[1]
+    R = sym(np.asarray(R, dtype=np.float64))
+    R_inv, _ = spd_inverse(R)
+    Qs = sym(np.asarray(Q, dtype=np.float64))
+    Aa = np.zeros((N, n + 1, n + 1))
+    Ba = np.zeros((N, n + 1, m))
+    Qa = np.zeros((N, n + 1, n + 1))
+    for k in range(N):
+        e = wrap_angles(X[k] - xg, wrap_idx)
+        du = np.atleast_1d(U[k] - u_ref)
+        Qe = Q @ e
+        blk = np.zeros((n + 1, n + 1))
+        blk[:n, :n] = Qs + q_reg * np.eye(n)
+        blk[:n, n] = Qe
+        blk[n, :n] = Qe
+        blk[n, n] = float(e @ Q @ e) + 2.0 * float(w) + rho_reg
+        if extra is not None:
+            c, cx, cxx = extra(X[k], U[k])
+            blk[:n, :n] += sym(np.asarray(cxx, dtype=np.float64))
+            cx = np.asarray(cx, dtype=np.float64).reshape(-1)
+            blk[:n, n] += cx
+            blk[n, :n] += cx
+            blk[n, n] += 2.0 * float(c)
+        Qa[k] = sym(blk)
+        Aa[k, :n, :n] = A_list[k]
+        Aa[k, :n, n] = np.asarray(a_res[k]).reshape(-1) - B_list[k] @ du
+        Aa[k, n, n] = 1.0
+        Ba[k, :n, :] = B_list[k]
+    z0 = np.zeros(n + 1)
+    z0[-1] = 1.0
+    return Aa, Ba, Qa, R, z0, R_inv
+
+
+def augment_terminal(X, xg, alpha, wrap_idx=None, rho_reg=1e-12):
+    """augmented.py:63-87: QT[t-1] for t = 1..N (N = len(X) - 1)."""
+    n = X.shape[1]
+    P = sym(terminal_weight(alpha, n))
+    N = X.shape[0] - 1
+    out = np.zeros((N, n + 1, n + 1))
+    for t in range(1, N + 1):
+        e = wrap_angles(X[t] - xg, wrap_idx)
+        Pe = P @ e
+        blk = np.zeros((n + 1, n + 1))
+        blk[:n, :n] = P
+        blk[:n, n] = Pe
+        blk[n, :n] = Pe
+        blk[n, n] = float(e @ Pe) + rho_reg
+        out[t - 1] = sym(blk)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# a9 / a10 / a11 : Riccati passes
+# ---------------------------------------------------------------------------
+
+def riccati_truncated(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_star,
+                      lm_lambda=1e-3, wrap_idx=None, extra=None, want_v=False):
+    """solver.py:156-230.  Returns (k_list, K_list, ok[, Vxx_list, Vx_list]).
+
+    Vxx/Vx are internal in the reference; with want_v they are returned for
+    index 0..T_star (index T_star = terminal).
+    """
+    T = int(T_star)
+    if T <= 0:
+        return (None, None, False) + ((None, None) if want_v else ())
+    n = X.shape[1]
+    m = U.shape[1]
+    Qf = terminal_weight(alpha, n)
+    fail = (None, None, False) + ((None, None) if want_v else ())
+    eT = wrap_angles(X[T] - xg, wrap_idx)
+    if not np.isfinite(eT).all():
+        return fail
+    Vx = Qf @ eT
+    Vxx = sym(Qf)
+    ks, Ks = [None] * T, [None] * T
+    Vxxs, Vxs = [None] * (T + 1), [None] * (T + 1)
+    Vxxs[T], Vxs[T] = Vxx, Vx
+    for k in range(T - 1, -1, -1):
+        e = wrap_angles(X[k] - xg, wrap_idx)
+        du = np.atleast_1d(U[k] - u_ref)
+        if not (np.isfinite(e).all() and np.isfinite(du).all()):
+            return fail
+        lx = Q @ e
+        lu = R @ du
+        Qst = Q
+        if extra is not None:
+            _, cx, cxx = extra(X[k], U[k])
+            lx = lx + np.asarray(cx, dtype=np.float64).reshape(-1)
+            Qst = sym(Qst + np.asarray(cxx, dtype=np.float64))
+        A, B = A_list[k], B_list[k]
+        Qx = lx + A.T @ Vx
+        Qu = lu + B.T @ Vx
+        Qxx = Qst + A.T @ Vxx @ A
+        Quu = R + B.T @ Vxx @ B
+        Qux = B.T @ Vxx @ A
+        Quu_reg = sym(Quu) + float(lm_lambda) * np.eye(m)
+        try:
+            np.linalg.cholesky(Quu_reg)
+        except np.linalg.LinAlgError:
+            return fail
+        x1, s1 = spd_solve(Quu_reg, Qu)
+        x2, s2 = spd_solve(Quu_reg, Qux)
+        if x1 is None or x2 is None:
+            return fail  # reference raises LinAlgError here; treated as failure
+        kap = -x1
+        Kk = -x2
+        ks[k], Ks[k] = kap, Kk
+        Vx = Qx + Kk.T @ Qu + Qux.T @ kap + Kk.T @ Quu @ kap
+        Vxx = sym(Qxx + Kk.T @ Qux + Qux.T @ Kk + Kk.T @ Quu @ Kk)
+        if not (np.isfinite(Vx).all() and np.isfinite(Vxx).all()):
+            return fail
+        Vxxs[k], Vxs[k] = Vxx, Vx
+    if want_v:
+        return ks, Ks, True, Vxxs, Vxs
+    return ks, Ks, True
+
+
+def riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
+                   lm_lambda=1e-6, w_stage=0.0, wrap_idx=None, extra=None,
+                   reg_max_tries=12):
+    """horizon_selection.py:97-212 -> (Vxx, Vx, V0, K, k), index i = t + S_right.
+
+    Raises FloatingPointError / LinAlgError where the reference does.
+    """
+    n = X.shape[1]
+    m = U.shape[1]
+    Qf = terminal_weight(alpha, n)
+    L = int(T_bar) + int(S_right)
+    Vxx = [np.zeros((n, n)) for _ in range(L + 1)]
+    Vx = [np.zeros(n) for _ in range(L + 1)]
+    V0 = [0.0] * (L + 1)
+    K = [None] * L
+    kk = [None] * L
+    eT = wrap_angles(X[L] - xg, wrap_idx)
+    if not np.isfinite(eT).all():
+        raise FloatingPointError("non-finite terminal error")
+    Vxx[L] = sym(Qf)
+    Vx[L] = Qf @ eT
+    V0[L] = 0.5 * float(eT @ (Qf @ eT))
+    for i in range(L - 1, -1, -1):
+        e = wrap_angles(X[i] - xg, wrap_idx)
+        du = np.atleast_1d(U[i] - u_ref)
+        if not (np.isfinite(e).all() and np.isfinite(du).all()):
+            raise FloatingPointError("non-finite e/du")
+        lx = Q @ e
+        lu = R @ du
+        l0 = 0.5 * float(e @ (Q @ e)) + 0.5 * float(du @ (R @ du)) + float(w_stage)
+        Qst = Q
+        if extra is not None:
+            c, cx, cxx = extra(X[i], U[i])
+            l0 += float(c)
+            lx = lx + np.asarray(cx, dtype=np.float64).reshape(-1)
+            Qst = sym(Qst + np.asarray(cxx, dtype=np.float64))
+        A = np.asarray(A_list[i], dtype=np.float64)
+        B = np.asarray(B_list[i], dtype=np.float64)
+        Qx = lx + A.T @ Vx[i + 1]
+        Qu = lu + B.T @ Vx[i + 1]
+        Qxx = Qst + A.T @ Vxx[i + 1] @ A
+        Quu = R + B.T @ Vxx[i + 1] @ B
+        Qux = B.T @ Vxx[i + 1] @ A
+        lam = float(max(lm_lambda, 1e-12))
+        sol = None
+        for _ in range(int(reg_max_tries)):
+            Quu_reg = sym(Quu) + lam * np.eye(m)
+            a, s1 = spd_solve(Quu_reg, Qu)
+            b, s2 = spd_solve(Quu_reg, Qux)
+            if a is not None and b is not None:
+                sol = (a, b)
+                break
+            lam *= 10.0
+        if sol is None:
+            raise np.linalg.LinAlgError("Quu not PD for any regularisation")
+        a, b = sol
+        kk[i] = -a
+        K[i] = -b
+        Vxx[i] = sym(Qxx - Qux.T @ b)
+        Vx[i] = Qx - Qux.T @ a
+        V0[i] = l0 + V0[i + 1] - 0.5 * float(Qu @ a)
+    return Vxx, Vx, V0, K, kk
+
+
+def bruteforce_J(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, w, T_max,
+                 lm_lambda=1e-6, wrap_idx=None):
+    """solver.py:293-358: J[T-1] = V0 of a fresh Riccati sweep of length T."""
+    J = np.zeros(int(T_max))
+    for T in range(1, int(T_max) + 1):
+        _, _, V0, _, _ = riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R,
+                                         alpha, T, 0, lm_lambda=lm_lambda,
+                                         w_stage=w, wrap_idx=wrap_idx,
+                                         reg_max_tries=1)
+        J[T - 1] = V0[0]
+    return J
+
+
+# ---------------------------------------------------------------------------
+# Synthetic generators; PCG64 default_rng is platform-stable
+# ---------------------------------------------------------------------------
+
+def synth_lft_problem(seed, s, m, N):
+    """Well-conditioned augmented LFT inputs for one problem."""
+    rng = np.random.default_rng(int(seed))
+    n = s - 1
+    A = np.zeros((N, s, s))
+    Bm = np.zeros((N, s, m))
+    Q = np.zeros((N, s, s))
+    QT = np.zeros((N, s, s))
+    for k in range(N):
+        A[k, :n, :n] = np.eye(n) + 0.05 * rng.standard_normal((n, n))
+        A[k, :n, n] = 0.1 * rng.standard_normal(n)
+        A[k, n, n] = 1.0
+        Bm[k, :n, :] = 0.1 * rng.standard_normal((n, m))
+        M = rng.standard_normal((s, s))
+        Q[k] = M @ M.T / s + np.eye(s)
+        M = rng.standard_normal((s, s))
+        QT[k] = M @ M.T / s + np.eye(s)
+    R = np.diag(rng.uniform(0.5, 2.0, m))
+    R_inv, _ = spd_inverse(R)
+    z0 = np.zeros(s)
+    z0[-1] = 1.0
+    return A, Bm, Q, R, R_inv, z0, QT
+
+
+def synth_lft_batch(base_seed, B, s, m, N):
+    """Stack synth_lft_problem(base_seed + i) for i < B."""
+    parts = [synth_lft_problem(base_seed + i, s, m, N) for i in range(B)]
+    return tuple(np.stack([p[j] for p in parts]) for j in range(7))
+
+
+def synth_riccati_problem(seed, n, m, N):
+    """Trajectory-form Riccati inputs (A_k, B_k, X, U, xg, u_ref, Q, R, alpha)."""
+    rng = np.random.default_rng(int(seed))
+    A = np.eye(n) + 0.05 * rng.standard_normal((N, n, n))
+    B = 0.1 * rng.standard_normal((N, n, m))
+    X = 0.5 * rng.standard_normal((N + 1, n))
+    U = 0.1 * rng.standard_normal((N, m))
+    xg = 0.2 * rng.standard_normal(n)
+    u_ref = 0.05 * rng.standard_normal(m)
+    M = rng.standard_normal((n, n))
+    Q = M @ M.T / n + 0.5 * np.eye(n)
+    R = np.diag(rng.uniform(0.5, 2.0, m))
+    alpha = float(rng.uniform(5.0, 20.0))
+    return A, B, X, U, xg, u_ref, Q, R, alpha

@@ -1,0 +1,237 @@
+"""Generate the committed golden vectors by running the REFERENCE itself.
+
+Run in the build container only (the reference tree is not on the GPU box):
+
+    cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/make_golden.py
+
+It imports the reference modules from /root/reference (read-only, no bytecode
+written) and stores inputs/outputs as .npz data files next to this script.
+Synthetic inputs come from oracle.hop_oracle.synth_* (seeded PCG64), so only
+seeds, shapes and the reference outputs are stored for them; real-system
+captures (DoubleIntegrator, Quadrotor) store inputs too.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, REPO)
+sys.path.insert(0, REF)
+os.environ.setdefault("MPLBACKEND", "Agg")
+
+import utils as ref_utils  # noqa: E402
+import horizon_selection as ref_hs  # noqa: E402
+import solver as ref_solver  # noqa: E402
+import systems as ref_systems  # noqa: E402
+
+from oracle import hop_oracle as orc  # noqa: E402
+
+
+def _lists(*arrs):
+    return [list(a) for a in arrs]
+
+
+def synthetic_lft(tag, s, m, N, base_seed, count, T_min, T_max, efg_steps=4):
+    Js, Es, Fs, Gs = [], [], [], []
+    for i in range(count):
+        A, Bm, Q, R, R_inv, z0, QT = orc.synth_lft_problem(base_seed + i, s, m, N)
+        captured = []
+        real_chol_inv = ref_hs.chol_inv
+
+        def spy(M, *a, **k):
+            out = real_chol_inv(M, *a, **k)
+            captured.append(out)
+            return out
+
+        ref_hs.chol_inv = spy
+        try:
+            J = ref_hs.propagator_all_Jt_aug(list(A), list(Bm), list(Q), [R] * N, z0,
+                                             list(QT), T_use=N, R_inv_cached=R_inv)
+        finally:
+            ref_hs.chol_inv = real_chol_inv
+        # the first N chol_inv calls are E_k = chol_inv(Q_aug[k]) (horizon_selection.py:58)
+        E = np.array(captured[:efg_steps])
+        F = np.array([E[k] @ A[k].T for k in range(efg_steps)])
+        G = np.array([ref_utils._sym(A[k] @ E[k] @ A[k].T + Bm[k] @ R_inv @ Bm[k].T)
+                      for k in range(efg_steps)])
+        Js.append(J)
+        Es.append(E)
+        Fs.append(F)
+        Gs.append(G)
+    J = np.array(Js)
+    Tstar = np.array([int(np.argmin(j[T_min - 1:T_max]) + T_min) for j in J])
+    np.savez_compressed(os.path.join(HERE, f"lft_synth_{tag}.npz"), s=s, m=m, N=N,
+                        base_seed=base_seed, count=count, T_min=T_min, T_max=T_max,
+                        J=J, T_star=Tstar, E=np.array(Es), F=np.array(Fs), G=np.array(Gs))
+    print(f"lft_synth_{tag}: J[0,:3]={J[0, :3]} T*={Tstar}")
+
+
+def synthetic_lft_rlist(tag, s, m, N, seed):
+    """R_inv_cached=None path: per-stage R_k inverted inside the propagator."""
+    A, Bm, Q, R, R_inv, z0, QT = orc.synth_lft_problem(seed, s, m, N)
+    rng = np.random.default_rng(seed + 777)
+    Rl = np.array([np.diag(rng.uniform(0.5, 2.0, m)) for _ in range(N)])
+    J = ref_hs.propagator_all_Jt_aug(list(A), list(Bm), list(Q), list(Rl), z0, list(QT),
+                                     T_use=N, R_inv_cached=None)
+    np.savez_compressed(os.path.join(HERE, f"lft_rlist_{tag}.npz"), s=s, m=m, N=N, seed=seed,
+                        R_list=Rl, J=J)
+    print(f"lft_rlist_{tag}: J[:3]={J[:3]}")
+
+
+def real_capture(tag, maker_kwargs, maker, T_min=None, T_max=None, max_iter=12,
+                 S_window=20, central=False):
+    out = maker(**maker_kwargs)
+    F, x0, xg, u_ref, Q, R, alpha, w, N, tmin, tmax, wrap_idx, extra = out
+    T_min = tmin if T_min is None else T_min
+    T_max = tmax if T_max is None else T_max
+    prop_calls, bwd_calls = [], []
+    real_prop = ref_solver.propagator_all_Jt_aug
+    real_bwd = ref_solver.backward_pass_truncated
+
+    def prop_spy(A_aug, B_aug, Q_aug, R_list, z0, QT, T_use=None, R_inv_cached=None):
+        J = real_prop(A_aug, B_aug, Q_aug, R_list, z0, QT, T_use=T_use,
+                      R_inv_cached=R_inv_cached)
+        prop_calls.append(dict(A=np.array(A_aug[:T_use]), B=np.array(B_aug[:T_use]),
+                               Q=np.array(Q_aug[:T_use]), QT=np.array(QT[:T_use]),
+                               z0=np.array(z0), R_inv=np.array(R_inv_cached),
+                               T_use=int(T_use), J=np.array(J)))
+        return J
+
+    def bwd_spy(A_list, B_list, X, U, xg_, u_ref_, Q_, R_, alpha_, T_star, **kw):
+        res = real_bwd(A_list, B_list, X, U, xg_, u_ref_, Q_, R_, alpha_, T_star, **kw)
+        bwd_calls.append(dict(A=np.array(A_list), B=np.array(B_list), X=np.array(X),
+                              U=np.array(U), T_star=int(T_star),
+                              lm=float(kw.get("lm_lambda", 1e-3)), ok=bool(res[2]),
+                              k=None if res[0] is None else np.array(res[0]),
+                              K=None if res[1] is None else np.array(res[1])))
+        return res
+
+    ref_solver.propagator_all_Jt_aug = prop_spy
+    ref_solver.backward_pass_truncated = bwd_spy
+    try:
+        sol = ref_solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max,
+                                      method="propagator", max_iter=max_iter,
+                                      S_window=S_window, wrap_idx=wrap_idx,
+                                      use_central_diff=central, extra_stage_cost=None)
+    finally:
+        ref_solver.propagator_all_Jt_aug = real_prop
+        ref_solver.backward_pass_truncated = real_bwd
+    first, last = prop_calls[0], prop_calls[-1]
+    b_last = [c for c in bwd_calls if c["ok"]][-1]
+    d = dict(N=N, T_min=T_min, T_max=T_max, alpha=alpha, w=w, Q=Q, R=R, xg=xg,
+             u_ref=u_ref, wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64),
+             T_star_final=sol["T_star"], J_hist=np.array(sol["J_hist"]),
+             T_hist=np.array(sol["T_hist"]), n_prop_calls=len(prop_calls))
+    for name, c in (("first", first), ("last", last)):
+        for key in ("A", "B", "Q", "QT", "z0", "R_inv", "J"):
+            d[f"p{name}_{key}"] = c[key]
+        d[f"p{name}_T_use"] = c["T_use"]
+    for key in ("A", "B", "X", "U", "k", "K"):
+        d[f"bwd_{key}"] = b_last[key]
+    d["bwd_T_star"] = b_last["T_star"]
+    d["bwd_lm"] = b_last["lm"]
+    # brute-force J curve on the last backward call's linearisation
+    d["bf_J"] = np.array(ref_solver.bruteforce_all_Jt_backward_expansion(
+        list(b_last["A"]), list(b_last["B"]), b_last["X"], b_last["U"], xg, u_ref, Q, R,
+        alpha, w, min(T_max, len(b_last["U"])), wrap_idx=wrap_idx))
+    np.savez_compressed(os.path.join(HERE, f"real_{tag}.npz"), **d)
+    print(f"real_{tag}: T*={sol['T_star']} J*={sol['J_hist'][-1] if sol['J_hist'] else None} "
+          f"prop calls={len(prop_calls)}")
+
+
+def riccati_synth(tag, n, m, N, seeds, T_stars, lm):
+    rows = []
+    for seed, T in zip(seeds, T_stars):
+        A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed, n, m, N)
+        k_list, K_list, ok = ref_solver.backward_pass_truncated(
+            list(A), list(B), X, U, xg, u_ref, Q, R, alpha, T, lm_lambda=lm)
+        Vxx, Vx, V0, K2, k2 = ref_hs.value_expansions_and_gains_prefix(
+            list(A), list(B), X, U, xg, u_ref, Q, R, alpha, T, 0, lm_lambda=lm, w_stage=0.01)
+        rows.append(dict(seed=seed, T=T, ok=ok, k=np.array(k_list), K=np.array(K_list),
+                         Vxx=np.array(Vxx), Vx=np.array(Vx), V0=np.array(V0),
+                         K2=np.array(K2), k2=np.array(k2)))
+    d = dict(n=n, m=m, N=N, lm=lm, seeds=np.array(seeds), T_stars=np.array(T_stars),
+             w_stage=0.01)
+    for i, r in enumerate(rows):
+        for key in ("k", "K", "Vxx", "Vx", "V0", "K2", "k2"):
+            d[f"p{i}_{key}"] = r[key]
+        d[f"p{i}_ok"] = r["ok"]
+    np.savez_compressed(os.path.join(HERE, f"riccati_synth_{tag}.npz"), **d)
+    print(f"riccati_synth_{tag}: ok={[r['ok'] for r in rows]} k0={rows[0]['k'][0]}")
+
+
+def riccati_shift(tag, n, m, N, seed, T_bar, S_right, lm):
+    """value_expansions_and_gains_prefix with a negative-time prefix (S_right > 0)."""
+    A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed, n, m, N)
+    Vxx, Vx, V0, K, k = ref_hs.value_expansions_and_gains_prefix(
+        list(A), list(B), X, U, xg, u_ref, Q, R, alpha, T_bar, S_right, lm_lambda=lm,
+        w_stage=0.02, wrap_idx=[1])
+    np.savez_compressed(os.path.join(HERE, f"riccati_shift_{tag}.npz"), n=n, m=m, N=N,
+                        seed=seed, T_bar=T_bar, S_right=S_right, lm=lm, w_stage=0.02,
+                        wrap_idx=np.array([1]), Vxx=np.array(Vxx), Vx=np.array(Vx),
+                        V0=np.array(V0), K=np.array(K), k=np.array(k))
+    print(f"riccati_shift_{tag}: V0[0]={V0[0]}")
+
+
+def riccati_fail(tag, n, m, N, seed):
+    """Indefinite R -> backward_pass_truncated returns (None, None, False)."""
+    A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed, n, m, N)
+    Rneg = -50.0 * np.eye(m)
+    res = ref_solver.backward_pass_truncated(list(A), list(B), X, U, xg, u_ref, Q, Rneg,
+                                             alpha, N, lm_lambda=1e-3)
+    np.savez_compressed(os.path.join(HERE, f"riccati_fail_{tag}.npz"), n=n, m=m, N=N,
+                        seed=seed, R=Rneg, ok=res[2])
+    print(f"riccati_fail_{tag}: ok={res[2]}")
+
+
+def bruteforce_synth(tag, n, m, N, seed, T_max, w):
+    A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed, n, m, N)
+    J = ref_solver.bruteforce_all_Jt_backward_expansion(list(A), list(B), X, U, xg, u_ref,
+                                                         Q, R, alpha, w, T_max)
+    np.savez_compressed(os.path.join(HERE, f"bruteforce_{tag}.npz"), n=n, m=m, N=N,
+                        seed=seed, T_max=T_max, w=w, J=np.array(J))
+    print(f"bruteforce_{tag}: J[:3]={np.array(J)[:3]}")
+
+
+def chol_inv_cases():
+    """Escalation / fallback / failure behaviour of utils.chol_inv (a2)."""
+    cases = {
+        "spd": np.array([[4.0, 1.0], [1.0, 3.0]]),
+        "psd_singular": np.array([[1.0, 1.0], [1.0, 1.0]]),
+        "indef_small": np.array([[1.0, 0.0], [0.0, -1e-8]]),   # needs escalation
+        "indef_big": np.array([[1.0, 0.0], [0.0, -5.0]]),      # LU fallback
+        "asym": np.array([[2.0, 0.5], [0.1, 1.0]]),            # _sym first
+    }
+    d = {}
+    for name, M in cases.items():
+        d[f"{name}_in"] = M
+        d[f"{name}_out"] = ref_utils.chol_inv(M)
+    np.savez_compressed(os.path.join(HERE, "chol_inv_cases.npz"), **d)
+    print("chol_inv_cases:", list(cases))
+
+
+def main():
+    np.seterr(all="ignore")
+    synthetic_lft("s13_m4_N100", 13, 4, 100, 1000, 4, 40, 100)
+    synthetic_lft("s5_m1_N200", 5, 1, 200, 2000, 4, 20, 200)
+    synthetic_lft("s3_m1_N50", 3, 1, 50, 3000, 4, 10, 50)
+    synthetic_lft("s13_m4_N128", 13, 4, 128, 4000, 2, 40, 128)
+    synthetic_lft("s16_m6_N40", 16, 6, 40, 5000, 2, 5, 40)
+    synthetic_lft_rlist("s7_m3_N30", 7, 3, 30, 6000)
+    real_capture("DI_N50", dict(N=50), ref_systems.make_double_integrator, T_min=10, T_max=50)
+    real_capture("Quad_N160", {}, ref_systems.make_quadrotor, max_iter=3)
+    riccati_synth("n12_m4_N100", 12, 4, 100, [7000, 7001], [100, 57], 1e-3)
+    riccati_shift("n6_m2_N60", 6, 2, 60, 7100, 45, 15, 1e-6)
+    riccati_fail("n4_m2_N20", 4, 2, 20, 7200)
+    bruteforce_synth("n4_m2_N40", 4, 2, 40, 7300, 40, 0.05)
+    chol_inv_cases()
+
+
+if __name__ == "__main__":
+    main()

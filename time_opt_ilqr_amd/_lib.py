@@ -1,0 +1,91 @@
+"""ctypes binding of libhop_amd.so (include/hop.h).
+
+The shared library is plain HIP (no torch types cross the boundary): callers
+hand over device pointers (``tensor.data_ptr()``) and the raw HIP stream
+(``torch.cuda.current_stream().cuda_stream``).  There is deliberately no CPU
+fallback: without the built library or a GPU every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("HOP_LIB", os.path.join(HERE, "libhop_amd.so"))
+
+ST_JITTER = 1
+ST_LU = 2
+ST_NONFINITE = 4
+ST_FAIL = 8
+MAX_DIM = 16
+
+_P = C.c_void_p
+_I32 = C.c_int32
+_I64 = C.c_int64
+_U32 = C.c_uint32
+
+# (name, restype, argtypes) -- must match include/hop.h exactly
+_LFT = [_P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _I64, _I64, _I32, _I32, _I32, _I32, _I32,
+        _I32, _I32, _P, _P, _P, _P, _P, _P, _P]
+_SEL = [_P, _I64, _I32, _I32, _I32, _P, _P, _P]
+_RIC64 = [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P,
+          C.c_double, _U32, _I32, _I32, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]
+_RIC32 = list(_RIC64)
+_RIC32[19] = C.c_float
+
+SIGNATURES = {
+    "hop_abi_version": (C.c_int, []),
+    "hop_last_error": (C.c_char_p, []),
+    "hop_lft_sweep_f64": (C.c_int, _LFT),
+    "hop_lft_sweep_f32": (C.c_int, _LFT),
+    "hop_select_horizon_f64": (C.c_int, _SEL),
+    "hop_select_horizon_f32": (C.c_int, _SEL),
+    "hop_riccati_f64": (C.c_int, _RIC64),
+    "hop_riccati_f32": (C.c_int, _RIC32),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class HopError(RuntimeError):
+    pass
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes handle; raises if the .so is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise HopError(f"{p} not built: run `python -m time_opt_ilqr_amd.build` "
+                           "(the HIP engine has no CPU fallback)")
+        lib = C.CDLL(p)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.hop_abi_version() != 1:
+            raise HopError("libhop_amd.so ABI mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().hop_last_error()
+        raise HopError(f"hop call failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    import torch
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,91 @@
+"""Build libhop_amd.so (gfx950) in-tree with hipcc; no torch extension machinery.
+
+    python -m time_opt_ilqr_amd.build        # or __graft_entry__.build()
+
+The .so is git-ignored but travels to the GPU box with the repo snapshot.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+REPO = os.path.dirname(HERE)
+LIB = os.path.join(HERE, "libhop_amd.so")
+SOURCES = ["capi.hip", "lft_sweep.hip", "riccati.hip"]
+HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc"]
+ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable",
+         "-Wno-unused-but-set-variable"]
+
+
+def _hipcc():
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.sep not in cand or os.path.exists(cand)):
+            return cand
+    raise RuntimeError("hipcc not found")
+
+
+def _digest():
+    h = hashlib.sha256()
+    for name in SOURCES + HEADERS:
+        with open(os.path.join(CSRC, name), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(REPO, "include", "hop.h"), "rb") as f:
+        h.update(f.read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()
+
+
+def _stamp_path():
+    return LIB + ".sha256"
+
+
+def up_to_date():
+    if not os.path.exists(LIB) or not os.path.exists(_stamp_path()):
+        return False
+    with open(_stamp_path()) as f:
+        return f.read().strip() == _digest()
+
+
+def build(force=False, jobs=None, verbose=True):
+    """Compile every .hip source for gfx950 and link libhop_amd.so."""
+    gen = os.path.join(REPO, "tools", "gen_dpp.py")
+    inc = os.path.join(CSRC, "dpp_blocks.inc")
+    if not os.path.exists(inc) and os.path.exists(gen):
+        subprocess.check_call([sys.executable, gen])
+    if not force and up_to_date():
+        if verbose:
+            print("[hop] libhop_amd.so up to date")
+        return LIB
+    hipcc = _hipcc()
+    objdir = os.path.join(HERE, "_obj")
+    os.makedirs(objdir, exist_ok=True)
+    procs = []
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src.replace(".hip", ".o"))
+        objs.append(obj)
+        cmd = [hipcc, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print("[hop]", " ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+    for p in procs:
+        if p.wait() != 0:
+            raise RuntimeError("hipcc failed")
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
+    if verbose:
+        print("[hop]", " ".join(cmd))
+    subprocess.check_call(cmd)
+    os.replace(tmp, LIB)
+    with open(_stamp_path(), "w") as f:
+        f.write(_digest())
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,189 @@
+// extern "C" boundary of libhop_amd.so (include/hop.h): argument validation,
+// kernel dispatch, the horizon argmin kernel.
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/hop.h"
+#include "hop_device.hpp"
+#include "hop_kernels.hpp"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
+int hip_status(hipError_t e) {
+  if (e == hipSuccess) return HOP_OK;
+  snprintf(g_err, sizeof(g_err), "HIP error %d: %s", (int)e, hipGetErrorString(e));
+  return HOP_E_HIP;
+}
+
+// first minimiser of J[t_min-1 .. t_max-1]; NaN wins (np.argmin semantics)
+template <class T>
+__global__ __launch_bounds__(256) void select_kernel(const T* __restrict__ J, long long batch,
+                                                     int ld, int t_min, int t_max,
+                                                     int* __restrict__ t_star,
+                                                     T* __restrict__ j_star) {
+  const long long b = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  const T* row = J + b * ld;
+  T best = row[t_min - 1];
+  int tb = t_min;
+#pragma unroll 1
+  for (int t = t_min + 1; t <= t_max; ++t) {
+    if (best != best) break;
+    const T v = row[t - 1];
+    if (v != v || v < best) {
+      best = v;
+      tb = t;
+    }
+  }
+  t_star[b] = tb;
+  if (j_star) j_star[b] = best;
+}
+
+template <class T>
+int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int64_t r_ks,
+              int32_t r_inv, const T* QT, const T* z0, int64_t z_bs, int64_t batch,
+              int32_t n_alloc, int32_t n_use, int32_t s, int32_t m, int32_t max_tries,
+              int32_t t_min, int32_t t_max, T* J, int32_t* status, int32_t* t_star, T* j_star,
+              T* dbg_efg, T* dbg_pre, void* stream) {
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (n_use <= 0 || batch == 0) return HOP_OK;  // reference: empty J
+  if (s < 1 || s > HOP_MAX_DIM) return fail(HOP_E_SIZE, "s must be in [1, 16]");
+  if (m < 1 || m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
+  if (n_use > n_alloc) return fail(HOP_E_ARG, "n_use > n_alloc (reference IndexError)");
+  if (!A || !B || !Q || !R || !QT || !z0 || !J || !status)
+    return fail(HOP_E_ARG, "null input/output pointer");
+  if (r_bs < 0 || r_ks < 0 || z_bs < 0) return fail(HOP_E_ARG, "negative stride");
+  if (max_tries < 0 || max_tries > 64) return fail(HOP_E_ARG, "max_tries out of range");
+  if (t_max > 0) {
+    if (t_min < 1 || t_min > t_max || t_max > n_use)
+      return fail(HOP_E_ARG, "need 1 <= t_min <= t_max <= n_use for the fused argmin");
+    if (!t_star || !j_star) return fail(HOP_E_ARG, "t_star/j_star required when t_max > 0");
+  }
+  hop::LftArgs<T> a;
+  a.A = A; a.B = B; a.Q = Q; a.R = R; a.QT = QT; a.z0 = z0;
+  a.r_bstride = r_bs; a.r_kstride = r_ks; a.z_bstride = z_bs;
+  a.batch = batch; a.nalloc = n_alloc; a.n = n_use; a.s = s; a.m = m;
+  a.max_tries = max_tries; a.r_is_inv = r_inv ? 1 : 0;
+  a.t_min = t_min; a.t_max = t_max;
+  a.J = J; a.status = status; a.t_star = t_star; a.j_star = j_star;
+  a.dbg_efg = dbg_efg; a.dbg_pre = dbg_pre;
+  return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));
+}
+
+template <class T>
+int select_entry(const T* J, int64_t batch, int32_t ld, int32_t t_min, int32_t t_max,
+                 int32_t* t_star, T* j_star, void* stream) {
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (batch == 0) return HOP_OK;
+  if (!J || !t_star) return fail(HOP_E_ARG, "null pointer");
+  if (t_min < 1 || t_min > t_max || t_max > ld)
+    return fail(HOP_E_ARG, "need 1 <= t_min <= t_max <= ld");
+  const long long blocks = (batch + 255) / 256;
+  hipLaunchKernelGGL(select_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     J, (long long)batch, ld, t_min, t_max, t_star, j_star);
+  return hip_status(hipGetLastError());
+}
+
+template <class T>
+int riccati_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, int64_t xg_bs,
+                  const T* u_ref, int64_t ur_bs, const T* Q, int64_t q_bs, const T* R,
+                  int64_t r_bs, const T* Qf, int64_t qf_bs, const T* qxx_extra,
+                  const T* qx_extra, const T* c_extra, const int32_t* horizon, const T* lm,
+                  T w_stage, uint32_t wrap_mask, int32_t mode, int32_t reg_max_tries,
+                  int64_t batch, int32_t n_alloc, int32_t n, int32_t m, T* K, T* k, T* Vxx,
+                  T* Vx, T* V0, int32_t* status, void* stream) {
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (batch == 0) return HOP_OK;
+  if (n < 1 || n > HOP_MAX_DIM) return fail(HOP_E_SIZE, "n must be in [1, 16]");
+  if (m < 1 || m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
+  if (n_alloc < 1) return fail(HOP_E_ARG, "n_alloc < 1");
+  if (mode != 0 && mode != 1) return fail(HOP_E_ARG, "mode must be 0 or 1");
+  if (reg_max_tries < 1) return fail(HOP_E_ARG, "reg_max_tries < 1");
+  if (!A || !Bm || !X || !U || !xg || !u_ref || !Q || !R || !Qf || !horizon || !lm || !K || !k ||
+      !status)
+    return fail(HOP_E_ARG, "null pointer");
+  hop::RiccatiArgs<T> a;
+  a.A = A; a.Bm = Bm; a.X = X; a.U = U; a.xg = xg; a.u_ref = u_ref; a.Q = Q; a.R = R; a.Qf = Qf;
+  a.qxx_extra = qxx_extra; a.qx_extra = qx_extra; a.c_extra = c_extra;
+  a.horizon = horizon; a.lm = lm;
+  a.xg_bstride = xg_bs; a.uref_bstride = ur_bs; a.q_bstride = q_bs; a.r_bstride = r_bs;
+  a.qf_bstride = qf_bs;
+  a.batch = batch; a.nalloc = n_alloc; a.n = n; a.m = m; a.mode = mode;
+  a.reg_max_tries = reg_max_tries; a.max_tries = 8; a.wrap_mask = wrap_mask; a.w_stage = w_stage;
+  a.K = K; a.k = k; a.Vxx = Vxx; a.Vx = Vx; a.V0 = V0; a.status = status;
+  return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
+}
+
+}  // namespace
+
+extern "C" {
+
+int hop_abi_version(void) { return HOP_ABI_VERSION; }
+const char* hop_last_error(void) { return g_err; }
+
+int hop_lft_sweep_f64(const double* A, const double* B, const double* Q, const double* R,
+                      int64_t r_bs, int64_t r_ks, int32_t r_inv, const double* QT,
+                      const double* z0, int64_t z_bs, int64_t batch, int32_t n_alloc,
+                      int32_t n_use, int32_t s, int32_t m, int32_t max_tries, int32_t t_min,
+                      int32_t t_max, double* J, int32_t* status, int32_t* t_star,
+                      double* j_star, double* dbg_efg, double* dbg_prefix, void* stream) {
+  return lft_entry<double>(A, B, Q, R, r_bs, r_ks, r_inv, QT, z0, z_bs, batch, n_alloc, n_use, s,
+                           m, max_tries, t_min, t_max, J, status, t_star, j_star, dbg_efg,
+                           dbg_prefix, stream);
+}
+int hop_lft_sweep_f32(const float* A, const float* B, const float* Q, const float* R,
+                      int64_t r_bs, int64_t r_ks, int32_t r_inv, const float* QT,
+                      const float* z0, int64_t z_bs, int64_t batch, int32_t n_alloc,
+                      int32_t n_use, int32_t s, int32_t m, int32_t max_tries, int32_t t_min,
+                      int32_t t_max, float* J, int32_t* status, int32_t* t_star, float* j_star,
+                      float* dbg_efg, float* dbg_prefix, void* stream) {
+  return lft_entry<float>(A, B, Q, R, r_bs, r_ks, r_inv, QT, z0, z_bs, batch, n_alloc, n_use, s,
+                          m, max_tries, t_min, t_max, J, status, t_star, j_star, dbg_efg,
+                          dbg_prefix, stream);
+}
+
+int hop_select_horizon_f64(const double* J, int64_t batch, int32_t ld, int32_t t_min,
+                           int32_t t_max, int32_t* t_star, double* j_star, void* stream) {
+  return select_entry<double>(J, batch, ld, t_min, t_max, t_star, j_star, stream);
+}
+int hop_select_horizon_f32(const float* J, int64_t batch, int32_t ld, int32_t t_min,
+                           int32_t t_max, int32_t* t_star, float* j_star, void* stream) {
+  return select_entry<float>(J, batch, ld, t_min, t_max, t_star, j_star, stream);
+}
+
+int hop_riccati_f64(const double* A, const double* Bm, const double* X, const double* U,
+                    const double* xg, int64_t xg_bs, const double* u_ref, int64_t ur_bs,
+                    const double* Q, int64_t q_bs, const double* R, int64_t r_bs,
+                    const double* Qf, int64_t qf_bs, const double* qxx_extra,
+                    const double* qx_extra, const double* c_extra, const int32_t* horizon,
+                    const double* lm, double w_stage, uint32_t wrap_mask, int32_t mode,
+                    int32_t reg_max_tries, int64_t batch, int32_t n_alloc, int32_t n, int32_t m,
+                    double* K, double* k, double* Vxx, double* Vx, double* V0, int32_t* status,
+                    void* stream) {
+  return riccati_entry<double>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
+                               qxx_extra, qx_extra, c_extra, horizon, lm, w_stage, wrap_mask,
+                               mode, reg_max_tries, batch, n_alloc, n, m, K, k, Vxx, Vx, V0,
+                               status, stream);
+}
+int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float* U,
+                    const float* xg, int64_t xg_bs, const float* u_ref, int64_t ur_bs,
+                    const float* Q, int64_t q_bs, const float* R, int64_t r_bs, const float* Qf,
+                    int64_t qf_bs, const float* qxx_extra, const float* qx_extra,
+                    const float* c_extra, const int32_t* horizon, const float* lm,
+                    float w_stage, uint32_t wrap_mask, int32_t mode, int32_t reg_max_tries,
+                    int64_t batch, int32_t n_alloc, int32_t n, int32_t m, float* K, float* k,
+                    float* Vxx, float* Vx, float* V0, int32_t* status, void* stream) {
+  return riccati_entry<float>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
+                              qxx_extra, qx_extra, c_extra, horizon, lm, w_stage, wrap_mask,
+                              mode, reg_max_tries, batch, n_alloc, n, m, K, k, Vxx, Vx, V0,
+                              status, stream);
+}
+
+}  // extern "C"

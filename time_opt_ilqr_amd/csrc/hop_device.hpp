@@ -1,0 +1,215 @@
+// Device primitives of the MI355X (gfx950) horizon-selection engine.
+//
+// Data layout ("row groups"): a wave64 holds FOUR independent problems, one per
+// 16-lane DPP row.  Inside a row, lane c holds column c of every small matrix
+// (register i = row i), so an S x S matrix costs S registers per lane.  A
+// product X*Y or X^T*Y is a sequence of one-instruction broadcast-FMAs
+// (v_fmac_f64_dpp ... row_newbcast:L, see dpp_blocks.inc): the broadcast lane
+// picks the contraction index, the register picks the output row.  No LDS
+// traffic and no MFMA padding waste (s = 13 runs 13 of 16 lanes, 13 registers).
+// LDS is used only for transposes / symmetrisation (one 16x17 tile per problem).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <utility>
+
+#include "dpp_blocks.inc"
+
+namespace hop {
+
+constexpr int kRowLanes = 16;     // lanes per problem
+constexpr int kProbPerWave = 4;   // problems per wave64
+constexpr int kWavesPerBlock = 4; // 256-thread workgroups
+constexpr int kProbPerBlock = kProbPerWave * kWavesPerBlock;
+constexpr int kLdsRow = 17;       // padded LDS row (elements)
+constexpr int kLdsTile = 272;     // 16*17; == 16 (mod 32) -> conflict-free b64 transposed reads
+
+// status bits (include/hop.h)
+constexpr unsigned ST_JITTER = 1u, ST_LU = 2u, ST_NONFINITE = 4u, ST_FAIL = 8u;
+
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+  }(std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class T, int S>
+__device__ __forceinline__ void zero(T (&x)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) x[i] = T(0);
+}
+template <class T, int S>
+__device__ __forceinline__ void copy(T (&d)[S], const T (&s)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) d[i] = s[i];
+}
+
+// out[i] (+/-)= sum_{j<K} X[i][j] * Y[j][c]   (X: lanes 0..K-1 hold its columns)
+template <bool NEG, class T, int S, int K>
+__device__ __forceinline__ void acc_xy(T (&out)[S], const T (&x)[S], const T (&y)[K]) {
+  static_for<K>([&](auto J) {
+    if constexpr (NEG) RowB<S>::template fma_neg<J>(out, x, y[J]);
+    else RowB<S>::template fma<J>(out, x, y[J]);
+  });
+}
+
+// out[i] (+/-)= sum_{j<K} X[j][i] * Y[j][c]   (X: lanes 0..S-1 hold its columns, K rows)
+template <bool NEG, class T, int S, int K>
+__device__ __forceinline__ void acc_xty(T (&out)[S], const T (&x)[K], const T (&y)[K]) {
+  static_for<K>([&](auto J) {
+    if constexpr (NEG) LaneB<S>::fma_neg(out, x[J], y[J]);
+    else LaneB<S>::fma(out, x[J], y[J]);
+  });
+}
+
+// ---------------------------------------------------------------------------
+// LDS transposes (per-problem tile, row stride 17)
+// ---------------------------------------------------------------------------
+template <class T, int S>
+__device__ __forceinline__ void lds_put(T* tile, int c, const T (&x)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) tile[i * kLdsRow + c] = x[i];
+}
+template <class T, int S>
+__device__ __forceinline__ void lds_get_t(const T* tile, int c, T (&x)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) x[i] = tile[c * kLdsRow + i];
+}
+// x <- 0.5 (x + x^T)  (bitwise symmetric, same rounding as NumPy's 0.5*(A+A.T))
+template <class T, int S>
+__device__ __forceinline__ void symmetrize(T (&x)[S], T* tile, int c) {
+  lds_put(tile, c, x);
+  wave_sync();
+  T t[S];
+  lds_get_t(tile, c, t);
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < S; ++i) x[i] = T(0.5) * (x[i] + t[i]);
+}
+template <class T, int S>
+__device__ __forceinline__ void transpose(T (&dst)[S], const T (&src)[S], T* tile, int c) {
+  lds_put(tile, c, src);
+  wave_sync();
+  lds_get_t(tile, c, dst);
+  wave_sync();
+}
+
+// Sum over the 16 lanes of a row (every lane of the row gets the total).
+template <class T>
+__device__ __forceinline__ T row_sum(T v) {
+  v += __shfl_xor(v, 8, 16);
+  v += __shfl_xor(v, 4, 16);
+  v += __shfl_xor(v, 2, 16);
+  v += __shfl_xor(v, 1, 16);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// SPD inverse with the reference's jitter semantics (utils.py:69-93):
+//   out = (sym(in) + eps I)^{-1}, eps = 1e-9, x10 per failed factorisation,
+//   up to max_tries, then one unguarded elimination (the LU-fallback slot).
+// Gauss-Jordan "sweep" on column-per-lane data: pivot p broadcasts column p
+// (lane p) and uses row p from the lane's own register p.  A pivot d <= 0 (or
+// NaN) is exactly the condition under which LAPACK's potrf rejects (its
+// pivots are the same Schur complements).  The caller passes a symmetric
+// matrix (symmetrize() first).
+// ---------------------------------------------------------------------------
+template <class T, int S>
+__device__ __forceinline__ void sweep_neg_inverse(T (&r)[S], T eps, int c, bool& ok) {
+  static_for<S>([&](auto P) {
+    constexpr int p = P;
+    const T d = bcast<p>(r[p]) + eps;
+    ok = ok && (d > T(0));
+    const T rd = T(1) / d;
+    const T t = r[p] + ((c == p) ? (eps - T(1)) : T(0));  // column p minus e_p
+    const T sc = -t * rd;
+    r[p] = t;
+    RowB<S>::template sweep<p>(r, sc);                     // r += t' (-(t'_c)/d)
+    r[p] = r[p] - ((c == p) ? T(1) : T(0));                // pivot -> -1/d
+  });
+}
+
+// In place: r <- (sym(r) + eps I)^{-1}.  The unsymmetrised input is parked in
+// the problem's LDS tile, so a retry (rare) re-forms sym(r) from LDS instead of
+// keeping a second register copy.  Rows that already succeeded redo the same
+// sweep with the same eps (bitwise identical), so no per-row select is needed.
+template <class T, int S>
+__device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int max_tries,
+                                                unsigned& st) {
+  lds_put(tile, c, r);
+  wave_sync();
+  {
+    T t[S];
+    lds_get_t(tile, c, t);
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = T(0.5) * (r[i] + t[i]);
+  }
+  T eps = T(1e-9);
+  int tries = 0;
+  bool done = false;
+#pragma unroll 1
+  while (true) {
+    bool ok = true;
+    sweep_neg_inverse(r, eps, c, ok);
+    const bool last = tries >= max_tries;
+    if (!done && !ok && last) st |= ST_LU;
+    done = ok || last;
+    if (!__any(!done)) break;
+    if (!done) {
+      eps *= T(10);
+      ++tries;
+      st |= ST_JITTER;
+    }
+    T t[S];
+    lds_get_t(tile, c, t);
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = T(0.5) * (tile[i * kLdsRow + c] + t[i]);
+  }
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < S; ++i) r[i] = -r[i];
+}
+
+// Same, without the LU slot (utils.py:96-120 chol_solve): returns false when
+// every jitter failed (the reference raises LinAlgError).  Input must already
+// be symmetric; it is parked in the LDS tile for retries.
+template <class T, int S>
+__device__ __forceinline__ bool spd_inverse_nofallback(T (&r)[S], T* tile, int c, int max_tries,
+                                                       unsigned& st) {
+  lds_put(tile, c, r);
+  wave_sync();
+  T eps = T(1e-9);
+  int tries = 0;
+  bool done = false, good = false;
+#pragma unroll 1
+  while (true) {
+    bool ok = true;
+    sweep_neg_inverse(r, eps, c, ok);
+    ++tries;
+    good = ok;
+    done = ok || (tries >= max_tries);
+    if (!__any(!done)) break;
+    if (!done) {
+      eps *= T(10);
+      st |= ST_JITTER;
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = tile[i * kLdsRow + c];
+  }
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < S; ++i) r[i] = -r[i];
+  return good;
+}
+
+__device__ __forceinline__ bool finite_val(double x) { return __builtin_isfinite(x); }
+__device__ __forceinline__ bool finite_val(float x) { return __builtin_isfinite(x); }
+
+}  // namespace hop

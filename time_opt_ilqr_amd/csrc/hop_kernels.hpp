@@ -1,0 +1,62 @@
+// Host-visible kernel argument blocks and dispatchers (internal to libhop_amd.so).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hop {
+
+template <class T>
+struct LftArgs {
+  const T* A;    // [B][nalloc][s][s]   augmented A_k
+  const T* B;    // [B][nalloc][s][m]   augmented B_k
+  const T* Q;    // [B][nalloc][s][s]   augmented Q_k
+  const T* R;    // R^-1 (r_is_inv) or R_k; batch/step strides in elements
+  const T* QT;   // [B][nalloc][s][s]   terminal blocks, QT[k] <-> horizon k+1
+  const T* z0;   // [B or 1][s]
+  long long r_bstride, r_kstride, z_bstride;
+  long long batch;
+  int nalloc, n, s, m, max_tries, r_is_inv;
+  int t_min, t_max;  // fused argmin window (t_max <= 0: off)
+  T* J;              // [B][n]
+  int* status;       // [B]
+  int* t_star;       // [B] or null
+  T* j_star;         // [B] or null
+  T* dbg_efg;        // [B][n][3][s][s] or null  (E_k, F_k, G_k)
+  T* dbg_pre;        // [B][n][3][s][s] or null  (Ebar_k, Fbar_k, Gbar_k)
+};
+
+template <class T>
+struct RiccatiArgs {
+  const T* A;      // [B][nalloc][n][n]
+  const T* Bm;     // [B][nalloc][n][m]
+  const T* X;      // [B][nalloc+1][n]
+  const T* U;      // [B][nalloc][m]
+  const T* xg;     // [B or 1][n]
+  const T* u_ref;  // [B or 1][m]
+  const T* Q;      // [B or 1][n][n]
+  const T* R;      // [B or 1][m][m]
+  const T* Qf;     // [B or 1][n][n]  (already as_terminal_weight'ed)
+  const T* qxx_extra;  // [B][nalloc][n][n] or null
+  const T* qx_extra;   // [B][nalloc][n] or null
+  const T* c_extra;    // [B][nalloc] or null
+  const int* horizon;  // [B]  L_b (terminal index)
+  const T* lm;         // [B]
+  long long xg_bstride, uref_bstride, q_bstride, r_bstride, qf_bstride;
+  long long batch;
+  int nalloc, n, m, mode, reg_max_tries, max_tries;
+  unsigned wrap_mask;
+  T w_stage;
+  T* K;    // [B][nalloc][m][n]
+  T* k;    // [B][nalloc][m]
+  T* Vxx;  // [B][nalloc+1][n][n] or null
+  T* Vx;   // [B][nalloc+1][n] or null
+  T* V0;   // [B][nalloc+1] or null
+  int* status;  // [B]
+};
+
+template <class T>
+hipError_t dispatch_lft(const LftArgs<T>& a, hipStream_t stream);
+template <class T>
+hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream);
+
+}  // namespace hop

@@ -1,0 +1,307 @@
+// Batched Riccati backward passes producing the feedback gains K_k, k_k and the
+// value expansion V_k, one problem per 16-lane row (hop_device.hpp layout).
+//   mode 0 = backward_pass_truncated        (solver.py:156-230)
+//   mode 1 = value_expansions_and_gains_prefix (horizon_selection.py:97-212)
+// Per step the Q-function assembly (Qx, Qu, Qxx, Quu, Qux), the regularised
+// Quu solve (jitter / LM escalation semantics of utils.chol_solve and the
+// reference loops) and the value update are fused; vectors live one entry per
+// lane, matrices one column per lane.  Each problem runs its own horizon
+// (horizon[b] = T* for mode 0, T_bar + S_right for mode 1).
+#include <math.h>
+
+#include "hop_device.hpp"
+#include "hop_kernels.hpp"
+
+namespace hop {
+
+template <class T>
+__device__ __forceinline__ T wrap_angle(T a) {
+  // NumPy: (a + pi) % (2 pi) - pi  (np.remainder: fmod, then shift into [0, 2pi))
+  const T two_pi = T(2.0 * 3.141592653589793);
+  const T pi = T(3.141592653589793);
+  T r = fmod(a + pi, two_pi);
+  if (r != T(0)) {
+    if (r < T(0)) r += two_pi;
+  } else {
+    r = T(0);
+  }
+  return r - pi;
+}
+
+template <class T, int S>
+__device__ __forceinline__ void rload_col(const T* M, int rows, int cols, int c, T pad, T (&x)[S]) {
+  // column c of a rows x cols row-major matrix, identity(pad)/zero padded
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const bool in = (i < rows) && (c < cols);
+    const T v = M[in ? i * cols + c : 0];
+    x[i] = in ? v : ((i == c) ? pad : T(0));
+  }
+}
+template <class T, int S>
+__device__ __forceinline__ void rload_row(const T* M, int rows, int cols, int c, T pad, T (&x)[S]) {
+  // row c of a rows x cols row-major matrix
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const bool in = (c < rows) && (j < cols);
+    const T v = M[in ? c * cols + j : 0];
+    x[j] = in ? v : ((j == c) ? pad : T(0));
+  }
+}
+
+template <class T, int S, int MM>
+__global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, c = lane & 15, g = lane >> 4, w = tid >> 6;
+  const long long prob = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave + g;
+  const bool valid = prob < a.batch;
+  const long long pb = valid ? prob : a.batch - 1;
+  T* tile = smem + (w * kProbPerWave + g) * kLdsTile;
+#pragma unroll 1
+  for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = T(0);
+  wave_sync();
+
+  const int n = a.n, m = a.m, NA = a.nalloc, mode = a.mode;
+  const long long nn = (long long)n * n, nm = (long long)n * m, mmx = (long long)m * m;
+  const T* Ap = a.A + pb * NA * nn;
+  const T* Bp = a.Bm + pb * NA * nm;
+  const T* Xp = a.X + pb * (NA + 1) * n;
+  const T* Up = a.U + pb * NA * m;
+  const T* xgp = a.xg + pb * a.xg_bstride;
+  const T* urp = a.u_ref + pb * a.uref_bstride;
+  const T* Qp = a.Q + pb * a.q_bstride;
+  const T* Rp = a.R + pb * a.r_bstride;
+  const T* Qfp = a.Qf + pb * a.qf_bstride;
+  const int L = valid ? a.horizon[pb] : 0;
+  int Lw = L;
+  Lw = max(Lw, __shfl_xor(Lw, 16));
+  Lw = max(Lw, __shfl_xor(Lw, 32));
+  Lw = __builtin_amdgcn_readfirstlane(Lw);
+  const T lam0 = a.lm[pb];
+
+  // loop-invariant cost blocks
+  T qcol[S], qrow[S];
+  rload_col(Qp, n, n, c, T(0), qcol);
+  rload_row(Qp, n, n, c, T(0), qrow);
+  T rcol[MM], rrow[MM];
+  rload_col(Rp, m, m, c, T(1), rcol);
+  rload_row(Rp, m, m, c, T(1), rrow);
+  const T xg_c = (c < n) ? xgp[c < n ? c : 0] : T(0);
+  const T ur_c = (c < m) ? urp[c < m ? c : 0] : T(0);
+  const bool wrap_c = (c < n) && ((a.wrap_mask >> c) & 1u);
+
+  unsigned st = 0;
+  bool alive = valid && L > 0 && L <= NA;
+  if (valid && !(L > 0 && L <= NA)) st |= ST_FAIL;
+
+  // terminal: Vxx = sym(Qf), Vx = Qf eT, V0 = 1/2 eT' Qf eT
+  T Vxx[S];
+  rload_col(Qfp, n, n, c, T(0), Vxx);
+  T vx, v0;
+  {
+    T qfrow[S];
+    rload_row(Qfp, n, n, c, T(0), qfrow);
+    const int iT = (L > 0 && L <= NA) ? L : 0;
+    T eT = (c < n) ? Xp[(long long)iT * n + (c < n ? c : 0)] - xg_c : T(0);
+    if (wrap_c) eT = wrap_angle(eT);
+    const bool fin = ((__ballot(!finite_val(eT)) >> (16 * g)) & 0xffffull) == 0ull;
+    if (!fin) {
+      st |= ST_NONFINITE | ST_FAIL;
+      alive = false;
+    }
+    vx = T(0);
+    LaneDot<S>::fma(vx, eT, qfrow);  // (Qf eT)[c]
+    v0 = T(0.5) * row_sum((c < n) ? eT * vx : T(0));
+    symmetrize(Vxx, tile, c);
+    if (alive) {
+      if (a.Vxx) {
+        T* o = a.Vxx + (pb * (NA + 1) + L) * nn;
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+          if (i < n && c < n) o[i * n + c] = Vxx[i];
+      }
+      if (a.Vx && c < n) a.Vx[pb * (NA + 1) * n + (long long)L * n + c] = vx;
+      if (a.V0 && c == 0) a.V0[pb * (NA + 1) + L] = v0;
+    }
+  }
+
+#pragma unroll 1
+  for (int i = Lw - 1; i >= 0; --i) {
+    const bool act = alive && (i < L);
+    if (!__any(act)) continue;
+    const T* Ai = Ap + (long long)i * nn;
+    const T* Bi = Bp + (long long)i * nm;
+    T acol[S], bcol[S];
+    rload_col(Ai, n, n, c, T(0), acol);
+    rload_col(Bi, n, m, c, T(0), bcol);  // lanes c < m: column c of B_i
+    T e = (c < n) ? Xp[(long long)i * n + (c < n ? c : 0)] - xg_c : T(0);
+    if (wrap_c) e = wrap_angle(e);
+    const T du = (c < m) ? Up[(long long)i * m + (c < m ? c : 0)] - ur_c : T(0);
+    const unsigned long long badm = __ballot(!(finite_val(e) && finite_val(du)));
+    const bool bad = ((badm >> (16 * g)) & 0xffffull) != 0ull;
+
+    // lx = Q e (+ cx), lu = R du, l0
+    T lx = T(0), lu = T(0);
+    LaneDot<S>::fma(lx, e, qrow);
+    LaneDot<MM>::fma(lu, du, rrow);
+    T l0 = T(0.5) * row_sum((c < n) ? e * lx : T(0)) + T(0.5) * row_sum((c < m) ? du * lu : T(0)) +
+           a.w_stage;
+    T qst[S];
+    copy(qst, qcol);
+    if (a.qx_extra) {
+      const T* xp = a.qx_extra + (pb * NA + i) * n;
+      lx += (c < n) ? xp[c < n ? c : 0] : T(0);
+    }
+    if (a.c_extra) l0 += a.c_extra[pb * NA + i];
+    if (a.qxx_extra) {
+      T ex[S];
+      rload_col(a.qxx_extra + (pb * NA + i) * nn, n, n, c, T(0), ex);
+#pragma unroll
+      for (int r = 0; r < S; ++r) qst[r] += ex[r];
+      symmetrize(qst, tile, c);
+    }
+
+    // Q-function assembly
+    T qx = lx, qu = lu;
+    LaneDot<S>::fma(qx, vx, acol);  // Qx = lx + A^T Vx
+    LaneDot<S>::fma(qu, vx, bcol);  // Qu = lu + B^T Vx   (lanes < m)
+    T VA[S];
+    zero(VA);
+    acc_xy<false>(VA, Vxx, acol);   // Vxx A
+    T VB[S];
+    zero(VB);
+    acc_xy<false>(VB, Vxx, bcol);   // Vxx B          (lanes < m)
+    T Qxx[S];
+    copy(Qxx, qst);
+    acc_xty<false>(Qxx, acol, VA);  // Qst + A^T Vxx A
+    T Quu[MM];
+    copy(Quu, rcol);
+    acc_xty<false, T, MM, S>(Quu, bcol, VB);  // R + B^T Vxx B   (lanes < m)
+    T Qux[MM];
+    zero(Qux);
+    acc_xty<false, T, MM, S>(Qux, bcol, VA);  // B^T Vxx A       (lanes < n)
+
+    // regularised solve: Quu_reg = sym(Quu) + lam I ; (Quu_reg + eps I)^-1
+    T QuuT[MM];
+    transpose(QuuT, Quu, tile, c);
+    T Qi[MM];
+    bool solved = false;
+    if (mode == 0) {
+#pragma unroll
+      for (int r = 0; r < MM; ++r) Qi[r] = T(0.5) * (Quu[r] + QuuT[r]) + ((c == r) ? lam0 : T(0));
+      // the reference first checks cholesky(Quu_reg) (no jitter), then solves with jitter
+      bool ok = true;
+      {
+        T tmp[MM];
+        copy(tmp, Qi);
+        sweep_neg_inverse(tmp, T(0), c, ok);
+      }
+      solved = spd_inverse_nofallback(Qi, tile, c, 8, st) && ok;
+    } else {
+      T lam = lam0 > T(1e-12) ? lam0 : T(1e-12);
+      int tries = 0;
+      bool done = false;
+#pragma unroll 1
+      while (true) {
+#pragma unroll
+        for (int r = 0; r < MM; ++r) Qi[r] = T(0.5) * (Quu[r] + QuuT[r]) + ((c == r) ? lam : T(0));
+        const bool okr = spd_inverse_nofallback(Qi, tile, c, 8, st);
+        ++tries;
+        solved = okr;
+        done = okr || tries >= a.reg_max_tries;
+        if (!__any(!done && act)) break;
+        if (!done) lam *= T(10);
+      }
+    }
+    const bool fail_row = act && (bad || !solved);
+
+    // gains
+    T K[MM];
+    zero(K);
+    acc_xy<true, T, MM, MM>(K, Qi, Qux);  // K = -Quu_reg^-1 Qux   (column c)
+    T kv = T(0);
+    LaneDot<MM>::fma_neg(kv, qu, Qi);     // k = -Quu_reg^-1 Qu    (lanes < m)
+
+    // value update
+    T Vn[S];
+    copy(Vn, Qxx);
+    T vxn = qx;
+    T v0n = v0;
+    if (mode == 0) {
+      LaneDot<MM>::fma(vxn, qu, K);        // + K^T Qu
+      LaneDot<MM>::fma(vxn, kv, Qux);      // + Qux^T k
+      T qk = T(0);
+      LaneDot<MM>::fma(qk, kv, QuuT);      // (Quu k)[c]
+      LaneDot<MM>::fma(vxn, qk, K);        // + K^T Quu k
+      acc_xty<false, T, S, MM>(Vn, K, Qux);  // + K^T Qux
+      acc_xty<false, T, S, MM>(Vn, Qux, K);  // + Qux^T K
+      T QK[MM];
+      zero(QK);
+      acc_xy<false, T, MM, MM>(QK, Quu, K);  // Quu K
+      acc_xty<false, T, S, MM>(Vn, K, QK);   // + K^T Quu K
+    } else {
+      acc_xty<false, T, S, MM>(Vn, Qux, K);  // Qxx - Qux^T Quu^-1 Qux
+      LaneDot<MM>::fma(vxn, kv, Qux);        // Qx - Qux^T Quu^-1 Qu
+      v0n = l0 + v0 + T(0.5) * row_sum((c < m) ? qu * kv : T(0));
+    }
+    symmetrize(Vn, tile, c);
+    bool vbad = !finite_val(vxn) || !finite_val(v0n);
+#pragma unroll
+    for (int r = 0; r < S; ++r) vbad = vbad || !finite_val(Vn[r]);
+    const unsigned long long vbm = __ballot(vbad && c < n);
+    const bool vfail = act && (((vbm >> (16 * g)) & 0xffffull) != 0ull);
+
+    const bool commit = act && !fail_row && !vfail;
+    if (act && (fail_row || vfail)) {
+      st |= ST_FAIL;
+      if (bad || vfail) st |= ST_NONFINITE;
+      alive = false;
+    }
+    if (commit) {
+#pragma unroll
+      for (int r = 0; r < S; ++r) Vxx[r] = Vn[r];
+      vx = vxn;
+      v0 = v0n;
+      T* Ko = a.K + (pb * NA + i) * (long long)m * n;
+#pragma unroll
+      for (int r = 0; r < MM; ++r)
+        if (r < m && c < n) Ko[r * n + c] = K[r];
+      if (c < m) a.k[(pb * NA + i) * m + c] = kv;
+      if (a.Vxx) {
+        T* o = a.Vxx + (pb * (NA + 1) + i) * nn;
+#pragma unroll
+        for (int r = 0; r < S; ++r)
+          if (r < n && c < n) o[r * n + c] = Vn[r];
+      }
+      if (a.Vx && c < n) a.Vx[pb * (NA + 1) * n + (long long)i * n + c] = vxn;
+      if (a.V0 && c == 0) a.V0[pb * (NA + 1) + i] = v0n;
+    }
+  }
+  if (valid && c == 0) a.status[prob] = (int)st;
+}
+
+template <class T, int S, int MM>
+hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
+  const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+  const size_t lds = (size_t)kProbPerBlock * kLdsTile * sizeof(T);
+  hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream, a);
+  return hipGetLastError();
+}
+
+template <class T>
+hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
+  if (a.m <= 4) {
+    if (a.n <= 4) return launch_riccati<T, 4, 4>(a, stream);
+    if (a.n <= 8) return launch_riccati<T, 8, 4>(a, stream);
+    if (a.n <= 12) return launch_riccati<T, 12, 4>(a, stream);
+    return launch_riccati<T, 16, 4>(a, stream);
+  }
+  return launch_riccati<T, 16, 16>(a, stream);
+}
+
+template hipError_t dispatch_riccati<double>(const RiccatiArgs<double>&, hipStream_t);
+template hipError_t dispatch_riccati<float>(const RiccatiArgs<float>&, hipStream_t);
+
+}  // namespace hop
