@@ -326,3 +326,31 @@ def test_real_DI_dropins(dev, golden_dir):
         list(d["bwd_A"]), list(d["bwd_B"]), d["bwd_X"], d["bwd_U"], d["xg"], d["u_ref"],
         d["Q"], d["R"], float(d["alpha"]), float(d["w"]), len(d["bf_J"]))
     assert _rel(bf, d["bf_J"]) <= RTOL64
+
+
+def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch):
+    """The exact-size fp64 kernel (LDS-DMA streamed, s=13/m=4) and the generic
+    kernel agree, including the jitter / LU retry paths and batch tails."""
+    from time_opt_ilqr_amd import engine
+    Bn, s, m, N = 37, 13, 4, 30
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(700, Bn, s, m, N)
+    Q = Q.copy()
+    Q[3, 5] = Q[3, 5] - np.eye(s) * (np.linalg.eigvalsh(Q[3, 5]).min() + 5e-7)  # jitter
+    Q[20, 7] = -np.eye(s)                                                    # LU slot
+    QT = QT.copy()
+    QT[36, 2] = QT[36, 2] - np.eye(s) * (np.linalg.eigvalsh(QT[36, 2]).min() + 5e-6)
+    args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
+    fast = engine.propagate(*args, t_min=5, t_max=30)
+    monkeypatch.setenv("HOP_FORCE_GENERIC", "1")
+    gen = engine.propagate(*args, t_min=5, t_max=30)
+    monkeypatch.delenv("HOP_FORCE_GENERIC")
+    st_f, st_g = fast.status.cpu().numpy(), gen.status.cpu().numpy()
+    assert st_f.tolist() == st_g.tolist()
+    assert st_f[3] & orc.ST_JITTER and st_f[20] & orc.ST_LU and st_f[36] & orc.ST_JITTER
+    ok = [i for i in range(Bn) if i not in (3, 20, 36)]
+    assert _elem_rel(fast.J.cpu().numpy()[ok], gen.J.cpu().numpy()[ok]) <= 1e-10
+    Jo, sto = orc.lft_sweep_batch(A, Bm, Q, Ri, z0[0], QT)
+    assert sto.tolist() == st_f.tolist()
+    assert _elem_rel(fast.J.cpu().numpy()[ok], Jo[ok]) <= RTOL64
+    assert _elem_rel(fast.J.cpu().numpy()[20], Jo[20]) <= 1e-6
+    assert fast.t_star.cpu().numpy()[ok].tolist() == gen.t_star.cpu().numpy()[ok].tolist()

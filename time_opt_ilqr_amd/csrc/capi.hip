@@ -1,6 +1,7 @@
 // extern "C" boundary of libhop_amd.so (include/hop.h): argument validation,
 // kernel dispatch, the horizon argmin kernel.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/hop.h"
@@ -74,6 +75,12 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
   a.t_min = t_min; a.t_max = t_max;
   a.J = J; a.status = status; a.t_star = t_star; a.j_star = j_star;
   a.dbg_efg = dbg_efg; a.dbg_pre = dbg_pre;
+  if constexpr (sizeof(T) == 8) {
+    if (!getenv("HOP_FORCE_GENERIC")) {
+      const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
+      if (e != hipErrorNotSupported) return hip_status(e);
+    }
+  }
   return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));
 }
 

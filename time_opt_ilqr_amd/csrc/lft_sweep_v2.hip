@@ -1,0 +1,379 @@
+// LFT horizon sweep, exact-size fp64 specialisation (s == S, m == MM) -- the
+// hot kernel for the Quadrotor shape (s = 13, m = 4).  Same algorithm and
+// outputs as lft_sweep.hip (horizon_selection.py:36-86), restructured for a
+// wave that is alone on its SIMD (B = 4096 -> 1024 waves = 1 per SIMD):
+//
+//  * inputs of step k+1 (Q, A, B, QT) stream into per-wave LDS images by
+//    LDS-DMA (buffer_load_dwordx4 ... lds, bounds-checked) while step k
+//    computes; no VGPRs are held for prefetch and no global-load latency is
+//    exposed.  Rows/columns of Q, QT, A^T and B come straight from the image,
+//    so the symmetrisation of inverse inputs and A^T cost no extra transposes.
+//  * the two input-only inverses of a step (E_k = Q_k^-1, QT_k^-1) run as one
+//    interleaved pivot sequence (their divide chains overlap).
+//  * every inverse is kept NEGATED (the sweep's native output, -M^-1) and the
+//    sign is folded into the consuming broadcast-FMAs (fma_neg).
+//  * pivot reciprocals use v_rcp_f64 + two Newton steps instead of IEEE div.
+#include "hop_device.hpp"
+#include "hop_kernels.hpp"
+
+namespace hop {
+namespace v2 {
+
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  return r;
+}
+
+// lanes whose row-local index equals P: bits P, P+16, P+32, P+48 (an SGPR constant)
+template <int P>
+__device__ __forceinline__ double sel_lane(double a, double b) {
+  constexpr unsigned long long mask = 0x0001000100010001ull << P;
+  const int2 x = __builtin_bit_cast(int2, a), y = __builtin_bit_cast(int2, b);
+  int2 r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.x) : "v"(x.x), "v"(y.x), "s"(mask));
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r.y) : "v"(x.y), "v"(y.y), "s"(mask));
+  return __builtin_bit_cast(double, r);
+}
+
+// One Gauss-Jordan sweep of a column-per-lane matrix with diagonal jitter eps:
+// r <- -(r + eps I)^-1, ok &= every pivot > 0.
+template <int S>
+__device__ __forceinline__ void sweep(double (&r)[S], double eps, bool& ok) {
+  static_for<S>([&](auto P) {
+    constexpr int p = P;
+    const double d = bcast<p>(r[p]) + eps;
+    ok = ok && (d > 0.0);
+    const double rd = rcp_nr(d);
+    const double t = sel_lane<p>(r[p], d - 1.0);  // column p minus e_p (lane p: d-1)
+    r[p] = t;
+    RowB<S>::template sweep<p>(r, -t * rd);
+    r[p] = sel_lane<p>(r[p], r[p] - 1.0);         // lane p: (d-1)/d - 1 = -1/d
+  });
+}
+
+// Two independent sweeps, pivots interleaved so their reciprocal chains overlap.
+template <int S>
+__device__ __forceinline__ void sweep2(double (&r)[S], double epsr, bool& okr, double (&q)[S],
+                                       double epsq, bool& okq) {
+  static_for<S>([&](auto P) {
+    constexpr int p = P;
+    const double d1 = bcast<p>(r[p]) + epsr;
+    const double d2 = bcast<p>(q[p]) + epsq;
+    okr = okr && (d1 > 0.0);
+    okq = okq && (d2 > 0.0);
+    const double rd1 = rcp_nr(d1);
+    const double rd2 = rcp_nr(d2);
+    const double t1 = sel_lane<p>(r[p], d1 - 1.0);
+    const double t2 = sel_lane<p>(q[p], d2 - 1.0);
+    r[p] = t1;
+    q[p] = t2;
+    RowB<S>::template sweep<p>(r, -t1 * rd1);
+    RowB<S>::template sweep<p>(q, -t2 * rd2);
+    r[p] = sel_lane<p>(r[p], r[p] - 1.0);
+    q[p] = sel_lane<p>(q[p], q[p] - 1.0);
+  });
+}
+
+// sym(M) from a row-major S x S image (LDS) or a padded tile
+template <int S, int LD>
+__device__ __forceinline__ void sym_from(const double* img, int c, double (&r)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) r[i] = 0.5 * (img[i * LD + c] + img[c * LD + i]);
+}
+
+// Retry ladder shared by all inverses (utils.py:69-93 semantics): rows that
+// failed re-form their input with eps x 10; after max_tries the last sweep is
+// kept (LU slot) and flagged.  Rows that already succeeded recompute bitwise
+// the same result.  Rare path: kept out of line of the main schedule.
+template <int S, int LD>
+__device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img, int c, bool ok0,
+                                           int max_tries, unsigned& st) {
+  double eps = ok0 ? 1e-9 : 1e-8;  // rows that succeeded keep their jitter
+  int tries = ok0 ? 0 : 1;
+  bool done = ok0;
+  if (!ok0) st |= ST_JITTER;
+#pragma unroll 1
+  while (true) {
+    sym_from<S, LD>(img, c, r);
+    bool ok = true;
+    sweep<S>(r, eps, ok);
+    const bool last = tries >= max_tries;
+    if (!done && !ok && last) st |= ST_LU;
+    done = done || ok || last;
+    if (!__any(!done)) break;
+    if (!done) {
+      eps *= 10.0;
+      ++tries;
+    }
+  }
+}
+
+// Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1
+template <int S, int LD>
+__device__ __forceinline__ void neg_inverse(double (&r)[S], const double* img, int c, int mt,
+                                            unsigned& st) {
+  sym_from<S, LD>(img, c, r);
+  bool ok = true;
+  sweep<S>(r, 1e-9, ok);
+  if (__any(!ok)) retry_inverse<S, LD>(r, img, c, ok, mt, st);
+}
+
+template <int S, int LD1, int LD2>
+__device__ __forceinline__ void neg_inverse2(double (&r)[S], const double* img1, double (&q)[S],
+                                             const double* img2, int c, int mt, unsigned& st) {
+  sym_from<S, LD1>(img1, c, r);
+  sym_from<S, LD2>(img2, c, q);
+  bool okr = true, okq = true;
+  sweep2<S>(r, 1e-9, okr, q, 1e-9, okq);
+  if (__any(!okr)) retry_inverse<S, LD1>(r, img1, c, okr, mt, st);
+  if (__any(!okq)) retry_inverse<S, LD2>(q, img2, c, okq, mt, st);
+}
+
+// Negated inverse of sym(x) for a register matrix: x is parked in the tile.
+template <int S>
+__device__ __forceinline__ void neg_inverse_reg(double (&r)[S], double* tile, int c, int mt,
+                                                unsigned& st) {
+  lds_put(tile, c, r);
+  wave_sync();
+  neg_inverse<S, kLdsRow>(r, tile, c, mt, st);
+  wave_sync();
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA streaming of one step's blocks into the wave's images
+// ---------------------------------------------------------------------------
+struct Rsrc {
+  __amdgpu_buffer_rsrc_t r;
+};
+
+__device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds,
+                                      unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+      : "memory");
+}
+
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int S, int MM>
+struct Geo {
+  static constexpr int SS = S * S;
+  static constexpr int CHM = (SS * 8 + 15) / 16;      // 16-B chunks per S x S block
+  static constexpr int IMGM = CHM * 16;               // bytes per problem image (16-aligned)
+  static constexpr int NJM = (kProbPerWave * CHM + 63) / 64;  // DMA instrs per block type
+  static constexpr int IMGM_W = NJM * 1024;           // bytes per wave image (DMA writes 1 KiB)
+  static constexpr int SM = S * MM;
+  static constexpr int CHB = (SM * 8 + 15) / 16;
+  static constexpr int IMGB = CHB * 16;
+  static constexpr int NJB = (kProbPerWave * CHB + 63) / 64;
+  static constexpr int IMGB_W = NJB * 1024;
+  static constexpr int TILE_W = kProbPerWave * kLdsTile * 8;
+  // per-wave layout: [Q][A][QT][B][tiles]
+  static constexpr int OFF_Q = 0, OFF_A = IMGM_W, OFF_QT = 2 * IMGM_W, OFF_B = 3 * IMGM_W;
+  static constexpr int OFF_T = 3 * IMGM_W + IMGB_W;
+  static constexpr int WAVE_BYTES = OFF_T + TILE_W;
+};
+
+template <int S, int MM>
+__global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a) {
+  using G = Geo<S, MM>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned char* wbase = smem_raw + w * G::WAVE_BYTES;
+  const unsigned wlds = (unsigned)(uintptr_t)wbase;  // LDS byte address (wave-uniform)
+  double* tile = reinterpret_cast<double*>(wbase + G::OFF_T) + g * kLdsTile;
+  const double* imQ = reinterpret_cast<const double*>(wbase + G::OFF_Q + g * G::IMGM);
+  const double* imA = reinterpret_cast<const double*>(wbase + G::OFF_A + g * G::IMGM);
+  const double* imT = reinterpret_cast<const double*>(wbase + G::OFF_QT + g * G::IMGM);
+  const double* imB = reinterpret_cast<const double*>(wbase + G::OFF_B + g * G::IMGB);
+#pragma unroll 1
+  for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = 0.0;
+
+  const long long wave_prob0 = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave;
+  const long long prob = wave_prob0 + g;
+  const bool valid = prob < a.batch;
+  const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;  // wave-uniform
+  const int N = a.n, mt = a.max_tries;
+  constexpr int SS = S * S, SM = S * MM;
+  const long long pstrM = (long long)a.nalloc * SS * 8;  // bytes per problem (Q/A/QT)
+  const long long pstrB = (long long)a.nalloc * SM * 8;
+
+  // buffer descriptors for the wave's 4 problems (bounds-checked: OOB -> 0)
+  auto mk = [&](const double* base, long long pstr) {
+    // +16: the last 16-B chunk of a block may read 8 bytes past it (never used)
+    const long long left = (a.batch - pb0) * pstr + 16;
+    const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rQ = mk(a.Q, pstrM), rA = mk(a.A, pstrM), rT = mk(a.QT, pstrM),
+                               rB = mk(a.B, pstrB);
+  // per-lane chunk offsets (static over steps)
+  unsigned voM[G::NJM], voB[G::NJB];
+#pragma unroll
+  for (int j = 0; j < G::NJM; ++j) {
+    const int q = 64 * j + lane;
+    const int p = q / G::CHM, r = q % G::CHM;
+    long long pe = wave_prob0 + p < a.batch ? wave_prob0 + p : a.batch - 1;
+    voM[j] = (q < kProbPerWave * G::CHM) ? (unsigned)((pe - pb0) * pstrM + r * 16) : 0x7FFFFFFFu;
+  }
+#pragma unroll
+  for (int j = 0; j < G::NJB; ++j) {
+    const int q = 64 * j + lane;
+    const int p = q / G::CHB, r = q % G::CHB;
+    long long pe = wave_prob0 + p < a.batch ? wave_prob0 + p : a.batch - 1;
+    voB[j] = (q < kProbPerWave * G::CHB) ? (unsigned)((pe - pb0) * pstrB + r * 16) : 0x7FFFFFFFu;
+  }
+  auto dma_stage = [&](int k) {  // Q, A, B of step k
+    const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
+#pragma unroll
+    for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rQ, wlds + G::OFF_Q + 1024 * j, soM);
+#pragma unroll
+    for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rA, wlds + G::OFF_A + 1024 * j, soM);
+#pragma unroll
+    for (int j = 0; j < G::NJB; ++j) dma16(voB[j], rB, wlds + G::OFF_B + 1024 * j, soB);
+  };
+  auto dma_query = [&](int k) {  // QT of step k
+    const unsigned soM = (unsigned)(k * SS * 8);
+#pragma unroll
+    for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rT, wlds + G::OFF_QT + 1024 * j, soM);
+  };
+
+  const long long pb = valid ? prob : a.batch - 1;
+  const double* zp = a.z0 + pb * a.z_bstride;
+  const double zc = (c < S) ? zp[c < S ? c : 0] : 0.0;
+  unsigned st = 0;
+  // R^-1 (cached, shared or per problem) as columns on lanes 0..MM-1
+  double rinv[MM];
+  {
+    const double* Rp = a.R + pb * a.r_bstride;
+#pragma unroll
+    for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
+  }
+
+  dma_stage(0);
+  dma_query(0);
+  double Eb[S], H[S], Gb[S];
+  double best = 0.0;
+  int tbest = 0;
+  const bool fuse_argmin = a.t_max > 0;
+
+#pragma unroll 1
+  for (int k = 0; k < N; ++k) {
+    dma_wait();
+    wave_sync();
+    // ---- stage: NE = -(Q_k)^-1 and NX = -(QT_k)^-1 together
+    double NE[S], NX[S];
+    neg_inverse2<S, S, S>(NE, imQ, NX, imT, c, mt, st);
+    double at[S], brow[MM];
+#pragma unroll
+    for (int j = 0; j < S; ++j) at[j] = imA[c * S + j];   // row c of A
+#pragma unroll
+    for (int j = 0; j < MM; ++j) brow[j] = imB[c * MM + j];
+    wave_sync();
+    if (k + 1 < N) {
+      dma_stage(k + 1);
+      dma_query(k + 1);
+    }
+    double F[S];
+    zero(F);
+    acc_xy<true>(F, NE, at);    // F = E A^T
+    double Gk[S];
+    zero(Gk);
+    acc_xty<false>(Gk, at, F);  // A F
+    double y[MM];
+    zero(y);
+    acc_xy<false, double, MM, MM>(y, rinv, brow);
+    acc_xty<false, double, S, MM>(Gk, brow, y);  // + B R^-1 B^T
+
+    if (k == 0) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) Eb[i] = -NE[i];
+      transpose(H, F, tile, c);
+      copy(Gb, Gk);
+    } else {
+      double NW[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) NW[i] = Gb[i] - NE[i];  // E_k + Gbar
+      neg_inverse_reg<S>(NW, tile, c, mt, st);           // NW = -W
+      double Z[S];
+      zero(Z);
+      acc_xy<true>(Z, NW, H);     // Z = W Fbar^T
+      acc_xty<true>(Eb, H, Z);    // Ebar -= Fbar W Fbar^T
+      zero(H);
+      acc_xty<false>(H, F, Z);    // H' = F^T W Fbar^T
+      zero(Z);
+      acc_xy<true>(Z, NW, F);     // W F
+      copy(Gb, Gk);
+      acc_xty<true>(Gb, F, Z);    // Gbar = G - F^T W F
+    }
+
+    // ---- query horizon t = k + 1
+#pragma unroll
+    for (int i = 0; i < S; ++i) NX[i] = Gb[i] - NX[i];   // QT^-1 + Gbar
+    neg_inverse_reg<S>(NX, tile, c, mt, st);             // NX = -Wt
+    double V[S];
+    zero(V);
+    acc_xy<true>(V, NX, H);      // Wt Fbar^T
+    copy(NX, Eb);
+    acc_xty<true>(NX, H, V);     // X0 = Ebar - Fbar Wt Fbar^T
+    neg_inverse_reg<S>(NX, tile, c, mt, st);             // NX = -P0
+    double u = 0.0;
+    LaneDot<S>::fma_neg(u, zc, NX);  // (z0^T P0)[c]
+    const double jk = 0.5 * row_sum((c < S) ? u * zc : 0.0);
+    if (!finite_val(jk)) st |= ST_NONFINITE;
+    if (valid && c == 0) a.J[prob * N + k] = jk;
+    if (fuse_argmin) {
+      const int t = k + 1;
+      if (t == a.t_min) {
+        best = jk;
+        tbest = t;
+      } else if (t > a.t_min && t <= a.t_max) {
+        const bool bnan = best != best, jnan = jk != jk;
+        if (!bnan && (jnan || jk < best)) {
+          best = jk;
+          tbest = t;
+        }
+      }
+    }
+  }
+  dma_wait();
+  if (valid && c == 0) {
+    a.status[prob] = (int)st;
+    if (fuse_argmin && a.t_star != nullptr) {
+      a.t_star[prob] = tbest;
+      a.j_star[prob] = best;
+    }
+  }
+}
+
+}  // namespace v2
+
+// exact-size fast path: returns hipErrorNotSupported when the shape has none
+hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
+  if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv) return hipErrorNotSupported;
+  auto go = [&](auto kern, int bytes) {
+    const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+    return hipGetLastError();
+  };
+  if (a.s == 13 && a.m == 4)
+    return go(v2::lft_sweep_v2_kernel<13, 4>, v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock);
+  return hipErrorNotSupported;
+}
+
+}  // namespace hop
