@@ -1,0 +1,146 @@
+"""CPU: the C ABI library loads and exports every symbol of include/hop.h;
+argument validation rejects bad calls before touching a device; host-side
+preparation (augmented builders, wrap, terminal weight, shard plan) matches the
+oracle; the product path refuses to run without a HIP device."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import hop_oracle as orc
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from time_opt_ilqr_amd import _lib, build
+    build.build(verbose=False)
+    return _lib.load()
+
+
+def _header_functions():
+    src = open(os.path.join(REPO, "include", "hop.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(hop_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_symbols_exported(lib):
+    names = _header_functions()
+    assert len(names) == 8
+    from time_opt_ilqr_amd import _lib
+    assert sorted(_lib.SIGNATURES) == names
+    for n in names:
+        assert hasattr(lib, n)
+    out = os.popen(f"nm -D {_lib.LIB_PATH}").read()
+    for n in names:
+        assert re.search(rf"\bT {n}\b", out), n
+    assert lib.hop_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object(lib):
+    from time_opt_ilqr_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_argument_validation_without_gpu(lib):
+    """Bad shapes are rejected on the host (no launch happens)."""
+    nul = None
+    rc = lib.hop_lft_sweep_f64(nul, nul, nul, nul, 0, 0, 1, nul, nul, 0, 4, 10, 10, 17, 4, 8,
+                               0, 0, nul, nul, nul, nul, nul, nul, nul)
+    assert rc == -2 and b"s must be" in lib.hop_last_error()
+    rc = lib.hop_lft_sweep_f64(nul, nul, nul, nul, 0, 0, 1, nul, nul, 0, 4, 10, 11, 13, 4, 8,
+                               0, 0, nul, nul, nul, nul, nul, nul, nul)
+    assert rc == -1 and b"n_use > n_alloc" in lib.hop_last_error()
+    # n_use <= 0 is the reference's empty result: accepted, nothing launched
+    assert lib.hop_lft_sweep_f64(nul, nul, nul, nul, 0, 0, 1, nul, nul, 0, 4, 10, 0, 13, 4, 8,
+                                 0, 0, nul, nul, nul, nul, nul, nul, nul) == 0
+    rc = lib.hop_select_horizon_f64(nul, 3, 10, 5, 11, nul, nul, nul)
+    assert rc == -1
+    rc = lib.hop_riccati_f64(*([nul] * 4), nul, 0, nul, 0, nul, 0, nul, 0, nul, 0, nul, nul, nul,
+                             nul, nul, 0.0, 0, 2, 12, 4, 10, 12, 4, *([nul] * 6), nul)
+    assert rc == -1 and b"mode" in lib.hop_last_error()
+
+
+def test_product_path_has_no_cpu_fallback():
+    import torch
+    from time_opt_ilqr_amd import HopError, engine
+    A = torch.zeros((1, 2, 3, 3), dtype=torch.float64)
+    with pytest.raises(HopError):
+        engine.propagate(A, torch.zeros((1, 2, 3, 1), dtype=torch.float64), A,
+                         torch.eye(1, dtype=torch.float64), torch.zeros(3, dtype=torch.float64), A)
+
+
+def test_augmented_builders_match_oracle():
+    from time_opt_ilqr_amd import augmented
+    rng = np.random.default_rng(0)
+    n, m, N = 4, 2, 6
+    A = [np.eye(n) + 0.1 * rng.standard_normal((n, n)) for _ in range(N)]
+    B = [0.1 * rng.standard_normal((n, m)) for _ in range(N)]
+    X = rng.standard_normal((N + 1, n))
+    U = rng.standard_normal((N, m))
+    xg = rng.standard_normal(n)
+    ur = rng.standard_normal(m)
+    Q = np.diag(rng.uniform(1, 2, n))
+    R = np.diag(rng.uniform(1, 2, m))
+
+    def F(x, u):
+        return 0.9 * x + 0.05 * np.concatenate([u, u])[:n]
+
+    Aa, Ba, Qa, Rl, z0, Ri = augmented.build_augmented_sequence_QR(F, A, B, X, U, xg, ur, Q, R,
+                                                                   0.03, wrap_idx=[2])
+    res = [F(X[k], U[k]) - X[k + 1] for k in range(N)]
+    oA, oB, oQ, oR, oz, oRi = orc.augment_stage(A, B, res, X, U, xg, ur, Q, R, 0.03, wrap_idx=[2])
+    assert np.allclose(np.array(Aa), oA, atol=1e-15) and np.allclose(np.array(Qa), oQ, atol=1e-15)
+    assert np.allclose(np.array(Ba), oB) and np.allclose(Ri, oRi) and np.array_equal(z0, oz)
+    QT = augmented.build_terminal_aug_list(X, xg, np.array([1.0, 2.0, 3.0, 4.0]), wrap_idx=[2])
+    oQT = orc.augment_terminal(X, xg, np.array([1.0, 2.0, 3.0, 4.0]), wrap_idx=[2])
+    assert np.allclose(np.array(QT), oQT, atol=1e-15)
+
+
+def test_wrap_and_terminal_weight():
+    from time_opt_ilqr_amd import utils
+    e = np.array([7.0, -7.0, 3.2, np.pi])
+    w = utils.wrap_error(e, [0, 1, 2, 3])
+    assert np.array_equal(w, orc.wrap_angles(e, [0, 1, 2, 3]))
+    for a in (2.0, np.array([1.0, 2.0]), np.array([[1.0, 0.5], [0.0, 1.0]])):
+        assert np.array_equal(utils.as_terminal_weight(a, 2), orc.terminal_weight(a, 2))
+    with pytest.raises(ValueError):
+        utils.as_terminal_weight(np.ones(3), 2)
+
+
+def test_wrap_mask():
+    from time_opt_ilqr_amd.engine import wrap_mask
+    assert wrap_mask([6, 7, 8], 12) == (1 << 6) | (1 << 7) | (1 << 8)
+    assert wrap_mask(None, 4) == 0
+    assert wrap_mask([-1], 4) == 8
+    with pytest.raises(IndexError):
+        wrap_mask([5], 4)
+
+
+def test_shard_bounds_cover_batch():
+    from time_opt_ilqr_amd.distributed import shard_bounds
+    for total in (0, 1, 7, 4096, 262144, 131071):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(total, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == total
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_dpp_blocks_generated_in_sync():
+    """csrc/dpp_blocks.inc is exactly what tools/gen_dpp.py produces."""
+    import subprocess
+    import sys
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "x.inc")
+        subprocess.check_call([sys.executable, os.path.join(REPO, "tools", "gen_dpp.py"), out],
+                              stdout=subprocess.DEVNULL)
+        want = open(out).read()
+    have = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    assert want == have

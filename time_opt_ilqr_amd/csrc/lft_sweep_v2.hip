@@ -13,18 +13,24 @@
 //  * every inverse is kept NEGATED (the sweep's native output, -M^-1) and the
 //    sign is folded into the consuming broadcast-FMAs (fma_neg).
 //  * pivot reciprocals use v_rcp_f64 + two Newton steps instead of IEEE div.
+#include <stdlib.h>
+
 #include "hop_device.hpp"
 #include "hop_kernels.hpp"
 
 namespace hop {
 namespace v2 {
 
+// v_rcp_f64 + NR Newton steps (NR = 1 checked against the IEEE-division
+// generic kernel at 1e-10 in tests)
+template <int NR>
 __device__ __forceinline__ double rcp_nr(double d) {
   double r = __builtin_amdgcn_rcp(d);
-  double e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
-  e = __builtin_fma(-d, r, 1.0);
-  r = __builtin_fma(r, e, r);
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const double e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+  }
   return r;
 }
 
@@ -39,42 +45,51 @@ __device__ __forceinline__ double sel_lane(double a, double b) {
   return __builtin_bit_cast(double, r);
 }
 
-// One Gauss-Jordan sweep of a column-per-lane matrix with diagonal jitter eps:
-// r <- -(r + eps I)^-1, ok &= every pivot > 0.
-template <int S>
-__device__ __forceinline__ void sweep(double (&r)[S], double eps, bool& ok) {
-  static_for<S>([&](auto P) {
-    constexpr int p = P;
-    const double d = bcast<p>(r[p]) + eps;
-    ok = ok && (d > 0.0);
-    const double rd = rcp_nr(d);
-    const double t = sel_lane<p>(r[p], d - 1.0);  // column p minus e_p (lane p: d-1)
+// Kernel variants (runtime-selectable for same-process A/B, HOP_LFT_VARIANT)
+struct Cfg1 {  // exec-masked pivot fix-ups, row p out of the block, 1 Newton step
+  static constexpr int PIV = 1, NR = 1;
+};
+struct Cfg0 {  // VALU-select pivot (column p minus e_p trick), 2 Newton steps
+  static constexpr int PIV = 0, NR = 2;
+};
+struct Cfg2 {  // VALU-select pivot, 1 Newton step
+  static constexpr int PIV = 0, NR = 1;
+};
+
+// One Gauss-Jordan pivot of a column-per-lane matrix (r <- sweep_p(r)),
+// d = M_pp + eps broadcast from lane p.  Result after all pivots: -(M+eps)^-1.
+template <class C, int S, int p>
+__device__ __forceinline__ void pivot(double (&r)[S], double eps, bool& ok) {
+  const double d = bcast<p>(r[p]) + eps;
+  ok = ok && (d > 0.0);
+  const double rd = rcp_nr<C::NR>(d);
+  if constexpr (C::PIV == 1) {
+    // lanes c != p: s = -M_pc/d, row p -> M_pc/d ; lane p: s = 1/d - 1, M_pp -> -1/d
+    constexpr unsigned long long mask = 0x0001000100010001ull << p;
+    double sc = -r[p] * rd;
+    r[p] = r[p] * rd;
+    PivB<S>::template pivot<p>(r, sc, rd - 1.0, -rd, mask);
+  } else {
+    // column p minus e_p: lane p broadcasts d-1; all rows in one block; fix lane p after
+    const double t = sel_lane<p>(r[p], d - 1.0);
     r[p] = t;
     RowB<S>::template sweep<p>(r, -t * rd);
-    r[p] = sel_lane<p>(r[p], r[p] - 1.0);         // lane p: (d-1)/d - 1 = -1/d
-  });
+    r[p] = sel_lane<p>(r[p], r[p] - 1.0);
+  }
+}
+
+template <class C, int S>
+__device__ __forceinline__ void sweep(double (&r)[S], double eps, bool& ok) {
+  static_for<S>([&](auto P) { pivot<C, S, P>(r, eps, ok); });
 }
 
 // Two independent sweeps, pivots interleaved so their reciprocal chains overlap.
-template <int S>
+template <class C, int S>
 __device__ __forceinline__ void sweep2(double (&r)[S], double epsr, bool& okr, double (&q)[S],
                                        double epsq, bool& okq) {
   static_for<S>([&](auto P) {
-    constexpr int p = P;
-    const double d1 = bcast<p>(r[p]) + epsr;
-    const double d2 = bcast<p>(q[p]) + epsq;
-    okr = okr && (d1 > 0.0);
-    okq = okq && (d2 > 0.0);
-    const double rd1 = rcp_nr(d1);
-    const double rd2 = rcp_nr(d2);
-    const double t1 = sel_lane<p>(r[p], d1 - 1.0);
-    const double t2 = sel_lane<p>(q[p], d2 - 1.0);
-    r[p] = t1;
-    q[p] = t2;
-    RowB<S>::template sweep<p>(r, -t1 * rd1);
-    RowB<S>::template sweep<p>(q, -t2 * rd2);
-    r[p] = sel_lane<p>(r[p], r[p] - 1.0);
-    q[p] = sel_lane<p>(q[p], q[p] - 1.0);
+    pivot<C, S, P>(r, epsr, okr);
+    pivot<C, S, P>(q, epsq, okq);
   });
 }
 
@@ -89,7 +104,7 @@ __device__ __forceinline__ void sym_from(const double* img, int c, double (&r)[S
 // failed re-form their input with eps x 10; after max_tries the last sweep is
 // kept (LU slot) and flagged.  Rows that already succeeded recompute bitwise
 // the same result.  Rare path: kept out of line of the main schedule.
-template <int S, int LD>
+template <class C, int S, int LD>
 __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img, int c, bool ok0,
                                            int max_tries, unsigned& st) {
   double eps = ok0 ? 1e-9 : 1e-8;  // rows that succeeded keep their jitter
@@ -100,7 +115,7 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
   while (true) {
     sym_from<S, LD>(img, c, r);
     bool ok = true;
-    sweep<S>(r, eps, ok);
+    sweep<C, S>(r, eps, ok);
     const bool last = tries >= max_tries;
     if (!done && !ok && last) st |= ST_LU;
     done = done || ok || last;
@@ -113,33 +128,33 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
 }
 
 // Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1
-template <int S, int LD>
+template <class C, int S, int LD>
 __device__ __forceinline__ void neg_inverse(double (&r)[S], const double* img, int c, int mt,
                                             unsigned& st) {
   sym_from<S, LD>(img, c, r);
   bool ok = true;
-  sweep<S>(r, 1e-9, ok);
-  if (__any(!ok)) retry_inverse<S, LD>(r, img, c, ok, mt, st);
+  sweep<C, S>(r, 1e-9, ok);
+  if (__any(!ok)) retry_inverse<C, S, LD>(r, img, c, ok, mt, st);
 }
 
-template <int S, int LD1, int LD2>
+template <class C, int S, int LD1, int LD2>
 __device__ __forceinline__ void neg_inverse2(double (&r)[S], const double* img1, double (&q)[S],
                                              const double* img2, int c, int mt, unsigned& st) {
   sym_from<S, LD1>(img1, c, r);
   sym_from<S, LD2>(img2, c, q);
   bool okr = true, okq = true;
-  sweep2<S>(r, 1e-9, okr, q, 1e-9, okq);
-  if (__any(!okr)) retry_inverse<S, LD1>(r, img1, c, okr, mt, st);
-  if (__any(!okq)) retry_inverse<S, LD2>(q, img2, c, okq, mt, st);
+  sweep2<C, S>(r, 1e-9, okr, q, 1e-9, okq);
+  if (__any(!okr)) retry_inverse<C, S, LD1>(r, img1, c, okr, mt, st);
+  if (__any(!okq)) retry_inverse<C, S, LD2>(q, img2, c, okq, mt, st);
 }
 
 // Negated inverse of sym(x) for a register matrix: x is parked in the tile.
-template <int S>
+template <class C, int S>
 __device__ __forceinline__ void neg_inverse_reg(double (&r)[S], double* tile, int c, int mt,
                                                 unsigned& st) {
   lds_put(tile, c, r);
   wave_sync();
-  neg_inverse<S, kLdsRow>(r, tile, c, mt, st);
+  neg_inverse<C, S, kLdsRow>(r, tile, c, mt, st);
   wave_sync();
 }
 
@@ -186,7 +201,7 @@ struct Geo {
   static constexpr int WAVE_BYTES = OFF_T + TILE_W;
 };
 
-template <int S, int MM>
+template <class C, int S, int MM>
 __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a) {
   using G = Geo<S, MM>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -272,13 +287,17 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   int tbest = 0;
   const bool fuse_argmin = a.t_max > 0;
 
+  double jprev = 0.0;
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
     dma_wait();
     wave_sync();
+    // J of the previous step is stored only now, so that the vmcnt(0) above
+    // never waits on a store issued at the end of the previous step
+    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
     // ---- stage: NE = -(Q_k)^-1 and NX = -(QT_k)^-1 together
     double NE[S], NX[S];
-    neg_inverse2<S, S, S>(NE, imQ, NX, imT, c, mt, st);
+    neg_inverse2<C, S, S, S>(NE, imQ, NX, imT, c, mt, st);
     double at[S], brow[MM];
 #pragma unroll
     for (int j = 0; j < S; ++j) at[j] = imA[c * S + j];   // row c of A
@@ -309,7 +328,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       double NW[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) NW[i] = Gb[i] - NE[i];  // E_k + Gbar
-      neg_inverse_reg<S>(NW, tile, c, mt, st);           // NW = -W
+      neg_inverse_reg<C, S>(NW, tile, c, mt, st);           // NW = -W
       double Z[S];
       zero(Z);
       acc_xy<true>(Z, NW, H);     // Z = W Fbar^T
@@ -325,18 +344,18 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     // ---- query horizon t = k + 1
 #pragma unroll
     for (int i = 0; i < S; ++i) NX[i] = Gb[i] - NX[i];   // QT^-1 + Gbar
-    neg_inverse_reg<S>(NX, tile, c, mt, st);             // NX = -Wt
+    neg_inverse_reg<C, S>(NX, tile, c, mt, st);             // NX = -Wt
     double V[S];
     zero(V);
     acc_xy<true>(V, NX, H);      // Wt Fbar^T
     copy(NX, Eb);
     acc_xty<true>(NX, H, V);     // X0 = Ebar - Fbar Wt Fbar^T
-    neg_inverse_reg<S>(NX, tile, c, mt, st);             // NX = -P0
+    neg_inverse_reg<C, S>(NX, tile, c, mt, st);             // NX = -P0
     double u = 0.0;
     LaneDot<S>::fma_neg(u, zc, NX);  // (z0^T P0)[c]
     const double jk = 0.5 * row_sum((c < S) ? u * zc : 0.0);
     if (!finite_val(jk)) st |= ST_NONFINITE;
-    if (valid && c == 0) a.J[prob * N + k] = jk;
+    jprev = jk;
     if (fuse_argmin) {
       const int t = k + 1;
       if (t == a.t_min) {
@@ -353,6 +372,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   }
   dma_wait();
   if (valid && c == 0) {
+    if (N > 0) a.J[prob * N + N - 1] = jprev;
     a.status[prob] = (int)st;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
@@ -371,8 +391,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
     return hipGetLastError();
   };
-  if (a.s == 13 && a.m == 4)
-    return go(v2::lft_sweep_v2_kernel<13, 4>, v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock);
+  const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
+  const int variant = ev ? atoi(ev) : 1;
+  if (a.s == 13 && a.m == 4) {
+    constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
+    if (variant == 0) return go(v2::lft_sweep_v2_kernel<v2::Cfg0, 13, 4>, bytes);
+    if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Cfg2, 13, 4>, bytes);
+    return go(v2::lft_sweep_v2_kernel<v2::Cfg1, 13, 4>, bytes);
+  }
   return hipErrorNotSupported;
 }
 

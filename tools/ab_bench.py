@@ -1,0 +1,64 @@
+"""Same-process interleaved A/B of LFT kernel variants (HOP_LFT_VARIANT / HOP_FORCE_GENERIC).
+
+    python tools/ab_bench.py --variants 0,1,2,g --rounds 7 --iters 10
+
+Rule: never rank builds by timings from different devices/processes
+(cdna_hip_programming.md 5.4 rule 24).  Prints median / min ms per launch.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=100)
+    args = ap.parse_args()
+    import torch
+    from time_opt_ilqr_amd import engine, synth
+    dev = torch.device("cuda", 0)
+    A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, 13, 4, args.N, seed=5, device=dev)
+    variants = args.variants.split(",")
+
+    def setv(v):
+        os.environ.pop("HOP_FORCE_GENERIC", None)
+        if v == "g":
+            os.environ["HOP_FORCE_GENERIC"] = "1"
+        else:
+            os.environ["HOP_LFT_VARIANT"] = v
+
+    ref = None
+    for v in variants:  # warm + cross-check
+        setv(v)
+        r = engine.propagate(A, Bm, Q, Ri, z0, QT)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = r.J.clone()
+        rel = float(((r.J - ref).abs() / ref.abs()).max())
+        print(f"variant {v}: max rel vs first = {rel:.3e}", flush=True)
+    times = {v: [] for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            setv(v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                engine.propagate(A, Bm, Q, Ri, z0, QT)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / args.iters)
+    out = {v: {"median_ms": statistics.median(t), "min_ms": min(t),
+               "sweeps_per_s": args.batch / (statistics.median(t) * 1e-3)} for v, t in times.items()}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
