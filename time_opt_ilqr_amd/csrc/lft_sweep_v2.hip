@@ -47,19 +47,33 @@ __device__ __forceinline__ double sel_lane(double a, double b) {
 
 // Kernel variants (runtime-selectable for same-process A/B, HOP_LFT_VARIANT)
 struct Cfg1 {  // exec-masked pivot fix-ups, row p out of the block, 1 Newton step
-  static constexpr int PIV = 1, NR = 1;
+  static constexpr int PIV = 1, NR = 1, LDSASM = 0;
 };
 struct Cfg0 {  // VALU-select pivot (column p minus e_p trick), 2 Newton steps
-  static constexpr int PIV = 0, NR = 2;
+  static constexpr int PIV = 0, NR = 2, LDSASM = 0;
 };
 struct Cfg2 {  // VALU-select pivot, 1 Newton step
-  static constexpr int PIV = 0, NR = 1;
+  static constexpr int PIV = 0, NR = 1, LDSASM = 0;
+};
+struct Cfg3 {  // Cfg2 + every LDS matrix read issued as one asm block (one lgkmcnt wait)
+  static constexpr int PIV = 0, NR = 1, LDSASM = 1;
+};
+struct Cfg4 {  // hand-scheduled asm sweep (pivot chains interleaved into the previous block)
+  static constexpr int PIV = 2, NR = 1, LDSASM = 1;
+};
+struct Cfg9 {  // TIMING ONLY (wrong results): pivot chain replaced by constants
+  static constexpr int PIV = 9, NR = 1, LDSASM = 1;
 };
 
 // One Gauss-Jordan pivot of a column-per-lane matrix (r <- sweep_p(r)),
 // d = M_pp + eps broadcast from lane p.  Result after all pivots: -(M+eps)^-1.
 template <class C, int S, int p>
 __device__ __forceinline__ void pivot(double (&r)[S], double eps, bool& ok) {
+  if constexpr (C::PIV == 9) {
+    // ablation: keep the broadcast block, drop the dependent reciprocal chain
+    RowB<S>::template sweep<p>(r, eps);
+    return;
+  }
   const double d = bcast<p>(r[p]) + eps;
   ok = ok && (d > 0.0);
   const double rd = rcp_nr<C::NR>(d);
@@ -80,24 +94,71 @@ __device__ __forceinline__ void pivot(double (&r)[S], double eps, bool& ok) {
 
 template <class C, int S>
 __device__ __forceinline__ void sweep(double (&r)[S], double eps, bool& ok) {
-  static_for<S>([&](auto P) { pivot<C, S, P>(r, eps, ok); });
+  if constexpr (C::PIV == 2) {
+    unsigned long long okm = ~0ull;
+    SweepAsm<S>::run(r, eps, okm);
+    ok = ok && ((okm >> __lane_id()) & 1ull);
+  } else {
+    static_for<S>([&](auto P) { pivot<C, S, P>(r, eps, ok); });
+  }
 }
 
 // Two independent sweeps, pivots interleaved so their reciprocal chains overlap.
 template <class C, int S>
 __device__ __forceinline__ void sweep2(double (&r)[S], double epsr, bool& okr, double (&q)[S],
                                        double epsq, bool& okq) {
+  if constexpr (C::PIV == 2) {
+    sweep<C, S>(r, epsr, okr);
+    sweep<C, S>(q, epsq, okq);
+    return;
+  }
   static_for<S>([&](auto P) {
     pivot<C, S, P>(r, epsr, okr);
     pivot<C, S, P>(q, epsq, okq);
   });
 }
 
-// sym(M) from a row-major S x S image (LDS) or a padded tile
+// Read column c and row c of a row-major LD-strided S x S LDS matrix with all
+// 2S ds_read_b64 in flight and a single lgkmcnt wait (hipcc, short of VGPRs,
+// otherwise interleaves ~10 read/wait round trips per matrix).
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)p;
+}
+
+template <int I, int S, int LD>
+struct LdsColRow {
+  static __device__ __forceinline__ void run(unsigned bc, unsigned br, double (&col)[S],
+                                             double (&row)[S]) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(col[I]) : "v"(bc), "i"(8 * LD * I));
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(row[I]) : "v"(br), "i"(8 * I));
+    if constexpr (I + 1 < S) LdsColRow<I + 1, S, LD>::run(bc, br, col, row);
+  }
+};
 template <int S, int LD>
+__device__ __forceinline__ void lds_col_row(const double* img, int c, double (&col)[S],
+                                            double (&row)[S]) {
+  const unsigned bc = lds_addr(img) + 8u * c;        // (i, c): + 8 LD i
+  const unsigned br = lds_addr(img) + 8u * LD * c;   // (c, i): + 8 i
+  LdsColRow<0, S, LD>::run(bc, br, col, row);
+}
+template <int S>
+__device__ __forceinline__ void lgkm_wait(double (&a)[S], double (&b)[S]) {
+  LgkmWait<S>::run(a, b);  // one s_waitcnt naming all 2S destinations
+}
+
+// sym(M) from a row-major S x S image (LDS) or a padded tile
+template <class C, int S, int LD>
 __device__ __forceinline__ void sym_from(const double* img, int c, double (&r)[S]) {
+  if constexpr (C::LDSASM) {
+    double t[S];
+    lds_col_row<S, LD>(img, c, r, t);
+    lgkm_wait(r, t);
 #pragma unroll
-  for (int i = 0; i < S; ++i) r[i] = 0.5 * (img[i * LD + c] + img[c * LD + i]);
+    for (int i = 0; i < S; ++i) r[i] = 0.5 * (r[i] + t[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = 0.5 * (img[i * LD + c] + img[c * LD + i]);
+  }
 }
 
 // Retry ladder shared by all inverses (utils.py:69-93 semantics): rows that
@@ -113,7 +174,7 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
   if (!ok0) st |= ST_JITTER;
 #pragma unroll 1
   while (true) {
-    sym_from<S, LD>(img, c, r);
+    sym_from<C, S, LD>(img, c, r);
     bool ok = true;
     sweep<C, S>(r, eps, ok);
     const bool last = tries >= max_tries;
@@ -131,7 +192,7 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
 template <class C, int S, int LD>
 __device__ __forceinline__ void neg_inverse(double (&r)[S], const double* img, int c, int mt,
                                             unsigned& st) {
-  sym_from<S, LD>(img, c, r);
+  sym_from<C, S, LD>(img, c, r);
   bool ok = true;
   sweep<C, S>(r, 1e-9, ok);
   if (__any(!ok)) retry_inverse<C, S, LD>(r, img, c, ok, mt, st);
@@ -140,8 +201,8 @@ __device__ __forceinline__ void neg_inverse(double (&r)[S], const double* img, i
 template <class C, int S, int LD1, int LD2>
 __device__ __forceinline__ void neg_inverse2(double (&r)[S], const double* img1, double (&q)[S],
                                              const double* img2, int c, int mt, unsigned& st) {
-  sym_from<S, LD1>(img1, c, r);
-  sym_from<S, LD2>(img2, c, q);
+  sym_from<C, S, LD1>(img1, c, r);
+  sym_from<C, S, LD2>(img2, c, q);
   bool okr = true, okq = true;
   sweep2<C, S>(r, 1e-9, okr, q, 1e-9, okq);
   if (__any(!okr)) retry_inverse<C, S, LD1>(r, img1, c, okr, mt, st);
@@ -392,11 +453,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return hipGetLastError();
   };
   const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
-  const int variant = ev ? atoi(ev) : 1;
+  const int variant = ev ? atoi(ev) : 2;
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
     if (variant == 0) return go(v2::lft_sweep_v2_kernel<v2::Cfg0, 13, 4>, bytes);
     if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Cfg2, 13, 4>, bytes);
+    if (variant == 3) return go(v2::lft_sweep_v2_kernel<v2::Cfg3, 13, 4>, bytes);
+    if (variant == 9) return go(v2::lft_sweep_v2_kernel<v2::Cfg9, 13, 4>, bytes);
+    if (variant == 4) return go(v2::lft_sweep_v2_kernel<v2::Cfg4, 13, 4>, bytes);
     return go(v2::lft_sweep_v2_kernel<v2::Cfg1, 13, 4>, bytes);
   }
   return hipErrorNotSupported;
