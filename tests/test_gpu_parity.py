@@ -328,10 +328,13 @@ def test_real_DI_dropins(dev, golden_dir):
     assert _rel(bf, d["bf_J"]) <= RTOL64
 
 
-def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch):
-    """The exact-size fp64 kernel (LDS-DMA streamed, s=13/m=4) and the generic
-    kernel agree, including the jitter / LU retry paths and batch tails."""
+@pytest.mark.parametrize("schedule", ["2", "8", "10"])
+def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch, schedule):
+    """Every schedule of the exact-size fp64 kernel (LDS-DMA streamed, s=13/m=4:
+    2 select pivots, 8 offset-form C++ chain, 10 hand-scheduled asm sweep) and
+    the generic kernel agree, including the jitter / LU retry paths and batch tails."""
     from time_opt_ilqr_amd import engine
+    monkeypatch.setenv("HOP_LFT_VARIANT", schedule)
     Bn, s, m, N = 37, 13, 4, 30
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(700, Bn, s, m, N)
     Q = Q.copy()

@@ -144,3 +144,48 @@ def test_dpp_blocks_generated_in_sync():
         want = open(out).read()
     have = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
     assert want == have
+
+
+@pytest.mark.parametrize("n", [2, 5, 13, 16])
+def test_hand_scheduled_blocks_emulated(n):
+    """The whole-sweep asm blocks (SweepQ / ElimQ in dpp_blocks.inc) compute the
+    offset-form negated inverse and the bordered quadratic form (CPU emulation
+    of the instruction strings, tools/emu_dpp.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(n)
+    M = rng.standard_normal((n, n))
+    M = M @ M.T + n * np.eye(n)
+    eps = 1e-9
+    regs = {}
+    for i in range(n):  # register i = row i, lane c = column c; diagonal offset by eps - 1
+        col = rng.standard_normal(16)
+        col[:n] = M[i]
+        col[i] += eps - 1.0
+        regs[i] = col
+    regs[n] = np.ones(16)
+    for j in range(7):
+        regs[n + 1 + j] = np.full(16, np.nan)
+    E.run(E.extract(inc, "SweepQ", n), regs)
+    got = np.array([regs[i][:n] for i in range(n)])
+    want = np.eye(n) - np.linalg.inv(M + eps * np.eye(n))
+    assert np.abs(got - want).max() < 1e-12
+    assert regs[n][0] > 0
+    if n == 16:
+        return  # the bordered form needs a free lane
+    z = rng.standard_normal(n)
+    regs = {}
+    for i in range(n):
+        col = rng.standard_normal(16)
+        col[:n] = M[i]
+        col[n] = z[i]
+        regs[i] = col
+    regs[n], regs[n + 1] = np.zeros(16), np.ones(16)
+    for j in range(8):
+        regs[n + 2 + j] = np.full(16, np.nan)
+    regs[n + 10] = np.full(16, eps)
+    E.run(E.extract(inc, "ElimQ", n), regs)
+    q = z @ np.linalg.solve(M + eps * np.eye(n), z)
+    assert abs(regs[n][n] - q) <= 1e-12 * abs(q)

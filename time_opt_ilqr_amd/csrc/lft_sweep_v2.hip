@@ -5,14 +5,27 @@
 //
 //  * inputs of step k+1 (Q, A, B, QT) stream into per-wave LDS images by
 //    LDS-DMA (buffer_load_dwordx4 ... lds, bounds-checked) while step k
-//    computes; no VGPRs are held for prefetch and no global-load latency is
-//    exposed.  Rows/columns of Q, QT, A^T and B come straight from the image,
-//    so the symmetrisation of inverse inputs and A^T cost no extra transposes.
-//  * the two input-only inverses of a step (E_k = Q_k^-1, QT_k^-1) run as one
-//    interleaved pivot sequence (their divide chains overlap).
+//    computes; no VGPRs are held for prefetch.  Rows/columns of Q, QT, A^T and
+//    B come straight from the image, so symmetrising inverse inputs and
+//    forming A^T cost no extra transposes.
 //  * every inverse is kept NEGATED (the sweep's native output, -M^-1) and the
 //    sign is folded into the consuming broadcast-FMAs (fma_neg).
-//  * pivot reciprocals use v_rcp_f64 + two Newton steps instead of IEEE div.
+//  * offset form (Chain / Sched schedules): diagonals carry -1 + eps, applied
+//    by one LDS atomic per lane on the parked input, so a Gauss-Jordan pivot
+//    needs no lane-p fix-ups; inverses come out as -M^-1 + I and the +I is
+//    absorbed by starting the consuming products from Y instead of 0.
+//  * the query of horizon t needs only z0^T (X0 + eps I)^-1 z0, answered by a
+//    bordered forward elimination with z0 as column S (lane S is free when
+//    s < 16) -- no third inverse.
+//  * Sched (default): each sweep is one hand-scheduled asm block in which the
+//    dependent chain of pivot p+1 (broadcast, v_rcp_f64, Newton-folded scale)
+//    is interleaved into the 13 broadcast-FMAs of pivot p.
+//
+// Schedules are runtime-selectable (HOP_LFT_VARIANT) for same-process A/B:
+//   2  Select : compiler-scheduled pivots with lane-p selects (first v2)
+//   8  Chain  : offset form, short C++ pivot chain, pad-free DPP blocks
+//   10 Sched  : offset form, whole-sweep asm blocks (default)
+//   20 Sched + per-section s_memtime stamps (diagnostic, tools/stamps.py)
 #include <stdlib.h>
 
 #include "hop_device.hpp"
@@ -45,77 +58,103 @@ __device__ __forceinline__ double sel_lane(double a, double b) {
   return __builtin_bit_cast(double, r);
 }
 
-// Kernel variants (runtime-selectable for same-process A/B, HOP_LFT_VARIANT)
-struct Cfg1 {  // exec-masked pivot fix-ups, row p out of the block, 1 Newton step
-  static constexpr int PIV = 1, NR = 1, LDSASM = 0;
+// Schedules.  PIV: 0 select pivots, 4 short C++ chain, 5 whole-sweep asm.
+struct Select {
+  static constexpr int PIV = 0, NR = 1, LDSASM = 0, ELIM = 0, STAMP = 0;
 };
-struct Cfg0 {  // VALU-select pivot (column p minus e_p trick), 2 Newton steps
-  static constexpr int PIV = 0, NR = 2, LDSASM = 0;
+struct Chain {
+  static constexpr int PIV = 4, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0;
 };
-struct Cfg2 {  // VALU-select pivot, 1 Newton step
-  static constexpr int PIV = 0, NR = 1, LDSASM = 0;
+struct Sched {
+  static constexpr int PIV = 5, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0;
 };
-struct Cfg3 {  // Cfg2 + every LDS matrix read issued as one asm block (one lgkmcnt wait)
-  static constexpr int PIV = 0, NR = 1, LDSASM = 1;
+struct SchedStamped : Sched {
+  static constexpr int STAMP = 1;
 };
-struct Cfg4 {  // hand-scheduled asm sweep (pivot chains interleaved into the previous block)
-  static constexpr int PIV = 2, NR = 1, LDSASM = 1;
-};
-struct Cfg9 {  // TIMING ONLY (wrong results): pivot chain replaced by constants
-  static constexpr int PIV = 9, NR = 1, LDSASM = 1;
-};
+template <class C>
+constexpr bool offset_form() {
+  return C::PIV == 4 || C::PIV == 5;
+}
 
-// One Gauss-Jordan pivot of a column-per-lane matrix (r <- sweep_p(r)),
+// One Gauss-Jordan pivot of a column-per-lane matrix (Select schedule),
 // d = M_pp + eps broadcast from lane p.  Result after all pivots: -(M+eps)^-1.
+// Column p minus e_p: lane p broadcasts d-1; all rows in one block; fix lane p after.
 template <class C, int S, int p>
 __device__ __forceinline__ void pivot(double (&r)[S], double eps, bool& ok) {
-  if constexpr (C::PIV == 9) {
-    // ablation: keep the broadcast block, drop the dependent reciprocal chain
-    RowB<S>::template sweep<p>(r, eps);
-    return;
-  }
   const double d = bcast<p>(r[p]) + eps;
   ok = ok && (d > 0.0);
   const double rd = rcp_nr<C::NR>(d);
-  if constexpr (C::PIV == 1) {
-    // lanes c != p: s = -M_pc/d, row p -> M_pc/d ; lane p: s = 1/d - 1, M_pp -> -1/d
-    constexpr unsigned long long mask = 0x0001000100010001ull << p;
-    double sc = -r[p] * rd;
-    r[p] = r[p] * rd;
-    PivB<S>::template pivot<p>(r, sc, rd - 1.0, -rd, mask);
-  } else {
-    // column p minus e_p: lane p broadcasts d-1; all rows in one block; fix lane p after
-    const double t = sel_lane<p>(r[p], d - 1.0);
-    r[p] = t;
-    RowB<S>::template sweep<p>(r, -t * rd);
-    r[p] = sel_lane<p>(r[p], r[p] - 1.0);
-  }
+  const double t = sel_lane<p>(r[p], d - 1.0);
+  r[p] = t;
+  RowB<S>::template sweep<p>(r, -t * rd);
+  r[p] = sel_lane<p>(r[p], r[p] - 1.0);
+}
+
+// Offset-form pivot with the shortest dependent chain (Chain schedule):
+//   d = 1 + bcast_p(r_p)       one DPP FMA (no v_mov_dpp + s_nop + v_add)
+//   rd0 = rcp(d); sc = sc0 + sc0 e with sc0 = -r_p rd0, e = 1 - d rd0 (one Newton
+//   step folded into the scale: rcp -> fma -> fma instead of rcp -> fma -> fma -> mul)
+//   pivot test: min(d) in a VGPR (no v_cmp -> s_and VCC round trip per pivot);
+//   NaN pivots are caught once per sweep (they turn every entry NaN).
+// The block writes r[p+1] first and carries no s_nop: its DPP sources were last
+// written by the previous block, the chain lies in between (checked at build).
+template <class C, int S, int p>
+__device__ __forceinline__ void pivot4(double (&r)[S], double& dmin) {
+  double d = 1.0;
+  fmac_bcast<p, p == 0>(d, r[p], 1.0);
+  const double rd0 = __builtin_amdgcn_rcp(d);
+  const double e = __builtin_fma(-d, rd0, 1.0);
+  const double sc0 = -r[p] * rd0;
+  dmin = __builtin_fmin(dmin, d);
+  const double sc = __builtin_fma(sc0, e, sc0);
+  if constexpr (p == 0) RowB<S>::template sweep<p>(r, sc);
+  else RowB<S>::template sweepq<p>(r, sc);
+}
+
+// every pivot > 0 and none NaN (a NaN pivot makes every entry NaN, lane 0 included)
+template <int S>
+__device__ __forceinline__ bool pivots_ok(const double (&r)[S], double dmin) {
+  const double x = bcast<0>(r[0]);
+  return (dmin > 0.0) && (x == x);
 }
 
 template <class C, int S>
 __device__ __forceinline__ void sweep(double (&r)[S], double eps, bool& ok) {
-  if constexpr (C::PIV == 2) {
-    unsigned long long okm = ~0ull;
-    SweepAsm<S>::run(r, eps, okm);
-    ok = ok && ((okm >> __lane_id()) & 1ull);
+  if constexpr (C::PIV == 5) {
+    double dmin = 1.0;
+    SweepQ<S>::run(r, dmin);
+    ok = ok && pivots_ok(r, dmin);
+  } else if constexpr (C::PIV == 4) {
+    double dmin = 1.0;
+    static_for<S>([&](auto P) { pivot4<C, S, P>(r, dmin); });
+    ok = ok && pivots_ok(r, dmin);
   } else {
     static_for<S>([&](auto P) { pivot<C, S, P>(r, eps, ok); });
   }
 }
 
-// Two independent sweeps, pivots interleaved so their reciprocal chains overlap.
+// Two independent sweeps; the C++ schedules interleave their pivots so the
+// reciprocal chains overlap (the asm sweep hides its own chain).
 template <class C, int S>
 __device__ __forceinline__ void sweep2(double (&r)[S], double epsr, bool& okr, double (&q)[S],
                                        double epsq, bool& okq) {
-  if constexpr (C::PIV == 2) {
+  if constexpr (C::PIV == 5) {
     sweep<C, S>(r, epsr, okr);
     sweep<C, S>(q, epsq, okq);
-    return;
+  } else if constexpr (C::PIV == 4) {
+    double dr = 1.0, dq = 1.0;
+    static_for<S>([&](auto P) {
+      pivot4<C, S, P>(r, dr);
+      pivot4<C, S, P>(q, dq);
+    });
+    okr = okr && pivots_ok(r, dr);
+    okq = okq && pivots_ok(q, dq);
+  } else {
+    static_for<S>([&](auto P) {
+      pivot<C, S, P>(r, epsr, okr);
+      pivot<C, S, P>(q, epsq, okq);
+    });
   }
-  static_for<S>([&](auto P) {
-    pivot<C, S, P>(r, epsr, okr);
-    pivot<C, S, P>(q, epsq, okq);
-  });
 }
 
 // Read column c and row c of a row-major LD-strided S x S LDS matrix with all
@@ -141,10 +180,6 @@ __device__ __forceinline__ void lds_col_row(const double* img, int c, double (&c
   const unsigned br = lds_addr(img) + 8u * LD * c;   // (c, i): + 8 i
   LdsColRow<0, S, LD>::run(bc, br, col, row);
 }
-template <int S>
-__device__ __forceinline__ void lgkm_wait(double (&a)[S], double (&b)[S]) {
-  LgkmWait<S>::run(a, b);  // one s_waitcnt naming all 2S destinations
-}
 
 // sym(M) from a row-major S x S image (LDS) or a padded tile
 template <class C, int S, int LD>
@@ -152,7 +187,7 @@ __device__ __forceinline__ void sym_from(const double* img, int c, double (&r)[S
   if constexpr (C::LDSASM) {
     double t[S];
     lds_col_row<S, LD>(img, c, r, t);
-    lgkm_wait(r, t);
+    LgkmWait<S>::run(r, t);  // one s_waitcnt naming all 2S destinations
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = 0.5 * (r[i] + t[i]);
   } else {
@@ -161,19 +196,34 @@ __device__ __forceinline__ void sym_from(const double* img, int c, double (&r)[S
   }
 }
 
+// m[c][c] += delta on lanes c < S of a row-major LDS matrix (one LDS atomic per
+// lane, no VALU): applies the (eps - 1) diagonal offset of the offset form.
+template <int S, int LD>
+__device__ __forceinline__ void diag_add(const double* img, int c, double delta) {
+  if (c < S) {
+    const unsigned a = lds_addr(img) + 8u * (LD + 1) * c;
+    asm volatile("ds_add_f64 %0, %1" ::"v"(a), "v"(delta) : "memory");
+  }
+}
+
 // Retry ladder shared by all inverses (utils.py:69-93 semantics): rows that
 // failed re-form their input with eps x 10; after max_tries the last sweep is
 // kept (LU slot) and flagged.  Rows that already succeeded recompute bitwise
-// the same result.  Rare path: kept out of line of the main schedule.
+// the same result.  Rare path.
 template <class C, int S, int LD>
 __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img, int c, bool ok0,
-                                           int max_tries, unsigned& st) {
+                                              int max_tries, unsigned& st) {
   double eps = ok0 ? 1e-9 : 1e-8;  // rows that succeeded keep their jitter
+  double cur = 1e-9;               // offset form: jitter currently in the LDS diagonal
   int tries = ok0 ? 0 : 1;
   bool done = ok0;
   if (!ok0) st |= ST_JITTER;
 #pragma unroll 1
   while (true) {
+    if constexpr (offset_form<C>()) {
+      diag_add<S, LD>(img, c, eps - cur);  // +0 for rows that keep their jitter
+      cur = eps;
+    }
     sym_from<C, S, LD>(img, c, r);
     bool ok = true;
     sweep<C, S>(r, eps, ok);
@@ -188,7 +238,87 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
   }
 }
 
-// Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1
+// Bordered forward elimination: r holds [M | b] column-per-lane (b on lane S,
+// which is free when s < 16).  Gaussian elimination without pivoting (its
+// pivots are the Cholesky squares, so d > 0 is the potrf test) leaves
+// b^T (M + eps I)^-1 b = sum_p b_p^2 / d_p, returned broadcast to the row.
+template <class C, int S>
+__device__ __forceinline__ double elim_quad(double (&r)[S], double eps, bool& ok) {
+  double acc = 0.0;
+  if constexpr (C::PIV == 5) {
+    double dmin = 1.0;
+    ElimQ<S>::run(r, acc, dmin, eps);
+    const double q = bcast<S>(acc);
+    ok = ok && (dmin > 0.0) && (q == q);
+    return q;
+  } else if constexpr (C::PIV == 4) {
+    double dmin = 1.0;
+    static_for<S>([&](auto P) {
+      constexpr int p = P;
+      double d = eps;
+      // block p-1 wrote S-p rows, r[p] first: fewer than 3 leave < 2 wait states
+      fmac_bcast<p, p == 0 || (S - p) <= 2>(d, r[p], 1.0);
+      const double rd0 = __builtin_amdgcn_rcp(d);
+      const double e = __builtin_fma(-d, rd0, 1.0);
+      const double sc0 = -r[p] * rd0;
+      dmin = __builtin_fmin(dmin, d);
+      const double sc = __builtin_fma(sc0, e, sc0);
+      acc = __builtin_fma(-r[p], sc, acc);
+      if constexpr (p == 0) TailB<S>::template elim<p>(r, sc);
+      else TailB<S>::template elimq<p>(r, sc);
+    });
+    const double q = bcast<S>(acc);
+    ok = ok && (dmin > 0.0) && (q == q);
+    return q;
+  } else {
+    static_for<S>([&](auto P) {
+      constexpr int p = P;
+      const double d = bcast<p>(r[p]) + eps;
+      ok = ok && (d > 0.0);
+      const double sc = -r[p] * rcp_nr<C::NR>(d);
+      acc = __builtin_fma(-r[p], sc, acc);
+      TailB<S>::template elim<p>(r, sc);
+    });
+    return bcast<S>(acc);
+  }
+}
+
+// z0^T (sym(X0) + eps I)^-1 z0 with the chol_inv retry ladder; X0 parked in the
+// tile whose row S holds z0 (so that sym() keeps lane S = z0).
+template <class C, int S>
+__device__ __forceinline__ double quad_inverse(double (&r)[S], double* tile, int c, int mt,
+                                               unsigned& st) {
+  lds_put(tile, c, r);
+  wave_sync();
+  sym_from<C, S, kLdsRow>(tile, c, r);
+  bool ok = true;
+  double q = elim_quad<C, S>(r, 1e-9, ok);
+  if (__any(!ok)) {
+    const bool ok0 = ok;
+    double eps = ok0 ? 1e-9 : 1e-8;
+    int tries = ok0 ? 0 : 1;
+    bool done = ok0;
+    if (!ok0) st |= ST_JITTER;
+#pragma unroll 1
+    while (true) {
+      sym_from<C, S, kLdsRow>(tile, c, r);
+      bool ok2 = true;
+      q = elim_quad<C, S>(r, eps, ok2);
+      const bool last = tries >= mt;
+      if (!done && !ok2 && last) st |= ST_LU;
+      done = done || ok2 || last;
+      if (!__any(!done)) break;
+      if (!done) {
+        eps *= 10.0;
+        ++tries;
+      }
+    }
+  }
+  wave_sync();
+  return q;
+}
+
+// Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1  (+ I in offset form)
 template <class C, int S, int LD>
 __device__ __forceinline__ void neg_inverse(double (&r)[S], const double* img, int c, int mt,
                                             unsigned& st) {
@@ -210,22 +340,61 @@ __device__ __forceinline__ void neg_inverse2(double (&r)[S], const double* img1,
 }
 
 // Negated inverse of sym(x) for a register matrix: x is parked in the tile.
+// Offset form: `off` is the diagonal offset already in r (-1 when r was formed
+// from offset-form inverses), so the tile diagonal gets eps - 1 - off.
 template <class C, int S>
 __device__ __forceinline__ void neg_inverse_reg(double (&r)[S], double* tile, int c, int mt,
-                                                unsigned& st) {
+                                                unsigned& st, double off = 0.0) {
   lds_put(tile, c, r);
+  if constexpr (offset_form<C>()) diag_add<S, kLdsRow>(tile, c, 1e-9 - 1.0 - off);
   wave_sync();
   neg_inverse<C, S, kLdsRow>(r, tile, c, mt, st);
   wave_sync();
 }
 
+// Products: with the pad-free schedules only the first broadcast block of a
+// product is padded (its source may have just been written); later blocks
+// read the same, unchanged source registers.
+template <class C, bool NEG, int S, int K>
+__device__ __forceinline__ void gxy(double (&out)[S], const double (&x)[S], const double (&y)[K]) {
+  if constexpr (offset_form<C>()) {
+    static_for<K>([&](auto J) {
+      if constexpr (J == 0) {
+        if constexpr (NEG) RowB<S>::template fma_neg<J>(out, x, y[J]);
+        else RowB<S>::template fma<J>(out, x, y[J]);
+      } else {
+        if constexpr (NEG) RowB<S>::template fma_negq<J>(out, x, y[J]);
+        else RowB<S>::template fmaq<J>(out, x, y[J]);
+      }
+    });
+  } else {
+    acc_xy<NEG>(out, x, y);
+  }
+}
+template <class C, bool NEG, int S, int K>
+__device__ __forceinline__ void gxty(double (&out)[S], const double (&x)[K], const double (&y)[K]) {
+  if constexpr (offset_form<C>()) {
+    static_for<K>([&](auto J) {
+      if constexpr (J == 0) {
+        if constexpr (NEG) LaneB<S>::fma_neg(out, x[J], y[J]);
+        else LaneB<S>::fma(out, x[J], y[J]);
+      } else {
+        if constexpr (NEG) LaneB<S>::fma_negq(out, x[J], y[J]);
+        else LaneB<S>::fmaq(out, x[J], y[J]);
+      }
+    });
+  } else {
+    acc_xty<NEG>(out, x, y);
+  }
+}
+
+// Diagnostic section stamps: per-wave shader-clock totals per section, summed
+// over waves into g_hop_stamp (read by hop_debug_stamps; slot 15 counts waves).
+__device__ unsigned long long g_hop_stamp[16];
+
 // ---------------------------------------------------------------------------
 // LDS-DMA streaming of one step's blocks into the wave's images
 // ---------------------------------------------------------------------------
-struct Rsrc {
-  __amdgpu_buffer_rsrc_t r;
-};
-
 __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds,
                                       unsigned soff) {
   unsigned keep;
@@ -265,6 +434,7 @@ struct Geo {
 template <class C, int S, int MM>
 __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a) {
   using G = Geo<S, MM>;
+  constexpr bool OFF = offset_form<C>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
@@ -314,7 +484,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     long long pe = wave_prob0 + p < a.batch ? wave_prob0 + p : a.batch - 1;
     voB[j] = (q < kProbPerWave * G::CHB) ? (unsigned)((pe - pb0) * pstrB + r * 16) : 0x7FFFFFFFu;
   }
-  auto dma_stage = [&](int k) {  // Q, A, B of step k
+  auto dma_step = [&](int k) {  // Q, A, B, QT of step k
     const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
 #pragma unroll
     for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rQ, wlds + G::OFF_Q + 1024 * j, soM);
@@ -322,16 +492,18 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rA, wlds + G::OFF_A + 1024 * j, soM);
 #pragma unroll
     for (int j = 0; j < G::NJB; ++j) dma16(voB[j], rB, wlds + G::OFF_B + 1024 * j, soB);
-  };
-  auto dma_query = [&](int k) {  // QT of step k
-    const unsigned soM = (unsigned)(k * SS * 8);
 #pragma unroll
     for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rT, wlds + G::OFF_QT + 1024 * j, soM);
   };
 
   const long long pb = valid ? prob : a.batch - 1;
   const double* zp = a.z0 + pb * a.z_bstride;
-  const double zc = (c < S) ? zp[c < S ? c : 0] : 0.0;
+  const double zc = (!C::ELIM && c < S) ? zp[c < S ? c : 0] : 0.0;
+  if constexpr (C::ELIM) {  // tile row S holds z0 (lane S of Ebar / X0, see quad_inverse)
+    static_assert(S < kRowLanes, "bordered elimination needs a free lane");
+    wave_sync();  // the zeroing loop wrote these words from other lanes
+    if (c < S) tile[S * kLdsRow + c] = zp[c];
+  }
   unsigned st = 0;
   // R^-1 (cached, shared or per problem) as columns on lanes 0..MM-1
   double rinv[MM];
@@ -341,80 +513,116 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
   }
 
-  dma_stage(0);
-  dma_query(0);
+  dma_step(0);
   double Eb[S], H[S], Gb[S];
   double best = 0.0;
   int tbest = 0;
   const bool fuse_argmin = a.t_max > 0;
 
   double jprev = 0.0;
+  unsigned long long sec[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = 0;
+  auto stamp = [&](int j) {
+    if constexpr (C::STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (j >= 0) sec[j] += t - tprev;
+      tprev = t;
+    }
+  };
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
+    stamp(-1);
     dma_wait();
     wave_sync();
     // J of the previous step is stored only now, so that the vmcnt(0) above
     // never waits on a store issued at the end of the previous step
     if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
+    if constexpr (OFF) {
+      diag_add<S, S>(imQ, c, 1e-9 - 1.0);
+      diag_add<S, S>(imT, c, 1e-9 - 1.0);
+    }
     // ---- stage: NE = -(Q_k)^-1 and NX = -(QT_k)^-1 together
     double NE[S], NX[S];
+    stamp(0);
     neg_inverse2<C, S, S, S>(NE, imQ, NX, imT, c, mt, st);
+    stamp(1);
     double at[S], brow[MM];
 #pragma unroll
     for (int j = 0; j < S; ++j) at[j] = imA[c * S + j];   // row c of A
 #pragma unroll
     for (int j = 0; j < MM; ++j) brow[j] = imB[c * MM + j];
     wave_sync();
-    if (k + 1 < N) {
-      dma_stage(k + 1);
-      dma_query(k + 1);
-    }
+    if (k + 1 < N) dma_step(k + 1);
+    stamp(2);
+    // offset form: NE, NX, NW carry +I; a product -(N + I) Y = (-N) Y - Y starts from Y
     double F[S];
-    zero(F);
-    acc_xy<true>(F, NE, at);    // F = E A^T
+    if constexpr (OFF) copy(F, at); else zero(F);
+    gxy<C, true>(F, NE, at);    // F = E A^T
     double Gk[S];
     zero(Gk);
-    acc_xty<false>(Gk, at, F);  // A F
+    gxty<C, false>(Gk, at, F);  // A F
     double y[MM];
     zero(y);
     acc_xy<false, double, MM, MM>(y, rinv, brow);
     acc_xty<false, double, S, MM>(Gk, brow, y);  // + B R^-1 B^T
+    stamp(3);
 
     if (k == 0) {
 #pragma unroll
       for (int i = 0; i < S; ++i) Eb[i] = -NE[i];
+      if constexpr (OFF) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) Eb[i] = (c == i) ? Eb[i] + 1.0 : Eb[i];
+      }
       transpose(H, F, tile, c);
+      if constexpr (C::ELIM) {  // lane S: Ebar column = z0, Fbar^T column = 0 (invariant)
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          Eb[i] = (c == S) ? tile[S * kLdsRow + i] : Eb[i];
+          H[i] = (c == S) ? 0.0 : H[i];
+        }
+      }
       copy(Gb, Gk);
     } else {
       double NW[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) NW[i] = Gb[i] - NE[i];  // E_k + Gbar
-      neg_inverse_reg<C, S>(NW, tile, c, mt, st);           // NW = -W
+      neg_inverse_reg<C, S>(NW, tile, c, mt, st, -1.0);     // NW = -W
+      stamp(4);
       double Z[S];
-      zero(Z);
-      acc_xy<true>(Z, NW, H);     // Z = W Fbar^T
-      acc_xty<true>(Eb, H, Z);    // Ebar -= Fbar W Fbar^T
+      if constexpr (OFF) copy(Z, H); else zero(Z);
+      gxy<C, true>(Z, NW, H);     // Z = W Fbar^T
+      gxty<C, true>(Eb, H, Z);    // Ebar -= Fbar W Fbar^T
       zero(H);
-      acc_xty<false>(H, F, Z);    // H' = F^T W Fbar^T
-      zero(Z);
-      acc_xy<true>(Z, NW, F);     // W F
+      gxty<C, false>(H, F, Z);    // H' = F^T W Fbar^T
+      if constexpr (OFF) copy(Z, F); else zero(Z);
+      gxy<C, true>(Z, NW, F);     // W F
       copy(Gb, Gk);
-      acc_xty<true>(Gb, F, Z);    // Gbar = G - F^T W F
+      gxty<C, true>(Gb, F, Z);    // Gbar = G - F^T W F
     }
+    stamp(5);
 
     // ---- query horizon t = k + 1
 #pragma unroll
     for (int i = 0; i < S; ++i) NX[i] = Gb[i] - NX[i];   // QT^-1 + Gbar
-    neg_inverse_reg<C, S>(NX, tile, c, mt, st);             // NX = -Wt
+    neg_inverse_reg<C, S>(NX, tile, c, mt, st, -1.0);       // NX = -Wt
+    stamp(6);
     double V[S];
-    zero(V);
-    acc_xy<true>(V, NX, H);      // Wt Fbar^T
+    if constexpr (OFF) copy(V, H); else zero(V);
+    gxy<C, true>(V, NX, H);      // Wt Fbar^T
     copy(NX, Eb);
-    acc_xty<true>(NX, H, V);     // X0 = Ebar - Fbar Wt Fbar^T
-    neg_inverse_reg<C, S>(NX, tile, c, mt, st);             // NX = -P0
-    double u = 0.0;
-    LaneDot<S>::fma_neg(u, zc, NX);  // (z0^T P0)[c]
-    const double jk = 0.5 * row_sum((c < S) ? u * zc : 0.0);
+    gxty<C, true>(NX, H, V);     // X0 = Ebar - Fbar Wt Fbar^T
+    stamp(7);
+    double jk;
+    if constexpr (C::ELIM) {
+      jk = 0.5 * quad_inverse<C, S>(NX, tile, c, mt, st);
+    } else {
+      neg_inverse_reg<C, S>(NX, tile, c, mt, st);             // NX = -P0
+      double u = 0.0;
+      LaneDot<S>::fma_neg(u, zc, NX);  // (z0^T P0)[c]
+      jk = 0.5 * row_sum((c < S) ? u * zc : 0.0);
+    }
+    stamp(8);
     if (!finite_val(jk)) st |= ST_NONFINITE;
     jprev = jk;
     if (fuse_argmin) {
@@ -432,6 +640,12 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     }
   }
   dma_wait();
+  if constexpr (C::STAMP) {
+    if (lane == 0) {
+      for (int j = 0; j < 10; ++j) atomicAdd(&g_hop_stamp[j], sec[j]);
+      atomicAdd(&g_hop_stamp[15], 1ull);
+    }
+  }
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = jprev;
     a.status[prob] = (int)st;
@@ -453,17 +667,28 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return hipGetLastError();
   };
   const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
-  const int variant = ev ? atoi(ev) : 2;
+  const int variant = ev ? atoi(ev) : 10;
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
-    if (variant == 0) return go(v2::lft_sweep_v2_kernel<v2::Cfg0, 13, 4>, bytes);
-    if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Cfg2, 13, 4>, bytes);
-    if (variant == 3) return go(v2::lft_sweep_v2_kernel<v2::Cfg3, 13, 4>, bytes);
-    if (variant == 9) return go(v2::lft_sweep_v2_kernel<v2::Cfg9, 13, 4>, bytes);
-    if (variant == 4) return go(v2::lft_sweep_v2_kernel<v2::Cfg4, 13, 4>, bytes);
-    return go(v2::lft_sweep_v2_kernel<v2::Cfg1, 13, 4>, bytes);
+    if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes);
+    if (variant == 8) return go(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes);
+    if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
+    return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
   }
   return hipErrorNotSupported;
 }
 
 }  // namespace hop
+
+// Diagnostic (not part of include/hop.h): read (and optionally reset) the
+// section stamps of the stamped variant (HOP_LFT_VARIANT=20).
+extern "C" int hop_debug_stamps(unsigned long long* host16, int reset) {
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(hop::v2::g_hop_stamp),
+                          16 * sizeof(unsigned long long)) != hipSuccess)
+    return -3;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hop::v2::g_hop_stamp), z, sizeof(z)) != hipSuccess) return -3;
+  }
+  return 0;
+}

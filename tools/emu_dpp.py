@@ -1,0 +1,65 @@
+"""Tiny CPU emulator for the generated DPP asm blocks (one 16-lane row, fp64).
+
+Executes the instruction strings of a dpp_blocks.inc asm statement with the
+operand map of its C++ wrapper, so the hand-scheduled blocks (SweepQ, ElimQ)
+can be checked against numpy on the CPU.  Supported: v_mov_b64,
+v_fmac_f64_dpp (row_newbcast), v_fma_f64, v_mul_f64, v_min_f64, v_rcp_f64,
+s_nop.  Hazards are not modelled (tools/check_dpp_hazards.py covers them).
+"""
+import re
+
+import numpy as np
+
+LANES = 16
+
+
+def _val(tok, regs):
+    neg = tok.startswith("-")
+    t = tok[1:] if neg else tok
+    if t.startswith("%"):
+        v = regs[int(t[1:])].copy()
+    else:
+        v = np.full(LANES, float(t))
+    return -v if neg else v
+
+
+def run(asm_lines, regs):
+    """regs: dict operand index -> np.array(16) (modified in place)."""
+    for line in asm_lines:
+        line = line.split(" row_mask")[0].strip()
+        if not line or line.startswith("s_nop"):
+            continue
+        op, rest = line.split(None, 1)
+        bc = None
+        m = re.search(r"row_newbcast:(\d+)", rest)
+        if m:
+            bc = int(m.group(1))
+            rest = rest[:m.start()].strip()
+        args = [a.strip() for a in rest.split(",")]
+        dst = int(args[0][1:])
+        if op == "v_mov_b64":
+            regs[dst] = _val(args[1], regs)
+        elif op == "v_fmac_f64_dpp":
+            x = _val(args[1], regs)
+            if bc is not None:
+                x = np.full(LANES, x[bc])
+            regs[dst] = regs[dst] + x * _val(args[2], regs)
+        elif op == "v_fma_f64":
+            regs[dst] = _val(args[1], regs) * _val(args[2], regs) + _val(args[3], regs)
+        elif op == "v_mul_f64":
+            regs[dst] = _val(args[1], regs) * _val(args[2], regs)
+        elif op == "v_min_f64":
+            regs[dst] = np.fmin(_val(args[1], regs), _val(args[2], regs))
+        elif op == "v_rcp_f64":
+            regs[dst] = 1.0 / _val(args[1], regs)
+        else:
+            raise ValueError(f"unsupported: {line}")
+    return regs
+
+
+def extract(inc_text, struct, n):
+    """Instruction strings of `struct<n>`'s asm statement in dpp_blocks.inc."""
+    i = inc_text.index(f"template <> struct {struct}<{n}> {{")
+    j = inc_text.index("    : ", i)
+    body = inc_text[inc_text.index("asm volatile(", i):j]
+    return [s.replace("\\n", "") for s in re.findall(r'^"(.*)"$', body, flags=re.M)]

@@ -1,0 +1,50 @@
+"""Per-section cycle breakdown of the LFT kernel (diagnostic variant 20 = Sched + stamps).
+
+    python tools/stamps.py [--batch 4096] [--N 100]
+
+Prints shader-clock cycles per wave per step for each section of the step.
+Stamps perturb the schedule (each s_memtime waits on lgkmcnt): read them as a
+breakdown, not as the kernel's speed.
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+NAMES = ["top wait + J store + diag offsets", "E/Xt paired inverses", "A/B reads + DMA issue",
+         "F, G products", "W inverse", "compose products", "Wt inverse", "V, X0 products",
+         "bordered elimination", "-"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--variant", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    from time_opt_ilqr_amd import _lib, engine, synth
+    lib = _lib.load()
+    lib.hop_debug_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    dev = torch.device("cuda", 0)
+    A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, 13, 4, args.N, seed=5, device=dev)
+    os.environ["HOP_LFT_VARIANT"] = str(args.variant)
+    buf = (C.c_ulonglong * 16)()
+    engine.propagate(A, Bm, Q, Ri, z0, QT)
+    torch.cuda.synchronize()
+    lib.hop_debug_stamps(buf, 1)
+    engine.propagate(A, Bm, Q, Ri, z0, QT)
+    torch.cuda.synchronize()
+    lib.hop_debug_stamps(buf, 1)
+    waves = buf[15]
+    tot = 0.0
+    for j in range(9):
+        cyc = buf[j] / waves / args.N
+        tot += cyc
+        print(f"{j} {NAMES[j]:36s} {cyc:9.1f} cycles/wave/step")
+    print(f"  total {tot:9.1f} cycles/wave/step  (waves {waves})")
+
+
+if __name__ == "__main__":
+    main()
