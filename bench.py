@@ -177,7 +177,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_F64_TFLOPS,
                          "traffic": traffic,
-                         "kernel": "lft_sweep_v2_kernel<Sched,13,4>", "kernel_ms": kern_ms,
+                         "kernel": "lft_sweep_v2_kernel<SchedRow,13,4>", "kernel_ms": kern_ms,
                          "flops_per_sweep": lft_flops(N, s, m),
                          "alg_bytes_per_sweep": lft_bytes(N, s, m, 8 if dtype == torch.float64 else 4)},
             "cpu_baseline": cpu,

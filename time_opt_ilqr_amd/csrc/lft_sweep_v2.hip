@@ -17,15 +17,17 @@
 //  * the query of horizon t needs only z0^T (X0 + eps I)^-1 z0, answered by a
 //    bordered forward elimination with z0 as column S (lane S is free when
 //    s < 16) -- no third inverse.
-//  * Sched (default): each sweep is one hand-scheduled asm block in which the
+//  * Sched / SchedRow: each sweep is one hand-scheduled asm block in which the
 //    dependent chain of pivot p+1 (broadcast, v_rcp_f64, Newton-folded scale)
 //    is interleaved into the 13 broadcast-FMAs of pivot p.
 //
 // Schedules are runtime-selectable (HOP_LFT_VARIANT) for same-process A/B:
 //   2  Select : compiler-scheduled pivots with lane-p selects (first v2)
 //   8  Chain  : offset form, short C++ pivot chain, pad-free DPP blocks
-//   10 Sched  : offset form, whole-sweep asm blocks (default)
-//   20 Sched + per-section s_memtime stamps (diagnostic, tools/stamps.py)
+//   10 Sched  : offset form, whole-sweep asm blocks
+//   12 SchedRow: Sched + X*Y products as one dependent DPP chain per output
+//      row (accumulator forwarded: 4.0 vs 4.9 cycles per FMA)   (default)
+//   20 SchedRow + per-section s_memtime stamps (diagnostic, tools/stamps.py)
 #include <stdlib.h>
 
 #include "hop_device.hpp"
@@ -60,15 +62,19 @@ __device__ __forceinline__ double sel_lane(double a, double b) {
 
 // Schedules.  PIV: 0 select pivots, 4 short C++ chain, 5 whole-sweep asm.
 struct Select {
-  static constexpr int PIV = 0, NR = 1, LDSASM = 0, ELIM = 0, STAMP = 0;
+  static constexpr int PIV = 0, NR = 1, LDSASM = 0, ELIM = 0, STAMP = 0, XYROW = 0;
 };
 struct Chain {
-  static constexpr int PIV = 4, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0;
+  static constexpr int PIV = 4, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0, XYROW = 0;
 };
 struct Sched {
-  static constexpr int PIV = 5, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0;
+  static constexpr int PIV = 5, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0, XYROW = 0;
 };
-struct SchedStamped : Sched {
+struct SchedRow : Sched {  // X*Y products as one dependent chain per output row
+  static constexpr int XYROW = 1;
+};
+
+struct SchedStamped : SchedRow {
   static constexpr int STAMP = 1;
 };
 template <class C>
@@ -159,26 +165,19 @@ __device__ __forceinline__ void sweep2(double (&r)[S], double epsr, bool& okr, d
 
 // Read column c and row c of a row-major LD-strided S x S LDS matrix with all
 // 2S ds_read_b64 in flight and a single lgkmcnt wait (hipcc, short of VGPRs,
-// otherwise interleaves ~10 read/wait round trips per matrix).
+// otherwise interleaves ~10 read/wait round trips per matrix)
 __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)p;
 }
 
-template <int I, int S, int LD>
-struct LdsColRow {
-  static __device__ __forceinline__ void run(unsigned bc, unsigned br, double (&col)[S],
-                                             double (&row)[S]) {
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(col[I]) : "v"(bc), "i"(8 * LD * I));
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(row[I]) : "v"(br), "i"(8 * I));
-    if constexpr (I + 1 < S) LdsColRow<I + 1, S, LD>::run(bc, br, col, row);
-  }
-};
+// (loads and their wait are ONE asm statement with early-clobber outputs: a
+// separate wait statement lets hipcc copy a destination before its data lands)
 template <int S, int LD>
 __device__ __forceinline__ void lds_col_row(const double* img, int c, double (&col)[S],
                                             double (&row)[S]) {
   const unsigned bc = lds_addr(img) + 8u * c;        // (i, c): + 8 LD i
   const unsigned br = lds_addr(img) + 8u * LD * c;   // (c, i): + 8 i
-  LdsColRow<0, S, LD>::run(bc, br, col, row);
+  LdsSym<S, LD>::run(bc, br, col, row);
 }
 
 // sym(M) from a row-major S x S image (LDS) or a padded tile
@@ -187,7 +186,6 @@ __device__ __forceinline__ void sym_from(const double* img, int c, double (&r)[S
   if constexpr (C::LDSASM) {
     double t[S];
     lds_col_row<S, LD>(img, c, r, t);
-    LgkmWait<S>::run(r, t);  // one s_waitcnt naming all 2S destinations
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = 0.5 * (r[i] + t[i]);
   } else {
@@ -357,7 +355,19 @@ __device__ __forceinline__ void neg_inverse_reg(double (&r)[S], double* tile, in
 // read the same, unchanged source registers.
 template <class C, bool NEG, int S, int K>
 __device__ __forceinline__ void gxy(double (&out)[S], const double (&x)[S], const double (&y)[K]) {
-  if constexpr (offset_form<C>()) {
+  if constexpr (C::XYROW) {
+    // out[i] += sum_j bcast_j(x_i) y_j: the accumulator is forwarded between
+    // consecutive FMAs (4.0 cycles each vs 4.9 for 13 independent accumulators)
+    static_for<S>([&](auto I) {
+      if constexpr (I == 0) {
+        if constexpr (NEG) LaneDot<K>::fma_neg(out[I], x[I], y);
+        else LaneDot<K>::fma(out[I], x[I], y);
+      } else {
+        if constexpr (NEG) LaneDot<K>::fma_negq(out[I], x[I], y);
+        else LaneDot<K>::fmaq(out[I], x[I], y);
+      }
+    });
+  } else if constexpr (offset_form<C>()) {
     static_for<K>([&](auto J) {
       if constexpr (J == 0) {
         if constexpr (NEG) RowB<S>::template fma_neg<J>(out, x, y[J]);
@@ -667,13 +677,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return hipGetLastError();
   };
   const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
-  const int variant = ev ? atoi(ev) : 10;
+  const int variant = ev ? atoi(ev) : 12;
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
     if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes);
     if (variant == 8) return go(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes);
+    if (variant == 10) return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
     if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
-    return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
+    return go(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes);
   }
   return hipErrorNotSupported;
 }

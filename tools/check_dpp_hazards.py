@@ -9,6 +9,10 @@ fails if any DPP source could have been written inside the hazard window:
 
     python tools/check_dpp_hazards.py file.s [file.s ...]
 
+It also flags a v_fmac_f64_dpp whose multiplier operand shares VGPRs with its
+accumulator: the signature of LLVM coalescing an asm input with a value-equal
+"+v" output (the generated blocks use "+&v" to prevent it).
+
 Wait states: each instruction counts 1, `s_nop N` counts N + 1.  A label
 inside the window (another control path may enter there) counts as a
 violation unless two wait states follow it (the compiler writes EXEC only
@@ -90,6 +94,12 @@ def check(path, verbose=False):
             hist.append((0, set(), False, True, text))
             continue
         src = dpp_source(text)
+        if src is not None and text.startswith("v_fmac_f64_dpp"):
+            # the multiplier operand never legitimately shares the accumulator's VGPRs:
+            # that is an input operand coalesced with a value-equal "+v" output
+            args = [a.strip() for a in text[len("v_fmac_f64_dpp"):].split(" row_")[0].split(",")]
+            if len(args) >= 3 and regs(args[0]) & regs(args[2].lstrip("-")):
+                bad.append((func, text, "src1 aliases the accumulator (asm operand coalescing)"))
         if src is not None:
             n_dpp += 1
             ws = 0
