@@ -189,3 +189,35 @@ def test_hand_scheduled_blocks_emulated(n):
     E.run(E.extract(inc, "ElimQ", n), regs)
     q = z @ np.linalg.solve(M + eps * np.eye(n), z)
     assert abs(regs[n][n] - q) <= 1e-12 * abs(q)
+
+
+@pytest.mark.parametrize("n", [3, 13])
+def test_query_ldl_block_emulated(n):
+    """QueryLdl<n>: X0 = Ebar - H^T (Mt + eps I)^-1 H from the offset-form Mt
+    (diag - 1 + eps), by elimination + row operations + rank-1 streams."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(100 + n)
+    M = rng.standard_normal((n, n))
+    M = M @ M.T + n * np.eye(n)
+    H = rng.standard_normal((n, n))
+    Eb = rng.standard_normal((n, n))
+    Eb = Eb + Eb.T
+    eps = 1e-9
+    regs = {}
+    for i in range(n):
+        for base, src in ((0, M), (n, H), (2 * n, Eb)):
+            col = rng.standard_normal(16)
+            col[:n] = src[i]
+            regs[base + i] = col
+        regs[i][i] += eps - 1.0
+    regs[3 * n] = np.ones(16)
+    for j in range(10):
+        regs[3 * n + 1 + j] = np.full(16, np.nan)
+    E.run(E.extract(inc, "QueryLdl", n), regs)
+    got = np.array([regs[2 * n + i][:n] for i in range(n)])
+    want = Eb - H.T @ np.linalg.solve(M + eps * np.eye(n), H)
+    assert np.abs(got - want).max() <= 1e-12 * np.abs(want).max()
+    assert regs[3 * n][0] > 0

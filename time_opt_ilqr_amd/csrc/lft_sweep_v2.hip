@@ -26,8 +26,10 @@
 //   8  Chain  : offset form, short C++ pivot chain, pad-free DPP blocks
 //   10 Sched  : offset form, whole-sweep asm blocks
 //   12 SchedRow: Sched + X*Y products as one dependent DPP chain per output
-//      row (accumulator forwarded: 4.0 vs 4.9 cycles per FMA)   (default)
-//   20 SchedRow + per-section s_memtime stamps (diagnostic, tools/stamps.py)
+//      row (accumulator forwarded: 4.0 vs 4.9 cycles per FMA)
+//   14 SchedLdl: SchedRow + the query's Wt = (QT^-1 + Gbar)^-1 and its two
+//      products replaced by one LDL^T elimination that streams X0 (default)
+//   20 SchedLdl + per-section s_memtime stamps (diagnostic, tools/stamps.py)
 #include <stdlib.h>
 
 #include "hop_device.hpp"
@@ -74,7 +76,15 @@ struct SchedRow : Sched {  // X*Y products as one dependent chain per output row
   static constexpr int XYROW = 1;
 };
 
-struct SchedStamped : SchedRow {
+struct SchedLdl : SchedRow {  // + query by LDL^T elimination with row ops and rank-1 streams
+  static constexpr int QLDL = 1;
+};
+template <class C>
+constexpr bool has_qldl() {
+  if constexpr (requires { C::QLDL; }) return C::QLDL != 0;
+  return false;
+}
+struct SchedStamped : SchedLdl {
   static constexpr int STAMP = 1;
 };
 template <class C>
@@ -314,6 +324,53 @@ __device__ __forceinline__ double quad_inverse(double (&r)[S], double* tile, int
   }
   wave_sync();
   return q;
+}
+
+// Query without the Wt inverse (has_qldl): r = Xt + Gbar - I (offset form) is
+// parked, symmetrised and eliminated (QueryLdl); the same row operations turn a
+// copy of H = Fbar^T into L^-1 H and X0 = Ebar - sum_p Ht_p (x) Ht_p / d_p is
+// streamed.  chol_inv ladder on failure: re-form from the tile with eps x 10
+// (Ht and X0 restart from H and Ebar, which are untouched).
+template <class C, int S>
+__device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S],
+                                             const double (&Eb)[S], double (&X0)[S], double* tile,
+                                             int c, int mt, unsigned& st) {
+  lds_put(tile, c, r);
+  diag_add<S, kLdsRow>(tile, c, 1e-9);  // r carries -I: diagonal = value - 1 + eps
+  wave_sync();
+  sym_from<C, S, kLdsRow>(tile, c, r);
+  double Ht[S];
+  copy(Ht, H);
+  copy(X0, Eb);
+  double dmin = 1.0;
+  QueryLdl<S>::run(r, Ht, X0, dmin);
+  const bool ok0 = pivots_ok(X0, dmin);
+  if (__any(!ok0)) {
+    double eps = ok0 ? 1e-9 : 1e-8, cur = 1e-9;
+    int tries = ok0 ? 0 : 1;
+    bool done = ok0;
+    if (!ok0) st |= ST_JITTER;
+#pragma unroll 1
+    while (true) {
+      diag_add<S, kLdsRow>(tile, c, eps - cur);
+      cur = eps;
+      sym_from<C, S, kLdsRow>(tile, c, r);
+      copy(Ht, H);
+      copy(X0, Eb);
+      dmin = 1.0;
+      QueryLdl<S>::run(r, Ht, X0, dmin);
+      const bool ok = pivots_ok(X0, dmin);
+      const bool last = tries >= mt;
+      if (!done && !ok && last) st |= ST_LU;
+      done = done || ok || last;
+      if (!__any(!done)) break;
+      if (!done) {
+        eps *= 10.0;
+        ++tries;
+      }
+    }
+  }
+  wave_sync();
 }
 
 // Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1  (+ I in offset form)
@@ -615,13 +672,20 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     // ---- query horizon t = k + 1
 #pragma unroll
     for (int i = 0; i < S; ++i) NX[i] = Gb[i] - NX[i];   // QT^-1 + Gbar
-    neg_inverse_reg<C, S>(NX, tile, c, mt, st, -1.0);       // NX = -Wt
-    stamp(6);
-    double V[S];
-    if constexpr (OFF) copy(V, H); else zero(V);
-    gxy<C, true>(V, NX, H);      // Wt Fbar^T
-    copy(NX, Eb);
-    gxty<C, true>(NX, H, V);     // X0 = Ebar - Fbar Wt Fbar^T
+    if constexpr (has_qldl<C>()) {
+      double X0[S];
+      query_x0_ldl<C, S>(NX, H, Eb, X0, tile, c, mt, st);  // X0 = Ebar - Fbar Wt Fbar^T
+      copy(NX, X0);
+      stamp(6);
+    } else {
+      neg_inverse_reg<C, S>(NX, tile, c, mt, st, -1.0);     // NX = -Wt
+      stamp(6);
+      double V[S];
+      if constexpr (OFF) copy(V, H); else zero(V);
+      gxy<C, true>(V, NX, H);      // Wt Fbar^T
+      copy(NX, Eb);
+      gxty<C, true>(NX, H, V);     // X0 = Ebar - Fbar Wt Fbar^T
+    }
     stamp(7);
     double jk;
     if constexpr (C::ELIM) {
@@ -677,14 +741,15 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return hipGetLastError();
   };
   const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
-  const int variant = ev ? atoi(ev) : 12;
+  const int variant = ev ? atoi(ev) : 14;
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
     if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes);
     if (variant == 8) return go(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes);
     if (variant == 10) return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
+    if (variant == 12) return go(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes);
     if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
-    return go(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes);
+    return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
   }
   return hipErrorNotSupported;
 }
