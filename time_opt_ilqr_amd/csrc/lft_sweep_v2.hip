@@ -84,6 +84,17 @@ constexpr bool has_qldl() {
   if constexpr (requires { C::QLDL; }) return C::QLDL != 0;
   return false;
 }
+struct SchedLdl2 : SchedLdl {  // + compose by two-pass LDL^T (no W inverse, no products)
+  static constexpr int CLDL = 1;
+};
+template <class C>
+constexpr bool has_cldl() {
+  if constexpr (requires { C::CLDL; }) return C::CLDL != 0;
+  return false;
+}
+struct SchedLdl2Stamped : SchedLdl2 {
+  static constexpr int STAMP = 1;
+};
 struct SchedStamped : SchedLdl {
   static constexpr int STAMP = 1;
 };
@@ -373,6 +384,62 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
   wave_sync();
 }
 
+
+// ---------------------------------------------------------------------------
+// Compose by two-pass LDL^T (has_cldl): M = E_k + Gbar_{k-1} = L D L^T.
+//   pass 1: eliminate M (offset form, in registers, retry ladder from the tile);
+//           afterwards row p of r holds U_p = D L^T row p at lanes > p and
+//           d_p - 1 at lane p (rows are never touched once they are pivots).
+//   pass 2: no dependent chains: Htil = L^-1 H and Ftil = L^-1 F by forward
+//           substitution (H_i += bcast_i(U_p) (-Htil_p / d_p), i > p), and the
+//           three products of the compose streamed as rank-1 updates:
+//             Ebar   -= sum_p Htil_p (x) Htil_p / d_p    (Fbar W Fbar^T)
+//             Fbar^T' = sum_p Ftil_p (x) Htil_p / d_p    (F^T W Fbar^T)
+//             Gbar    = G - sum_p Ftil_p (x) Ftil_p / d_p (G - F^T W F)
+// ---------------------------------------------------------------------------
+template <class C, int S, int p>
+__device__ __forceinline__ void elim_pivot_off(double (&r)[S], double& dmin) {
+  double d = 1.0;
+  // block p-1 wrote S-p rows, r[p] first: fewer than 3 leave < 2 wait states
+  fmac_bcast<p, p == 0 || (S - p) <= 2>(d, r[p], 1.0);
+  const double rd0 = __builtin_amdgcn_rcp(d);
+  const double e = __builtin_fma(-d, rd0, 1.0);
+  const double sc0 = -r[p] * rd0;
+  dmin = __builtin_fmin(dmin, d);
+  const double sc = __builtin_fma(sc0, e, sc0);
+  if constexpr (p == 0) TailB<S>::template elim<p>(r, sc);
+  else TailB<S>::template elimq<p>(r, sc);
+}
+
+// a NaN pivot turns every later row NaN, the last one included
+template <int S>
+__device__ __forceinline__ bool elim_ok(const double (&r)[S], double dmin) {
+  const double x = bcast<S - 1>(r[S - 1]);
+  return (dmin > 0.0) && (x == x);
+}
+
+template <class C, int S>
+__device__ __forceinline__ void compose_pass2(const double (&r)[S], double (&H)[S], double (&F)[S],
+                                              double (&Eb)[S], double (&Gb)[S]) {
+  double H2[S];
+  zero(H2);
+  static_for<S>([&](auto P) {
+    constexpr int p = P;
+    double d = 1.0;
+    fmac_bcast<p, p == 0>(d, r[p], 1.0);
+    const double rd0 = __builtin_amdgcn_rcp(d);
+    const double e = __builtin_fma(-d, rd0, 1.0);
+    const double r1 = __builtin_fma(rd0, e, rd0);
+    const double hs = -H[p] * r1, fs = -F[p] * r1;
+    LaneT<S>::template fmaq<p>(H, r[p], hs);  // Htil rows below p
+    LaneT<S>::template fmaq<p>(F, r[p], fs);  // Ftil rows below p
+    LaneB<S>::fmaq(Eb, H[p], hs);
+    LaneB<S>::fma_negq(H2, F[p], hs);
+    LaneB<S>::fmaq(Gb, F[p], fs);
+  });
+  copy(H, H2);
+}
+
 // Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1  (+ I in offset form)
 template <class C, int S, int LD>
 __device__ __forceinline__ void neg_inverse(double (&r)[S], const double* img, int c, int mt,
@@ -496,6 +563,9 @@ struct Geo {
   static constexpr int OFF_Q = 0, OFF_A = IMGM_W, OFF_QT = 2 * IMGM_W, OFF_B = 3 * IMGM_W;
   static constexpr int OFF_T = 3 * IMGM_W + IMGB_W;
   static constexpr int WAVE_BYTES = OFF_T + TILE_W;
+  // has_cldl: a second tile set parks QT^-1 (NX) across the compose
+  static constexpr int OFF_X = OFF_T + TILE_W;
+  static constexpr int WAVE_BYTES_X = OFF_X + TILE_W;
 };
 
 template <class C, int S, int MM>
@@ -506,9 +576,11 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  unsigned char* wbase = smem_raw + w * G::WAVE_BYTES;
+  constexpr int WB = has_cldl<C>() ? G::WAVE_BYTES_X : G::WAVE_BYTES;
+  unsigned char* wbase = smem_raw + w * WB;
   const unsigned wlds = (unsigned)(uintptr_t)wbase;  // LDS byte address (wave-uniform)
   double* tile = reinterpret_cast<double*>(wbase + G::OFF_T) + g * kLdsTile;
+  double* tileX = reinterpret_cast<double*>(wbase + G::OFF_X) + g * kLdsTile;
   const double* imQ = reinterpret_cast<const double*>(wbase + G::OFF_Q + g * G::IMGM);
   const double* imA = reinterpret_cast<const double*>(wbase + G::OFF_A + g * G::IMGM);
   const double* imT = reinterpret_cast<const double*>(wbase + G::OFF_QT + g * G::IMGM);
@@ -591,7 +663,9 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   unsigned long long tprev = 0;
   auto stamp = [&](int j) {
     if constexpr (C::STAMP) {
+      __builtin_amdgcn_sched_barrier(0);  // keep the sections' code on their side
       const unsigned long long t = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
       if (j >= 0) sec[j] += t - tprev;
       tprev = t;
     }
@@ -613,6 +687,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     stamp(0);
     neg_inverse2<C, S, S, S>(NE, imQ, NX, imT, c, mt, st);
     stamp(1);
+    if constexpr (has_cldl<C>()) lds_put(tileX, c, NX);  // own column, read back at the query
     double at[S], brow[MM];
 #pragma unroll
     for (int j = 0; j < S; ++j) at[j] = imA[c * S + j];   // row c of A
@@ -624,7 +699,24 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     // offset form: NE, NX, NW carry +I; a product -(N + I) Y = (-N) Y - Y starts from Y
     double F[S];
     if constexpr (OFF) copy(F, at); else zero(F);
-    gxy<C, true>(F, NE, at);    // F = E A^T
+    double Mr[S];  // has_cldl: M = E_k + Gbar_{k-1}, eliminated in pass 1
+    double dminM = 1.0;
+    if (has_cldl<C>() && k > 0) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) Mr[i] = Gb[i] - NE[i];  // E_k + Gbar - I (offset form)
+      lds_put(tile, c, Mr);
+      diag_add<S, kLdsRow>(tile, c, 1e-9);
+      wave_sync();
+      sym_from<C, S, kLdsRow>(tile, c, Mr);
+      // pass 1 pivots interleaved with the rows of F = E A^T (independent work)
+      static_for<S>([&](auto P) {
+        elim_pivot_off<C, S, P>(Mr, dminM);
+        if constexpr (P == 0) LaneDot<S>::fma_neg(F[P], NE[P], at);
+        else LaneDot<S>::fma_negq(F[P], NE[P], at);
+      });
+    } else {
+      gxy<C, true>(F, NE, at);    // F = E A^T
+    }
     double Gk[S];
     zero(Gk);
     gxty<C, false>(Gk, at, F);  // A F
@@ -650,6 +742,35 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
         }
       }
       copy(Gb, Gk);
+    } else if constexpr (has_cldl<C>()) {
+      const bool ok0 = elim_ok(Mr, dminM);
+      if (__any(!ok0)) {  // chol_inv ladder on M alone (utils.py:69-93)
+        double eps = ok0 ? 1e-9 : 1e-8, cur = 1e-9;
+        int tries = ok0 ? 0 : 1;
+        bool done = ok0;
+        if (!ok0) st |= ST_JITTER;
+#pragma unroll 1
+        while (true) {
+          diag_add<S, kLdsRow>(tile, c, eps - cur);
+          cur = eps;
+          sym_from<C, S, kLdsRow>(tile, c, Mr);
+          double dm = 1.0;
+          static_for<S>([&](auto P) { elim_pivot_off<C, S, P>(Mr, dm); });
+          const bool ok = elim_ok(Mr, dm);
+          const bool last = tries >= mt;
+          if (!done && !ok && last) st |= ST_LU;
+          done = done || ok || last;
+          if (!__any(!done)) break;
+          if (!done) {
+            eps *= 10.0;
+            ++tries;
+          }
+        }
+      }
+      wave_sync();
+      stamp(4);
+      copy(Gb, Gk);
+      compose_pass2<C, S>(Mr, H, F, Eb, Gb);
     } else {
       double NW[S];
 #pragma unroll
@@ -670,6 +791,10 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     stamp(5);
 
     // ---- query horizon t = k + 1
+    if constexpr (has_cldl<C>()) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) NX[i] = tileX[i * kLdsRow + c];
+    }
 #pragma unroll
     for (int i = 0; i < S; ++i) NX[i] = Gb[i] - NX[i];   // QT^-1 + Gbar
     if constexpr (has_qldl<C>()) {
@@ -748,6 +873,12 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     if (variant == 8) return go(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes);
     if (variant == 10) return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
     if (variant == 12) return go(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes);
+    if (variant == 16)
+      return go(v2::lft_sweep_v2_kernel<v2::SchedLdl2, 13, 4>,
+                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
+    if (variant == 22)
+      return go(v2::lft_sweep_v2_kernel<v2::SchedLdl2Stamped, 13, 4>,
+                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
     if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
     return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
   }

@@ -1,0 +1,9 @@
+#!/bin/bash
+# instruction-fetch / I-cache counters for the LFT bench (GPU box, repo root)
+OUT=gpurun_out/$1
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+B="python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --prewarm-s 0"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_IFETCH SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_LDS -d $OUT/pmc_sq -o run --output-format csv -- $B > $OUT/pmc_sq.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQC_TC_INST_REQ SQC_ICACHE_REQ -d $OUT/pmc_sqc -o run --output-format csv -- $B > $OUT/pmc_sqc.log 2>&1
+echo "prof rc=$?"

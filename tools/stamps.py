@@ -12,8 +12,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-NAMES = ["top wait + J store + diag offsets", "E/Xt paired inverses", "A/B reads + DMA issue",
-         "F, G products", "W inverse", "compose products", "Wt inverse", "V, X0 products",
+NAMES = ["top wait + J store + diag offsets", "E/Xt inverses", "A/B reads + DMA issue",
+         "F, G products", "W inverse", "compose products", "query: X0 (LDL, or Wt inverse)", "V, X0 products (non-LDL)",
          "bordered elimination", "-"]
 
 
