@@ -357,3 +357,37 @@ def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch, schedule):
     assert _elem_rel(fast.J.cpu().numpy()[ok], Jo[ok]) <= RTOL64
     assert _elem_rel(fast.J.cpu().numpy()[20], Jo[20]) <= 1e-6
     assert fast.t_star.cpu().numpy()[ok].tolist() == gen.t_star.cpu().numpy()[ok].tolist()
+
+
+@pytest.mark.parametrize("s,m,dt,tol", [(5, 1, "f32", 2e-3), (3, 1, "f64", 1e-10),
+                                        (4, 2, "f64", 1e-10)])
+def test_lft_small_path_matches_generic_and_oracle(dev, monkeypatch, s, m, dt, tol):
+    """The one-problem-per-lane kernel (lft_small.hip, s <= 5) agrees with the
+    generic kernel and the oracle, including jitter / LU-slot problems and a
+    batch that is not a multiple of the 64-lane wave."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    Bn, N = 131, 40
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(900 + s, Bn, s, m, N)
+    Q = Q.copy()
+    Q[7, 3] = Q[7, 3] - np.eye(s) * (np.linalg.eigvalsh(Q[7, 3]).min() + 5e-7)  # jitter
+    Q[70, 5] = -np.eye(s)                                                   # LU slot
+    td = torch.float32 if dt == "f32" else torch.float64
+    args = [torch.as_tensor(np.ascontiguousarray(x), dtype=td, device=dev)
+            for x in (A, Bm, Q, Ri, z0[0], QT)]
+    small = engine.propagate(*args, t_min=3, t_max=N)
+    monkeypatch.setenv("HOP_FORCE_GENERIC", "1")
+    gen = engine.propagate(*args, t_min=3, t_max=N)
+    monkeypatch.delenv("HOP_FORCE_GENERIC")
+    ss = small.status.cpu().numpy()
+    assert ss[7] & orc.ST_JITTER and ss[70] & orc.ST_LU
+    ok = [i for i in range(Bn) if i not in (7, 70)]
+    Js, Jg = small.J.cpu().numpy().astype(float), gen.J.cpu().numpy().astype(float)
+    assert _elem_rel(Js[ok], Jg[ok]) <= tol
+    Jo, sto = orc.lft_sweep_batch(A, Bm, Q, Ri, z0[0], QT)
+    if dt == "f64":  # fp32 can legitimately need jitter where fp64 does not
+        diff = [(i, int(ss[i]), int(sto[i])) for i in range(Bn) if ss[i] != sto[i]]
+        assert not diff, diff
+    assert _elem_rel(Js[ok], Jo[ok]) <= max(tol, RTOL64)
+    if dt == "f64":
+        assert small.t_star.cpu().numpy()[ok].tolist() == gen.t_star.cpu().numpy()[ok].tolist()

@@ -221,3 +221,44 @@ def test_query_ldl_block_emulated(n):
     want = Eb - H.T @ np.linalg.solve(M + eps * np.eye(n), H)
     assert np.abs(got - want).max() <= 1e-12 * np.abs(want).max()
     assert regs[3 * n][0] > 0
+
+
+@pytest.fixture(scope="module")
+def small_host(tmp_path_factory):
+    """g++ build of csrc/small_math.hpp (the small-s kernel's per-problem math)."""
+    import subprocess
+    d = tmp_path_factory.mktemp("small")
+    so = str(d / "libsmall_host.so")
+    src = os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "small_host.cpp")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-DHOP_HD=", src, "-o", so])
+    return C.CDLL(so)
+
+
+@pytest.mark.parametrize("tag,dt", [("s5_m1_N200", np.float64), ("s3_m1_N50", np.float64),
+                                    ("s5_m1_N200", np.float32)])
+def test_small_kernel_math_vs_golden(small_host, golden_dir, tag, dt):
+    """The packed-symmetric sweep-operator arithmetic of lft_small.hip, run on the
+    CPU, reproduces the reference's J curves and T* (golden vectors)."""
+    d = np.load(os.path.join(golden_dir, f"lft_synth_{tag}.npz"))
+    s, m, N, bs, cnt = (int(d[k]) for k in ("s", "m", "N", "base_seed", "count"))
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(bs, cnt, s, m, N)
+    cast = lambda x: np.ascontiguousarray(x, dtype=dt)  # noqa: E731
+    J = np.zeros((cnt, N), dt)
+    st = np.zeros(cnt, np.int32)
+    ts = np.zeros(cnt, np.int32)
+    fn = small_host.small_host_sweep_f64 if dt == np.float64 else small_host.small_host_sweep_f32
+    args = [cast(x) for x in (A, Bm, Q, Ri, QT, np.broadcast_to(z0[0], (cnt, s)))]
+    p = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    rc = fn(*[p(x) for x in args], C.c_int64(cnt), N, s, m, 8, int(d["T_min"]), int(d["T_max"]),
+            p(J), p(st), p(ts))
+    assert rc == 0
+    tol = 1e-10 if dt == np.float64 else 2e-3
+    assert _rel_err(J, d["J"]) <= tol
+    assert (st == 0).all()
+    if dt == np.float64:
+        assert ts.tolist() == d["T_star"].tolist()
+
+
+def _rel_err(got, ref):
+    got, ref = np.asarray(got, float), np.asarray(ref, float)
+    return float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-300))

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
-SOURCES = ["capi.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "riccati.hip"]
+SOURCES = ["capi.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "riccati.hip"]
 HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",

@@ -75,11 +75,13 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
   a.t_min = t_min; a.t_max = t_max;
   a.J = J; a.status = status; a.t_star = t_star; a.j_star = j_star;
   a.dbg_efg = dbg_efg; a.dbg_pre = dbg_pre;
-  if constexpr (sizeof(T) == 8) {
-    if (!getenv("HOP_FORCE_GENERIC")) {
+  if (!getenv("HOP_FORCE_GENERIC")) {
+    if constexpr (sizeof(T) == 8) {
       const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
       if (e != hipErrorNotSupported) return hip_status(e);
     }
+    const hipError_t e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
+    if (e != hipErrorNotSupported) return hip_status(e);
   }
   return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));
 }

@@ -58,6 +58,8 @@ template <class T>
 hipError_t dispatch_lft(const LftArgs<T>& a, hipStream_t stream);
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream);
 template <class T>
+hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream);
+template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream);
 
 }  // namespace hop

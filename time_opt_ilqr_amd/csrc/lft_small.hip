@@ -1,0 +1,191 @@
+// LFT horizon sweep for small augmented dimension (s <= 5): one problem per
+// LANE.  At s = 5 a 16-lane row per problem (lft_sweep.hip) leaves 11 of 16
+// lanes idle and runs 4 problems per wave-instruction; here every lane owns
+// one problem, all its s x s blocks live in registers, and a wave-instruction
+// advances 64 problems.  Same algorithm, _sym placement, chol_inv jitter ladder
+// and status bits as horizon_selection.py:36-86 / utils.py:69-93.
+//
+// Streaming: step k+1's Q, A, B (and, after the query, QT) blocks of the
+// wave's 64 problems are loaded into LDS by LDS-DMA while step k computes.
+// Pieces are chunk-major: piece r holds the r-th 16-byte chunk of every lane's
+// block, so a lane reads its own chunk at base + 1024 r + 16 lane (conflict-free
+// ds_read_b128) and the DMA source of lane l is simply block(l) + 16 r.
+#include "hop_device.hpp"
+#include "hop_kernels.hpp"
+#include "small_math.hpp"
+
+namespace hop {
+namespace small {
+
+__device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds,
+                                      unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+      : "memory");
+}
+
+template <class T, int S, int MM>
+struct Geo {
+  static constexpr int CM = (S * S * (int)sizeof(T) + 15) / 16;   // chunks per s x s block
+  static constexpr int CB = (S * MM * (int)sizeof(T) + 15) / 16;  // chunks per B block
+  static constexpr int P_Q = 0, P_A = CM, P_B = 2 * CM, P_T = 2 * CM + CB;
+  static constexpr int PIECES = 3 * CM + CB;
+  static constexpr int WAVE_BYTES = PIECES * 1024;
+  static constexpr int TPB = 256;  // 4 waves per block
+};
+
+// read an (R x C) row-major block from the wave's chunk-major LDS image
+template <class T, int R, int C, int P0>
+__device__ __forceinline__ void read_block(const unsigned char* wimg, int lane, T (&out)[R][C]) {
+  constexpr int NE = R * C, CH = (NE * (int)sizeof(T) + 15) / 16, PER = 16 / (int)sizeof(T);
+  T buf[CH * PER];
+#pragma unroll
+  for (int r = 0; r < CH; ++r) {
+    const float4 v = *reinterpret_cast<const float4*>(wimg + (P0 + r) * 1024 + 16 * lane);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) buf[r * PER + q] = e[q];
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int j = 0; j < C; ++j) out[i][j] = buf[i * C + j];
+}
+
+template <class T, int S, int MM>
+__global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
+  using G = Geo<T, S, MM>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned char* wimg = smem_raw + w * G::WAVE_BYTES;
+  const unsigned wlds = (unsigned)(uintptr_t)wimg;
+  const long long wave_prob0 = (long long)blockIdx.x * G::TPB + w * 64;
+  const long long prob = wave_prob0 + lane;
+  const bool valid = prob < a.batch;
+  const long long pb = valid ? prob : a.batch - 1;
+  const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
+  const int N = a.n, mt = a.max_tries;
+  constexpr int SS = S * S, SM = S * MM, TS = (int)sizeof(T);
+  const long long pstrM = (long long)a.nalloc * SS * TS, pstrB = (long long)a.nalloc * SM * TS;
+  auto mk = [&](const T* base, long long pstr) {
+    // exact bounds: range checking is per dword (tools/ubench_oob.hip), so a chunk
+    // straddling the tensor end returns its valid dwords and zeros
+    const long long left = (a.batch - pb0) * pstr;
+    const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base) + pb0 * (pstr / TS), (short)0,
+                                             (int)nrec, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rQ = mk(a.Q, pstrM), rA = mk(a.A, pstrM), rT = mk(a.QT, pstrM),
+                               rB = mk(a.B, pstrB);
+  const unsigned vM = (unsigned)((pb - pb0) * pstrM), vB = (unsigned)((pb - pb0) * pstrB);
+  auto dma_stage = [&](int k) {  // Q, A, B of step k
+    const unsigned soM = (unsigned)(k * SS * TS), soB = (unsigned)(k * SM * TS);
+#pragma unroll
+    for (int r = 0; r < G::CM; ++r) dma16(vM + 16 * r, rQ, wlds + (G::P_Q + r) * 1024, soM);
+#pragma unroll
+    for (int r = 0; r < G::CM; ++r) dma16(vM + 16 * r, rA, wlds + (G::P_A + r) * 1024, soM);
+#pragma unroll
+    for (int r = 0; r < G::CB; ++r) dma16(vB + 16 * r, rB, wlds + (G::P_B + r) * 1024, soB);
+  };
+  auto dma_query = [&](int k) {  // QT of step k
+    const unsigned soM = (unsigned)(k * SS * TS);
+#pragma unroll
+    for (int r = 0; r < G::CM; ++r) dma16(vM + 16 * r, rT, wlds + (G::P_T + r) * 1024, soM);
+  };
+  auto vm_wait = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  T z[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) z[i] = a.z0[pb * a.z_bstride + i];
+  State<T, S, MM> ps;
+  ps.st = 0;
+  ps.best = T(0);
+  ps.tbest = 0;
+  T rinv[MM][MM];
+  {
+    const T* Rp = a.R + pb * a.r_bstride;
+    Gen<T, MM> r;
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+      for (int j = 0; j < MM; ++j) r.a[i][j] = Rp[i * MM + j];
+    Sym<T, MM> rs;
+    sym_of(rs, r);
+    if (!a.r_is_inv) spd_inverse(rs, mt, ps.st);
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+      for (int j = 0; j < MM; ++j) rinv[i][j] = a.r_is_inv ? r.a[i][j] : rs.at(i, j);
+  }
+  if (N > 0) {
+    dma_stage(0);
+    dma_query(0);
+  }
+#pragma unroll 1
+  for (int k = 0; k < N; ++k) {
+    vm_wait();     // this wave's LDS-DMA pieces of step k have landed
+    wave_sync();   // (each wave owns its LDS image: no workgroup barrier)
+    {
+      Gen<T, S> Q, A;
+      T Bk[S][MM];
+      read_block<T, S, S, G::P_Q>(wimg, lane, Q.a);
+      read_block<T, S, S, G::P_A>(wimg, lane, A.a);
+      read_block<T, S, MM, G::P_B>(wimg, lane, Bk);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (k + 1 < N) dma_stage(k + 1);
+      stage_compose<T, S, MM>(ps, k, Q, A, Bk, rinv, mt);
+    }
+    Gen<T, S> QT;
+    read_block<T, S, S, G::P_T>(wimg, lane, QT.a);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (k + 1 < N) dma_query(k + 1);
+    const T jk = query<T, S, MM>(ps, QT, z, mt);
+    if (valid) a.J[prob * N + k] = jk;
+    take(ps, k + 1, jk, a.t_min, a.t_max);
+  }
+  vm_wait();
+  if (valid) {
+    a.status[prob] = (int)ps.st;
+    if (a.t_max > 0 && a.t_star != nullptr) {
+      a.t_star[prob] = ps.tbest;
+      a.j_star[prob] = ps.best;
+    }
+  }
+}
+
+}  // namespace small
+
+// small-s path: returns hipErrorNotSupported when the shape has no instantiation
+template <class T>
+hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
+  if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
+  auto go = [&](auto kern, int bytes) {
+    const long long blocks = (a.batch + 255) / 256;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+    return hipGetLastError();
+  };
+#define HOP_SMALL(S_, M_)                                                                 \
+  if (a.s == S_ && a.m == M_)                                                             \
+    return go(small::lft_small_kernel<T, S_, M_>, small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+  if constexpr (sizeof(T) == 4) {
+    HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)
+    HOP_SMALL(5, 2)  // s = 6 spills: generic kernel
+  } else {
+    HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2)
+  }
+#undef HOP_SMALL
+  return hipErrorNotSupported;
+}
+
+template hipError_t dispatch_lft_small<float>(const LftArgs<float>&, hipStream_t);
+template hipError_t dispatch_lft_small<double>(const LftArgs<double>&, hipStream_t);
+
+}  // namespace hop

@@ -599,8 +599,10 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 
   // buffer descriptors for the wave's 4 problems (bounds-checked: OOB -> 0)
   auto mk = [&](const double* base, long long pstr) {
-    // +16: the last 16-B chunk of a block may read 8 bytes past it (never used)
-    const long long left = (a.batch - pb0) * pstr + 16;
+    // exact bounds: range checking is per dword (tools/ubench_oob.hip), so the
+    // last 16-B chunk of the tensor returns its valid dwords and zeros -- no
+    // read past the allocation (which can end on an unmapped page)
+    const long long left = (a.batch - pb0) * pstr;
     const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
     return __builtin_amdgcn_make_buffer_rsrc(
         const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);

@@ -1,0 +1,62 @@
+// Host build of small_math.hpp for the CPU test suite (not part of libhop_amd.so):
+//   g++ -O2 -std=c++17 -shared -fPIC -DHOP_HD= small_host.cpp -o libsmall_host.so
+// Runs the exact per-problem arithmetic of lft_small.hip on the CPU.
+#include <stdint.h>
+
+#include "small_math.hpp"
+
+using namespace hop::small;
+
+template <class T, int S, int MM>
+static void run(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, const T* z0,
+                int64_t batch, int n, int mt, int t_min, int t_max, T* J, int32_t* status,
+                int32_t* t_star) {
+  for (int64_t b = 0; b < batch; ++b) {
+    State<T, S, MM> ps;
+    ps.st = 0;
+    ps.best = T(0);
+    ps.tbest = 0;
+    T z[S], rinv[MM][MM];
+    for (int i = 0; i < S; ++i) z[i] = z0[b * S + i];
+    for (int i = 0; i < MM; ++i)
+      for (int j = 0; j < MM; ++j) rinv[i][j] = Rinv[b * MM * MM + i * MM + j];  // per problem
+    for (int k = 0; k < n; ++k) {
+      Gen<T, S> Qk, Ak, QTk;
+      T Bk[S][MM];
+      const int64_t o = (b * n + k) * S * S, ob = (b * n + k) * S * MM;
+      for (int i = 0; i < S; ++i)
+        for (int j = 0; j < S; ++j) {
+          Qk.a[i][j] = Q[o + i * S + j];
+          Ak.a[i][j] = A[o + i * S + j];
+          QTk.a[i][j] = QT[o + i * S + j];
+        }
+      for (int i = 0; i < S; ++i)
+        for (int j = 0; j < MM; ++j) Bk[i][j] = B[ob + i * MM + j];
+      stage_compose<T, S, MM>(ps, k, Qk, Ak, Bk, rinv, mt);
+      const T jk = query<T, S, MM>(ps, QTk, z, mt);
+      J[b * n + k] = jk;
+      take(ps, k + 1, jk, t_min, t_max);
+    }
+    status[b] = (int32_t)ps.st;
+    t_star[b] = ps.tbest;
+  }
+}
+
+extern "C" int small_host_sweep_f64(const double* A, const double* B, const double* Q,
+                                    const double* Rinv, const double* QT, const double* z0,
+                                    int64_t batch, int n, int s, int m, int mt, int t_min,
+                                    int t_max, double* J, int32_t* status, int32_t* t_star) {
+  if (s == 3 && m == 1) run<double, 3, 1>(A, B, Q, Rinv, QT, z0, batch, n, mt, t_min, t_max, J, status, t_star);
+  else if (s == 5 && m == 1) run<double, 5, 1>(A, B, Q, Rinv, QT, z0, batch, n, mt, t_min, t_max, J, status, t_star);
+  else return -1;
+  return 0;
+}
+
+extern "C" int small_host_sweep_f32(const float* A, const float* B, const float* Q,
+                                    const float* Rinv, const float* QT, const float* z0,
+                                    int64_t batch, int n, int s, int m, int mt, int t_min,
+                                    int t_max, float* J, int32_t* status, int32_t* t_star) {
+  if (s == 5 && m == 1) run<float, 5, 1>(A, B, Q, Rinv, QT, z0, batch, n, mt, t_min, t_max, J, status, t_star);
+  else return -1;
+  return 0;
+}

@@ -1,0 +1,306 @@
+// Per-problem LFT sweep math for small s (one problem per lane), shared by the
+// GPU kernel (lft_small.hip) and a host build used by the CPU test suite
+// (tests/test_host_cpu.py compiles it with g++ and checks it against the
+// oracle), so the arithmetic the kernel runs is exercised without a GPU.
+//
+// Symmetric matrices (E, W, Ebar, Gbar, G, QT^-1, Wt, X0) are stored packed
+// (upper triangle, s(s+1)/2 values): at s = 5 the live set fits in registers,
+// the symmetric sweep operator does half the FLOPs of a Gauss-Jordan inverse,
+// and symmetric products are formed on the upper triangle only.
+// Reference: horizon_selection.py:36-86 (LFT), utils.py:35-37 (_sym),
+// utils.py:69-93 (chol_inv jitter ladder).
+#pragma once
+
+#ifndef HOP_HD
+#define HOP_HD __host__ __device__
+#endif
+
+namespace hop {
+namespace small {
+
+constexpr unsigned kStJitter = 1u, kStLu = 2u, kStNonfinite = 4u;
+
+template <class T, int S>
+struct Gen {
+  T a[S][S];
+};
+
+template <class T, int S>
+struct Sym {
+  static constexpr int NP = S * (S + 1) / 2;
+  T v[NP];
+  static HOP_HD constexpr int idx(int i, int j) {  // i <= j
+    return i * S - i * (i - 1) / 2 + (j - i);
+  }
+  HOP_HD T& at(int i, int j) { return i <= j ? v[idx(i, j)] : v[idx(j, i)]; }
+  HOP_HD T at(int i, int j) const { return i <= j ? v[idx(i, j)] : v[idx(j, i)]; }
+};
+
+// _sym(M) of a general matrix
+template <class T, int S>
+HOP_HD inline void sym_of(Sym<T, S>& out, const Gen<T, S>& m) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = i; j < S; ++j) out.at(i, j) = T(0.5) * (m.a[i][j] + m.a[j][i]);
+}
+
+// Symmetric sweep operator on (M + eps I): after all pivots x = -(M + eps I)^-1.
+// Pivots are the Cholesky squares, so "all > 0" is the potrf test.
+template <class T, int S>
+HOP_HD inline bool sweep_neg_inverse(Sym<T, S>& x, T eps) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < S; ++i) x.at(i, i) += eps;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    const T d = x.at(p, p);
+    ok = ok && (d > T(0));
+    const T r = T(1) / d;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      if (i == p) continue;
+      const T aip = x.at(i, p) * r;
+#pragma unroll
+      for (int j = i; j < S; ++j) {
+        if (j == p) continue;
+        x.at(i, j) -= aip * x.at(p, j);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (i != p) x.at(i, p) *= r;
+    x.at(p, p) = -r;
+  }
+  return ok;
+}
+
+// chol_inv (utils.py:69-93) on an already symmetric input: jitter 1e-9, x10 per
+// failure; after max_tries the last attempt is kept (LU slot) and flagged.
+template <class T, int S>
+HOP_HD inline void spd_inverse(Sym<T, S>& m, int max_tries, unsigned& st) {
+  const Sym<T, S> in = m;
+  T eps = T(1e-9);
+  bool ok = sweep_neg_inverse(m, eps);
+  if (!ok) {
+    st |= kStJitter;
+    for (int tries = 1;; ++tries) {
+      eps *= T(10);
+      m = in;
+      ok = sweep_neg_inverse(m, eps);
+      if (ok) break;
+      if (tries >= max_tries) {
+        st |= kStLu;
+        break;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = -m.v[k];
+}
+
+// z^T (X + eps I)^-1 z by LDL^T elimination, same ladder (X symmetric)
+template <class T, int S>
+HOP_HD inline T quad_inverse(const Sym<T, S>& x0, const T (&z)[S], int max_tries, unsigned& st) {
+  T eps = T(1e-9);
+  for (int tries = 0;; ++tries) {
+    Sym<T, S> x = x0;
+    T b[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) b[i] = z[i];
+    T acc = T(0);
+    bool ok = true;
+#pragma unroll
+    for (int p = 0; p < S; ++p) {
+      const T d = x.at(p, p) + eps;
+      ok = ok && (d > T(0));
+      const T r = T(1) / d;
+      acc += b[p] * b[p] * r;
+#pragma unroll
+      for (int i = p + 1; i < S; ++i) {
+        const T l = x.at(i, p) * r;
+        b[i] -= l * b[p];
+#pragma unroll
+        for (int j = i; j < S; ++j) x.at(i, j) -= l * x.at(p, j);
+      }
+    }
+    if (ok) return acc;
+    if (tries == 0) st |= kStJitter;
+    if (tries >= max_tries) {
+      st |= kStLu;
+      return acc;
+    }
+    eps *= T(10);
+  }
+}
+
+// ---- products (G: general, Y: symmetric) --------------------------------
+// out = S_ * G^T   (general)
+template <class T, int S>
+HOP_HD inline void mul_sym_gt(Gen<T, S>& out, const Sym<T, S>& s, const Gen<T, S>& g) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < S; ++l) v += s.at(i, l) * g.a[j][l];
+      out.a[i][j] = v;
+    }
+}
+// out = S_ * G   (general)
+template <class T, int S>
+HOP_HD inline void mul_sym_g(Gen<T, S>& out, const Sym<T, S>& s, const Gen<T, S>& g) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < S; ++l) v += s.at(i, l) * g.a[l][j];
+      out.a[i][j] = v;
+    }
+}
+// out = G1 * G2   (general)
+template <class T, int S>
+HOP_HD inline void mul_gg(Gen<T, S>& out, const Gen<T, S>& x, const Gen<T, S>& y) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < S; ++l) v += x.a[i][l] * y.a[l][j];
+      out.a[i][j] = v;
+    }
+}
+// acc (upper triangle) += sgn * X * Y   (X*Y symmetric in exact arithmetic)
+template <bool NEG, class T, int S>
+HOP_HD inline void acc_sym_xy(Sym<T, S>& acc, const Gen<T, S>& x, const Gen<T, S>& y) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = i; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < S; ++l) v += x.a[i][l] * y.a[l][j];
+      acc.at(i, j) = NEG ? acc.at(i, j) - v : acc.at(i, j) + v;
+    }
+}
+// acc (upper triangle) += sgn * X^T * Y
+template <bool NEG, class T, int S>
+HOP_HD inline void acc_sym_xty(Sym<T, S>& acc, const Gen<T, S>& x, const Gen<T, S>& y) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = i; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < S; ++l) v += x.a[l][i] * y.a[l][j];
+      acc.at(i, j) = NEG ? acc.at(i, j) - v : acc.at(i, j) + v;
+    }
+}
+
+// ---- one step of the sweep ------------------------------------------------
+template <class T, int S, int MM>
+struct State {
+  Sym<T, S> Eb, Gb;
+  Gen<T, S> Fb;
+  T best;
+  int tbest;
+  unsigned st;
+};
+
+// stage + compose for step k (Q, A, B of step k given); returns nothing
+template <class T, int S, int MM>
+HOP_HD inline void stage_compose(State<T, S, MM>& s, int k, const Gen<T, S>& Q,
+                                 const Gen<T, S>& A, const T (&Bk)[S][MM],
+                                 const T (&rinv)[MM][MM], int mt) {
+  Sym<T, S> E;
+  sym_of(E, Q);
+  spd_inverse(E, mt, s.st);                 // E = chol_inv(Q)
+  Gen<T, S> F;
+  mul_sym_gt(F, E, A);                      // F = E A^T
+  Sym<T, S> G;                              // G = _sym(A F + B R^-1 B^T)
+#pragma unroll
+  for (int i = 0; i < Sym<T, S>::NP; ++i) G.v[i] = T(0);
+  acc_sym_xy<false>(G, A, F);
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    T y[MM];
+#pragma unroll
+    for (int q = 0; q < MM; ++q) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < MM; ++l) v += Bk[i][l] * rinv[l][q];
+      y[q] = v;
+    }
+#pragma unroll
+    for (int j = i; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int q = 0; q < MM; ++q) v += y[q] * Bk[j][q];
+      G.at(i, j) += v;
+    }
+  }
+  if (k == 0) {
+    s.Eb = E;
+    s.Fb = F;
+    s.Gb = G;
+    return;
+  }
+  Sym<T, S> W;
+#pragma unroll
+  for (int i = 0; i < Sym<T, S>::NP; ++i) W.v[i] = E.v[i] + s.Gb.v[i];
+  spd_inverse(W, mt, s.st);                 // W = (E_k + Gbar)^-1
+  Gen<T, S> Z;
+  mul_sym_gt(Z, W, s.Fb);                   // W Fbar^T
+  acc_sym_xy<true>(s.Eb, s.Fb, Z);          // Ebar = _sym(Ebar - Fbar W Fbar^T)
+  mul_sym_g(Z, W, F);                       // W F
+  Gen<T, S> Fn;
+  mul_gg(Fn, s.Fb, Z);                      // Fbar = Fbar W F
+  s.Fb = Fn;
+  s.Gb = G;
+  acc_sym_xty<true>(s.Gb, F, Z);            // Gbar = _sym(G - F^T W F)
+}
+
+// query horizon k+1 from QT_k; returns J
+template <class T, int S, int MM>
+HOP_HD inline T query(State<T, S, MM>& s, const Gen<T, S>& QT, const T (&z)[S], int mt) {
+  Sym<T, S> X;
+  sym_of(X, QT);
+  spd_inverse(X, mt, s.st);                 // QT^-1
+#pragma unroll
+  for (int i = 0; i < Sym<T, S>::NP; ++i) X.v[i] += s.Gb.v[i];
+  spd_inverse(X, mt, s.st);                 // Wt = (QT^-1 + Gbar)^-1
+  Gen<T, S> V;
+  mul_sym_gt(V, X, s.Fb);                   // Wt Fbar^T
+  Sym<T, S> X0 = s.Eb;
+  acc_sym_xy<true>(X0, s.Fb, V);            // X0 = _sym(Ebar - Fbar Wt Fbar^T)
+  return T(0.5) * quad_inverse(X0, z, mt, s.st);
+}
+
+template <class T>
+HOP_HD inline bool finite_t(T x) {
+  return x == x && x - x == T(0);
+}
+
+// argmin over [t_min, t_max] with np.argmin semantics (first minimiser, a NaN wins)
+template <class T, int S, int MM>
+HOP_HD inline void take(State<T, S, MM>& s, int t, T jk, int t_min, int t_max) {
+  if (!finite_t(jk)) s.st |= kStNonfinite;
+  if (t_max <= 0) return;
+  if (t == t_min) {
+    s.best = jk;
+    s.tbest = t;
+  } else if (t > t_min && t <= t_max) {
+    const bool bnan = s.best != s.best, jnan = jk != jk;
+    if (!bnan && (jnan || jk < s.best)) {
+      s.best = jk;
+      s.tbest = t;
+    }
+  }
+}
+
+}  // namespace small
+}  // namespace hop
