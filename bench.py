@@ -23,8 +23,20 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-PEAK_F64_TFLOPS = 78.6  # MI355X dense fp64 (vector == matrix), MI355X_MICROARCH.md / datasheet
+PEAK_F64_TFLOPS = 78.6   # MI355X dense fp64 (vector == matrix), MI355X_MICROARCH.md / datasheet
+PEAK_F32_TFLOPS = 157.3  # MI355X fp32 vector (packed)
 PEAK_HBM_GBS = 8000.0
+SMALL_SHAPES = {"f32": {(2, 1), (3, 1), (4, 1), (4, 2), (5, 1), (5, 2)},
+                "f64": {(2, 1), (3, 1), (4, 1), (4, 2)}}
+
+
+def kernel_path(s, m, dtype):
+    """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound."""
+    if dtype == "f64" and (s, m) == (13, 4):
+        return "lft_sweep_v2_kernel<SchedLdl,13,4>", "mfma"
+    if (s, m) in SMALL_SHAPES[dtype]:
+        return f"lft_small_kernel<{'float' if dtype == 'f32' else 'double'},{s},{m}>", "hbm"
+    return "lft_sweep_kernel", "mfma"
 
 
 def lft_flops(N, s, m):
@@ -157,8 +169,15 @@ def main():
     if rank == 0:
         total = Bn * world * K
         value = total / elapsed
-        fl = lft_flops(N, s, m) * (hi - lo)
-        achieved = fl / (kern_ms * 1e-3) / 1e12
+        kname, bound = kernel_path(s, m, args.dtype)
+        w = 8 if dtype == torch.float64 else 4
+        if bound == "hbm":
+            achieved = lft_bytes(N, s, m, w) * (hi - lo) / (kern_ms * 1e-3) / 1e9
+            peak, unit = PEAK_HBM_GBS, "GB/s"
+        else:
+            achieved = lft_flops(N, s, m) * (hi - lo) / (kern_ms * 1e-3) / 1e12
+            peak = PEAK_F64_TFLOPS if args.dtype == "f64" else PEAK_F32_TFLOPS
+            unit = "TFLOP/s"
         traffic = None
         try:
             with open(args.traffic_json) as f:
@@ -188,10 +207,10 @@ def main():
             "config": {"workload": f"LFT sweep + fused argmin, s={s} m={m} N={N}",
                        "batch_per_gpu": Bn, "global_batch": Bn * world, "s": s, "m": m,
                        "N": N, "t_min": t_min, "t_max": t_max, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F64_TFLOPS,
-                         "unit": "TFLOP/s", "frac": achieved / PEAK_F64_TFLOPS,
+            "roofline": {"bound": bound, "achieved": achieved, "peak": peak,
+                         "unit": unit, "frac": achieved / peak,
                          "traffic": traffic,
-                         "kernel": "lft_sweep_v2_kernel<SchedLdl,13,4>" if (s, m, args.dtype) == (13, 4, "f64") else "lft_sweep_kernel", "kernel_ms": kern_ms,
+                         "kernel": kname, "kernel_ms": kern_ms,
                          "flops_per_sweep": lft_flops(N, s, m),
                          "alg_bytes_per_sweep": lft_bytes(N, s, m, 8 if dtype == torch.float64 else 4)},
             "cpu_baseline": cpu,

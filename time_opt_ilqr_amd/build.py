@@ -15,8 +15,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
-SOURCES = ["capi.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "riccati.hip"]
-HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc"]
+SOURCES = ["capi.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "lft_small_noslp.hip",
+           "riccati.hip"]
+EXTRA = {"lft_small_noslp.hip": ["-fno-slp-vectorize"]}
+HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",
          "-Wno-unused-but-set-variable"]
@@ -37,6 +39,7 @@ def _digest():
     with open(os.path.join(REPO, "include", "hop.h"), "rb") as f:
         h.update(f.read())
     h.update(" ".join(FLAGS).encode())
+    h.update(repr(sorted(EXTRA.items())).encode())
     return h.hexdigest()
 
 
@@ -84,7 +87,8 @@ def build(force=False, jobs=None, verbose=True):
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
         objs.append(obj)
         # -save-temps=obj keeps the device assembly for the DPP hazard check
-        cmd = [hipcc, *FLAGS, "-save-temps=obj", "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc, *FLAGS, *EXTRA.get(src, []), "-save-temps=obj", "-c",
+               os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print("[hop]", " ".join(cmd))
         procs.append(subprocess.Popen(cmd))

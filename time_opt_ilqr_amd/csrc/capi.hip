@@ -80,7 +80,10 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
       const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
       if (e != hipErrorNotSupported) return hip_status(e);
     }
-    const hipError_t e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
+    const char* sv = getenv("HOP_SMALL_VARIANT");  // same-process A/B of the s <= 5 build
+    const hipError_t e = (sv && atoi(sv) == 1)
+                             ? hop::dispatch_lft_small_noslp<T>(a, (hipStream_t)stream)
+                             : hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
     if (e != hipErrorNotSupported) return hip_status(e);
   }
   return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));

@@ -60,6 +60,8 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream);
 template <class T>
+hipError_t dispatch_lft_small_noslp(const LftArgs<T>& a, hipStream_t stream);
+template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream);
 
 }  // namespace hop

@@ -12,6 +12,29 @@
 // ds_read_b128) and the DMA source of lane l is simply block(l) + 16 r.
 #include "hop_device.hpp"
 #include "hop_kernels.hpp"
+
+// lft_small_noslp.hip re-compiles this file under another namespace with
+// -fno-slp-vectorize (same-process A/B, HOP_SMALL_VARIANT=1)
+#ifndef HOP_SMALL_NS
+#define HOP_SMALL_NS small
+#define HOP_SMALL_DISPATCH dispatch_lft_small
+#endif
+#define small HOP_SMALL_NS
+
+namespace hop {
+namespace small {
+// 1/d as v_rcp + one Newton step (the IEEE division sequence is ~10 instructions)
+__device__ __forceinline__ float small_recip(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  return __builtin_fmaf(r, __builtin_fmaf(-d, r, 1.0f), r);
+}
+__device__ __forceinline__ double small_recip(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+}
+}  // namespace small
+}  // namespace hop
+
 #include "small_math.hpp"
 
 namespace hop {
@@ -129,10 +152,25 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
     dma_stage(0);
     dma_query(0);
   }
+  // J ring: the values of 8 steps are written together, right after a DMA wait,
+  // so that no vmcnt(0) ever waits on a scattered store and each lane writes
+  // 32 contiguous bytes instead of 4 (write traffic: 409 MB -> ~J's 52 MB)
+  constexpr int JR = 8;
+  T jring[JR];
+#pragma unroll
+  for (int i = 0; i < JR; ++i) jring[i] = T(0);
+  auto flush = [&](int k0, int cnt) {  // steps k0 .. k0+cnt-1 are jring[JR-cnt .. JR-1]
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < JR; ++i)
+        if (i >= JR - cnt) a.J[prob * N + k0 + i - (JR - cnt)] = jring[i];
+    }
+  };
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
     vm_wait();     // this wave's LDS-DMA pieces of step k have landed
     wave_sync();   // (each wave owns its LDS image: no workgroup barrier)
+    if (k >= JR && k % JR == 0) flush(k - JR, JR);
     {
       Gen<T, S> Q, A;
       T Bk[S][MM];
@@ -148,10 +186,16 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (k + 1 < N) dma_query(k + 1);
     const T jk = query<T, S, MM>(ps, QT, z, mt);
-    if (valid) a.J[prob * N + k] = jk;
+#pragma unroll
+    for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
+    jring[JR - 1] = jk;
     take(ps, k + 1, jk, a.t_min, a.t_max);
   }
   vm_wait();
+  if (N > 0) {
+    const int tail = N % JR == 0 ? JR : N % JR;  // steps not flushed by the loop
+    flush(N - tail, tail);
+  }
   if (valid) {
     a.status[prob] = (int)ps.st;
     if (a.t_max > 0 && a.t_star != nullptr) {
@@ -165,7 +209,7 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
 
 // small-s path: returns hipErrorNotSupported when the shape has no instantiation
 template <class T>
-hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
+hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
   auto go = [&](auto kern, int bytes) {
     const long long blocks = (a.batch + 255) / 256;
@@ -185,7 +229,7 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
   return hipErrorNotSupported;
 }
 
-template hipError_t dispatch_lft_small<float>(const LftArgs<float>&, hipStream_t);
-template hipError_t dispatch_lft_small<double>(const LftArgs<double>&, hipStream_t);
+template hipError_t HOP_SMALL_DISPATCH<float>(const LftArgs<float>&, hipStream_t);
+template hipError_t HOP_SMALL_DISPATCH<double>(const LftArgs<double>&, hipStream_t);
 
 }  // namespace hop

@@ -3,6 +3,13 @@
 // Runs the exact per-problem arithmetic of lft_small.hip on the CPU.
 #include <stdint.h>
 
+namespace hop {
+namespace small {
+template <class T>
+inline T small_recip(T d) { return T(1) / d; }
+}  // namespace small
+}  // namespace hop
+
 #include "small_math.hpp"
 
 using namespace hop::small;

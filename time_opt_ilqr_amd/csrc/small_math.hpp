@@ -20,6 +20,9 @@ namespace small {
 
 constexpr unsigned kStJitter = 1u, kStLu = 2u, kStNonfinite = 4u;
 
+// small_recip(d) = 1/d is supplied by the includer: the GPU kernel uses
+// v_rcp + one Newton step (lft_small.hip), the host test build exact division.
+
 template <class T, int S>
 struct Gen {
   T a[S][S];
@@ -56,7 +59,7 @@ HOP_HD inline bool sweep_neg_inverse(Sym<T, S>& x, T eps) {
   for (int p = 0; p < S; ++p) {
     const T d = x.at(p, p);
     ok = ok && (d > T(0));
-    const T r = T(1) / d;
+    const T r = small_recip(d);
 #pragma unroll
     for (int i = 0; i < S; ++i) {
       if (i == p) continue;
@@ -114,7 +117,7 @@ HOP_HD inline T quad_inverse(const Sym<T, S>& x0, const T (&z)[S], int max_tries
     for (int p = 0; p < S; ++p) {
       const T d = x.at(p, p) + eps;
       ok = ok && (d > T(0));
-      const T r = T(1) / d;
+      const T r = small_recip(d);
       acc += b[p] * b[p] * r;
 #pragma unroll
       for (int i = p + 1; i < S; ++i) {

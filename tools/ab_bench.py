@@ -21,11 +21,17 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--s", type=int, default=13)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--env", default="HOP_LFT_VARIANT", help="variable the variants set")
     args = ap.parse_args()
     import torch
     from time_opt_ilqr_amd import engine, synth
     dev = torch.device("cuda", 0)
-    A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, 13, 4, args.N, seed=5, device=dev)
+    dt = torch.float64 if args.dtype == "f64" else torch.float32
+    A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, args.s, args.m, args.N, seed=5,
+                                              device=dev, dtype=dt)
     variants = args.variants.split(",")
 
     def setv(v):
@@ -33,7 +39,7 @@ def main():
         if v == "g":
             os.environ["HOP_FORCE_GENERIC"] = "1"
         else:
-            os.environ["HOP_LFT_VARIANT"] = v
+            os.environ[args.env] = v
 
     ref = None
     for v in variants:  # warm + cross-check
