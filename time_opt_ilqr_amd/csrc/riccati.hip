@@ -127,18 +127,27 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
     }
   }
 
+  // step i's A, B, x, u are loaded one step ahead (software pipeline): the
+  // global-load latency of step i-1 hides behind step i's arithmetic
+  T acol_n[S], bcol_n[S], x_n, u_n;
+  auto load_step = [&](int i) {
+    rload_col(Ap + (long long)i * nn, n, n, c, T(0), acol_n);
+    rload_col(Bp + (long long)i * nm, n, m, c, T(0), bcol_n);  // lanes c < m: column c of B_i
+    x_n = Xp[(long long)i * n + (c < n ? c : 0)];
+    u_n = Up[(long long)i * m + (c < m ? c : 0)];
+  };
+  if (Lw > 0) load_step(Lw - 1);
 #pragma unroll 1
   for (int i = Lw - 1; i >= 0; --i) {
     const bool act = alive && (i < L);
-    if (!__any(act)) continue;
-    const T* Ai = Ap + (long long)i * nn;
-    const T* Bi = Bp + (long long)i * nm;
-    T acol[S], bcol[S];
-    rload_col(Ai, n, n, c, T(0), acol);
-    rload_col(Bi, n, m, c, T(0), bcol);  // lanes c < m: column c of B_i
-    T e = (c < n) ? Xp[(long long)i * n + (c < n ? c : 0)] - xg_c : T(0);
+    T e = (c < n) ? x_n - xg_c : T(0);
     if (wrap_c) e = wrap_angle(e);
-    const T du = (c < m) ? Up[(long long)i * m + (c < m ? c : 0)] - ur_c : T(0);
+    const T du = (c < m) ? u_n - ur_c : T(0);
+    T acol[S], bcol[S];
+    copy(acol, acol_n);
+    copy(bcol, bcol_n);
+    load_step(i > 0 ? i - 1 : 0);
+    if (!__any(act)) continue;
     const unsigned long long badm = __ballot(!(finite_val(e) && finite_val(du)));
     const bool bad = ((badm >> (16 * g)) & 0xffffull) != 0ull;
 
