@@ -101,6 +101,90 @@ int hop_select_horizon_f32(const float* J, int64_t batch, int32_t ld, int32_t t_
                            int32_t t_max, int32_t* t_star, float* j_star, void* stream);
 
 /*
+ * hop_augment_f64 / _f32
+ * Replaces build_augmented_sequence_QR(F, A_list, B_list, X, U, xg, u_ref, Q, R, w,
+ *            wrap_idx, q_reg, rho_reg, extra_stage_cost)
+ *            /root/reference/augmented.py:10-60
+ *      and build_terminal_aug_list(X, xg, alpha, wrap_idx, rho_reg)
+ *            /root/reference/augmented.py:63-87
+ * for a batch, on the device.  The dynamics stay with the caller: it passes
+ * the affine residuals a_res[k] = F(x_k, u_k) - x_{k+1}
+ * (compute_affine_residuals, linearization.py:269-270) and R_inv = chol_inv(R)
+ * is the caller's (the sweep takes it as R_inv_cached).
+ *
+ *   A [batch][n_alloc][n][n]   Bm [batch][n_alloc][n][m]   a_res [batch][n_alloc][n]
+ *   X [batch][n_alloc+1][n]    U  [batch][n_alloc][m]
+ *   xg [.][n], u_ref [.][m], Q [.][n][n] (raw stage weight), w [.] (time weight),
+ *   P [.][n][n] = _sym(as_terminal_weight(alpha)) (utils.py:49-62); batch
+ *      strides in elements, 0 = shared.
+ *   qxx_extra [batch][n_alloc][n][n], qx_extra [batch][n_alloc][n],
+ *   c_extra [batch][n_alloc]: extra_stage_cost (c, cx, cxx) at (X_k, U_k), or NULL.
+ *   wrap_mask bit i = wrap_idx contains i.  q_reg = 1e-9, rho_reg = 1e-12 in the
+ *      reference.
+ *   Outputs for steps k < n_build (s = n+1): A_aug, Q_aug, QT_aug [batch][n_build][s][s],
+ *      B_aug [batch][n_build][s][m]; z0 [s] = e_s (nullable).
+ */
+int hop_augment_f64(const double* A, const double* Bm, const double* a_res, const double* X,
+                    const double* U, const double* xg, int64_t xg_batch_stride,
+                    const double* u_ref, int64_t u_ref_batch_stride, const double* Q,
+                    int64_t q_batch_stride, const double* P, int64_t p_batch_stride,
+                    const double* w, int64_t w_batch_stride, const double* qxx_extra,
+                    const double* qx_extra, const double* c_extra, uint32_t wrap_mask,
+                    double q_reg, double rho_reg, int64_t batch, int32_t n_alloc,
+                    int32_t n_build, int32_t n, int32_t m, double* A_aug, double* B_aug,
+                    double* Q_aug, double* QT_aug, double* z0, void* stream);
+int hop_augment_f32(const float* A, const float* Bm, const float* a_res, const float* X,
+                    const float* U, const float* xg, int64_t xg_batch_stride,
+                    const float* u_ref, int64_t u_ref_batch_stride, const float* Q,
+                    int64_t q_batch_stride, const float* P, int64_t p_batch_stride,
+                    const float* w, int64_t w_batch_stride, const float* qxx_extra,
+                    const float* qx_extra, const float* c_extra, uint32_t wrap_mask,
+                    float q_reg, float rho_reg, int64_t batch, int32_t n_alloc,
+                    int32_t n_build, int32_t n, int32_t m, float* A_aug, float* B_aug,
+                    float* Q_aug, float* QT_aug, float* z0, void* stream);
+
+/*
+ * hop_lft_sweep_traj_f64 / _f32
+ * Replaces the "select" block of ilqr_timeopt (solver.py:514-522):
+ *   build_augmented_sequence_QR + build_terminal_aug_list
+ *   + propagator_all_Jt_aug(..., T_use=n_use, R_inv_cached=R_inv) [+ argmin]
+ * from the trajectory-form inputs of hop_augment_* (same meaning), for a batch.
+ * For s = 13, m = 4, fp64 without extra_stage_cost the blocks are built inside
+ * the sweep and never written to HBM (workspace unused, may be NULL).  Other
+ * shapes run hop_augment into `workspace` and then the sweep; size it with
+ * hop_lft_sweep_traj_workspace_bytes (256-B aligned; 0 = not needed).
+ *   R_inv [batch or 1][m][m] (r_batch_stride = m*m or 0); J/status/t_min/t_max/
+ *   t_star/j_star as hop_lft_sweep_*; max_tries as chol_inv (8).
+ */
+int64_t hop_lft_sweep_traj_workspace_bytes(int64_t batch, int32_t n_use, int32_t n, int32_t m,
+                                           int32_t elem_bytes, int32_t has_extra);
+int hop_lft_sweep_traj_f64(const double* A, const double* Bm, const double* a_res,
+                           const double* X, const double* U, const double* xg,
+                           int64_t xg_batch_stride, const double* u_ref,
+                           int64_t u_ref_batch_stride, const double* Q, int64_t q_batch_stride,
+                           const double* P, int64_t p_batch_stride, const double* w,
+                           int64_t w_batch_stride, const double* qxx_extra,
+                           const double* qx_extra, const double* c_extra, uint32_t wrap_mask,
+                           double q_reg, double rho_reg, const double* R_inv,
+                           int64_t r_batch_stride, int64_t batch, int32_t n_alloc,
+                           int32_t n_use, int32_t n, int32_t m, int32_t max_tries,
+                           int32_t t_min, int32_t t_max, double* J, int32_t* status,
+                           int32_t* t_star, double* j_star, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+int hop_lft_sweep_traj_f32(const float* A, const float* Bm, const float* a_res, const float* X,
+                           const float* U, const float* xg, int64_t xg_batch_stride,
+                           const float* u_ref, int64_t u_ref_batch_stride, const float* Q,
+                           int64_t q_batch_stride, const float* P, int64_t p_batch_stride,
+                           const float* w, int64_t w_batch_stride, const float* qxx_extra,
+                           const float* qx_extra, const float* c_extra, uint32_t wrap_mask,
+                           float q_reg, float rho_reg, const float* R_inv,
+                           int64_t r_batch_stride, int64_t batch, int32_t n_alloc,
+                           int32_t n_use, int32_t n, int32_t m, int32_t max_tries,
+                           int32_t t_min, int32_t t_max, float* J, int32_t* status,
+                           int32_t* t_star, float* j_star, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+
+/*
  * hop_riccati_f64 / _f32
  * mode 0 replaces backward_pass_truncated(A_list, B_list, X, U, xg, u_ref, Q, R,
  *        alpha, T_star, lm_lambda, wrap_idx, extra_stage_cost)

@@ -485,3 +485,29 @@ def synth_riccati_problem(seed, n, m, N):
     R = np.diag(rng.uniform(0.5, 2.0, m))
     alpha = float(rng.uniform(5.0, 20.0))
     return A, B, X, U, xg, u_ref, Q, R, alpha
+
+
+def synth_traj_problem(seed, n, m, N):
+    """Trajectory-form select inputs (augmented.py:10-87 + propagator) for one
+    problem: A_k, B_k, raw residuals a_k, X, U, xg, u_ref, Q, R, alpha (diagonal
+    terminal weight), w and wrap_idx.  Angles of state 0 span several turns so
+    the wrap is exercised.  The residual the reference forms,
+    F(x_k, u_k) - x_{k+1} with F(x_k, u_k) = x_{k+1} + a_raw_k, is returned as
+    a_res (same NumPy expression as compute_affine_residuals)."""
+    rng = np.random.default_rng(int(seed))
+    A = np.eye(n) + 0.05 * rng.standard_normal((N, n, n))
+    B = 0.1 * rng.standard_normal((N, n, m))
+    X = 0.5 * rng.standard_normal((N + 1, n))
+    X[:, 0] = 6.0 * rng.standard_normal(N + 1)
+    U = 0.3 * rng.standard_normal((N, m))
+    a_raw = 0.02 * rng.standard_normal((N, n))
+    xg = 0.2 * rng.standard_normal(n)
+    u_ref = 0.1 * rng.standard_normal(m)
+    M = rng.standard_normal((n, n))
+    Q = M @ M.T / n + 0.5 * np.eye(n)
+    R = np.diag(rng.uniform(0.5, 2.0, m))
+    alpha = rng.uniform(1.0, 10.0, n)
+    w = float(rng.uniform(0.2, 1.0))
+    a_res = np.stack([(X[k + 1] + a_raw[k]) - X[k + 1] for k in range(N)])
+    return dict(A=A, B=B, a_res=a_res, X=X, U=U, xg=xg, u_ref=u_ref, Q=Q, R=R, alpha=alpha,
+                w=w, wrap_idx=[0], a_raw=a_raw)

@@ -29,6 +29,8 @@ import utils as ref_utils  # noqa: E402
 import horizon_selection as ref_hs  # noqa: E402
 import solver as ref_solver  # noqa: E402
 import systems as ref_systems  # noqa: E402
+import augmented as ref_aug  # noqa: E402
+import linearization as ref_lin  # noqa: E402
 
 from oracle import hop_oracle as orc  # noqa: E402
 
@@ -216,6 +218,89 @@ def chol_inv_cases():
     print("chol_inv_cases:", list(cases))
 
 
+def _lookup_dynamics(X, U, a_raw):
+    """F with F(X[k], U[k]) = X[k+1] + a_raw[k] (the reference only evaluates F
+    on the trajectory inside compute_affine_residuals)."""
+    table = {X[k].tobytes() + U[k].tobytes(): X[k + 1] + a_raw[k] for k in range(len(U))}
+    return lambda x, u: table[np.asarray(x, dtype=float).tobytes()
+                              + np.asarray(u, dtype=float).tobytes()]
+
+
+def traj_synth(tag, n, m, N, seeds, rho_regs, blocks_steps=3):
+    """Reference builders (augmented.py:10-87) + propagator on trajectory-form inputs."""
+    d = dict(n=n, m=m, N=N, seeds=np.array(seeds), rho_regs=np.array(rho_regs))
+    Js, a_res, R_inv = [], [], []
+    for sd, rho in zip(seeds, rho_regs):
+        p = orc.synth_traj_problem(sd, n, m, N)
+        F = _lookup_dynamics(p["X"], p["U"], p["a_raw"])
+        a_list = ref_lin.compute_affine_residuals(F, p["X"], p["U"])
+        Aa, Ba, Qa, R_list, z0, Ri = ref_aug.build_augmented_sequence_QR(
+            F, list(p["A"]), list(p["B"]), p["X"], p["U"], p["xg"], p["u_ref"], p["Q"], p["R"],
+            p["w"], wrap_idx=p["wrap_idx"], rho_reg=rho)
+        QT = ref_aug.build_terminal_aug_list(p["X"], p["xg"], p["alpha"], wrap_idx=p["wrap_idx"],
+                                             rho_reg=rho)
+        J = ref_hs.propagator_all_Jt_aug(Aa, Ba, Qa, R_list, z0, QT, T_use=N, R_inv_cached=Ri)
+        Js.append(np.array(J))
+        a_res.append(np.array([a.ravel() for a in a_list]))
+        R_inv.append(np.array(Ri))
+        if len(Js) == 1:
+            for key, v in (("A_aug", Aa), ("B_aug", Ba), ("Q_aug", Qa), ("QT_aug", QT)):
+                d[key] = np.array(v[:blocks_steps])
+    d.update(J=np.array(Js), a_res=np.array(a_res), R_inv=np.array(R_inv))
+    np.savez_compressed(os.path.join(HERE, f"traj_synth_{tag}.npz"), **d)
+    print(f"traj_synth_{tag}: J[0][:3]={Js[0][:3]}")
+
+
+def traj_real(tag, maker_kwargs, maker, T_min=None, T_max=None, S_window=20):
+    """Raw inputs of the first build_augmented_sequence_QR call of ilqr_timeopt
+    (solver.py:514-522) on a real system, with the J curve that call produced."""
+    out = maker(**maker_kwargs)
+    F, x0, xg, u_ref, Q, R, alpha, w, N, tmin, tmax, wrap_idx, extra = out
+    T_min = tmin if T_min is None else T_min
+    T_max = tmax if T_max is None else T_max
+    builds, props = [], []
+    real_build = ref_solver.build_augmented_sequence_QR
+    real_prop = ref_solver.propagator_all_Jt_aug
+
+    def build_spy(F_, A_list, B_list, X, U, *a, **k):
+        builds.append(dict(A=np.array(A_list), B=np.array(B_list), X=np.array(X),
+                           U=np.array(U),
+                           a_res=np.array([r.ravel() for r in
+                                           ref_lin.compute_affine_residuals(F_, X, U)])))
+        return real_build(F_, A_list, B_list, X, U, *a, **k)
+
+    def prop_spy(*a, **k):
+        J = real_prop(*a, **k)
+        props.append(np.array(J))
+        return J
+
+    ref_solver.build_augmented_sequence_QR = build_spy
+    ref_solver.propagator_all_Jt_aug = prop_spy
+    try:
+        ref_solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max,
+                                method="propagator", max_iter=1, S_window=S_window,
+                                wrap_idx=wrap_idx, use_central_diff=False,
+                                extra_stage_cost=None)
+    finally:
+        ref_solver.build_augmented_sequence_QR = real_build
+        ref_solver.propagator_all_Jt_aug = real_prop
+    b = builds[0]
+    d = dict(N=N, T_min=T_min, T_max=T_max, alpha=alpha, w=w, Q=Q, R=R, xg=xg, u_ref=u_ref,
+             wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64),
+             P=np.array(ref_utils._sym(ref_utils.as_terminal_weight(alpha, len(xg)))),
+             R_inv=np.array(ref_utils.chol_inv(ref_utils._sym(R))), J=props[0], **b)
+    np.savez_compressed(os.path.join(HERE, f"traj_real_{tag}.npz"), **d)
+    print(f"traj_real_{tag}: N={N} T*={int(np.argmin(props[0][T_min - 1:T_max]) + T_min)}")
+
+
+def main_traj():
+    np.seterr(all="ignore")
+    traj_synth("n12_m4_N100", 12, 4, 100, [8000, 8001, 8002, 8003], [1.0, 1.0, 1e-12, 1e-12])
+    traj_synth("n4_m1_N60", 4, 1, 60, [8100, 8101], [1.0, 1e-12])
+    traj_real("DI_N50", dict(N=50), ref_systems.make_double_integrator, T_min=10, T_max=50)
+    traj_real("Quad_N160", {}, ref_systems.make_quadrotor)
+
+
 def main():
     np.seterr(all="ignore")
     synthetic_lft("s13_m4_N100", 13, 4, 100, 1000, 4, 40, 100)
@@ -234,4 +319,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--traj" in sys.argv:  # only the trajectory-form fixtures
+        main_traj()
+    else:
+        main()
+        main_traj()

@@ -1,0 +1,195 @@
+"""GPU parity of the trajectory-form path (augmented.py:10-87 on the device):
+hop_augment_* (batched builders) and hop_lft_sweep_traj_* (builders + the
+propagator, fused into the sweep for s = 13, m = 4 fp64), against the oracle
+pinned by the reference's own builders (tests/golden/traj_*.npz).
+
+Tolerances:
+  * builder blocks ............. 1e-14 relative (only the order of the Q e / e^T Q e
+                                 sums differs from NumPy's)
+  * J, well-conditioned terminal blocks (rho_reg = 1) ... 1e-9 relative, same T*
+  * J, the reference's rho_reg = 1e-12 (terminal Schur complement 1e-12): the
+    same bars as the augmented-form real captures in test_gpu_parity.py
+    (the 1e-16 differences of the built blocks are amplified ~1e12)
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import hop_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(x, dev, dtype=None):
+    import torch
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype or torch.float64, device=dev)
+
+
+def _rel(got, ref):
+    got = np.asarray(got, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    return float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-300))
+
+
+def _load(golden_dir, name):
+    return np.load(os.path.join(golden_dir, name))
+
+
+def _batch(seeds, n, m, N):
+    ps = [orc.synth_traj_problem(int(s), n, m, N) for s in seeds]
+    st = {k: np.stack([p[k] for p in ps]) for k in ("A", "B", "a_res", "X", "U", "xg", "u_ref",
+                                                     "Q", "R", "alpha", "w")}
+    st["P"] = np.stack([orc.terminal_weight(p["alpha"], n) for p in ps])
+    st["R_inv"] = np.stack([orc.spd_inverse(orc.sym(p["R"]))[0] for p in ps])
+    st["wrap_idx"] = ps[0]["wrap_idx"]
+    return ps, st
+
+
+def _blocks(p, rho, extra=None):
+    Aa, Ba, Qa, _, z0, Ri = orc.augment_stage(list(p["A"]), list(p["B"]), p["a_res"], p["X"],
+                                              p["U"], p["xg"], p["u_ref"], p["Q"], p["R"],
+                                              p["w"], wrap_idx=p["wrap_idx"], rho_reg=rho,
+                                              extra=extra)
+    QT = orc.augment_terminal(p["X"], p["xg"], p["alpha"], wrap_idx=p["wrap_idx"], rho_reg=rho)
+    return Aa, Ba, Qa, Ri, z0, QT
+
+
+def _oracle(p, rho, n_use=None, extra=None):
+    Aa, Ba, Qa, Ri, z0, QT = _blocks(p, rho, extra)
+    return (Aa, Ba, Qa, Ri, z0, QT), orc.lft_sweep(Aa, Ba, Qa, Ri, z0, QT, n_use)
+
+
+def _dev_args(st, dev, dtype=None):
+    return [_t(st[k], dev, dtype) for k in ("A", "B", "a_res", "X", "U", "xg", "u_ref", "Q")]
+
+
+@pytest.mark.parametrize("n,m,N,dt", [(12, 4, 40, "f64"), (4, 1, 33, "f64"), (2, 1, 20, "f64"),
+                                      (5, 2, 17, "f32")])
+def test_augment_kernel_matches_oracle_builders(dev, n, m, N, dt):
+    import torch
+    from time_opt_ilqr_amd import engine
+    dtype = torch.float64 if dt == "f64" else torch.float32
+    ps, st = _batch(range(900, 907), n, m, N)
+    out = engine.augment(*_dev_args(st, dev, dtype), _t(st["P"], dev, dtype),
+                         _t(st["w"], dev, dtype), wrap_idx=st["wrap_idx"])
+    tol = 1e-14 if dt == "f64" else 2e-6
+    for b, p in enumerate(ps):
+        Aa, Ba, Qa, Ri, z0, QT = _blocks(p, 1e-12)
+        assert _rel(out.A[b].cpu(), Aa) <= tol
+        assert _rel(out.B[b].cpu(), Ba) <= tol
+        assert _rel(out.Q[b].cpu(), Qa) <= tol
+        assert _rel(out.QT[b].cpu(), QT) <= tol
+        # structure is exact: A's bottom row [0 .. 0 1], B's zero row, raw blocks copied
+        bottom = np.zeros((N, n + 1))
+        bottom[:, n] = 1.0
+        assert np.array_equal(out.A[b, :, n, :].double().cpu().numpy(), bottom)
+        assert np.array_equal(out.B[b, :, n, :].double().cpu().numpy(), np.zeros((N, m)))
+        assert np.array_equal(out.A[b, :, :n, :n].cpu().numpy(), st["A"][b].astype(
+            out.A.cpu().numpy().dtype))
+    assert out.z0.cpu().tolist() == [0.0] * n + [1.0]
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_traj_sweep_vs_reference_goldens(dev, golden_dir, monkeypatch, fused):
+    """s = 13, m = 4: in-kernel builders (fused) and hop_augment + sweep (unfused)
+    against the reference's builders + propagator (traj_synth_n12_m4_N100)."""
+    from time_opt_ilqr_amd import engine
+    if not fused:
+        monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
+    d = _load(golden_dir, "traj_synth_n12_m4_N100.npz")
+    n, m, N = int(d["n"]), int(d["m"]), int(d["N"])
+    for rho in (1.0, 1e-12):
+        idx = [i for i, r in enumerate(d["rho_regs"]) if r == rho]
+        ps, st = _batch(d["seeds"][idx], n, m, N)
+        res = engine.propagate_traj(*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev),
+                                    _t(st["w"], dev), wrap_idx=st["wrap_idx"], rho_reg=rho,
+                                    t_min=10, t_max=N)
+        J = res.J.cpu().numpy()
+        Jref = d["J"][idx]
+        T_ref = np.argmin(Jref[:, 9:N], axis=1) + 10
+        if rho == 1.0:
+            assert _rel(J, Jref) <= 1e-9
+            assert (res.status.cpu().numpy() == 0).all()
+            assert res.t_star.cpu().tolist() == T_ref.tolist()
+        else:
+            assert _rel(J, Jref) <= 5e-2
+            assert np.isfinite(J).all()
+
+
+@pytest.mark.parametrize("n,m,N", [(4, 1, 60), (12, 4, 37), (2, 1, 25)])
+def test_traj_sweep_batch_vs_oracle(dev, monkeypatch, n, m, N):
+    """Batch tails (7 problems), n_use < N, the small-s and generic kernels behind
+    the unfused path, and the fused path when the shape has it."""
+    from time_opt_ilqr_amd import engine
+    ps, st = _batch(range(950, 957), n, m, N)
+    n_use = N - 3
+    res = engine.propagate_traj(*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev),
+                                _t(st["w"], dev), wrap_idx=st["wrap_idx"], rho_reg=1.0,
+                                n_use=n_use, t_min=2, t_max=n_use)
+    J = res.J.cpu().numpy()
+    for b, p in enumerate(ps):
+        _, o = _oracle(p, 1.0, n_use)
+        assert _rel(J[b], o["J"]) <= 1e-9
+        T, _ = orc.select_horizon(o["J"][None], 2, n_use)
+        assert int(res.t_star[b]) == int(T[0])
+    assert (res.status.cpu().numpy() == 0).all()
+
+
+def test_traj_fused_equals_unfused(dev, monkeypatch):
+    """The fused builder and hop_augment + the augmented-form sweep agree."""
+    from time_opt_ilqr_amd import engine
+    ps, st = _batch(range(970, 1003), 12, 4, 50)
+    args = (*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
+    a = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
+    monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
+    b = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
+    assert _rel(a, b) <= 1e-11
+
+
+def test_traj_extra_stage_cost(dev):
+    """extra_stage_cost (augmented.py:39-46) routes through hop_augment."""
+    from time_opt_ilqr_amd import engine
+    n, m, N = 12, 4, 24
+    ps, st = _batch(range(990, 993), n, m, N)
+    rng = np.random.default_rng(5)
+    L = rng.standard_normal((3, N, n, n))
+    cxx = 0.02 * L @ np.swapaxes(L, -1, -2)  # PSD: the stage blocks stay well-conditioned
+    cx = rng.standard_normal((3, N, n)) * 0.1
+    c0 = rng.uniform(0, 0.1, (3, N))
+    res = engine.propagate_traj(*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev),
+                                _t(st["w"], dev), wrap_idx=st["wrap_idx"], rho_reg=1.0,
+                                qxx_extra=_t(cxx, dev), qx_extra=_t(cx, dev),
+                                c_extra=_t(c0, dev))
+    for b, p in enumerate(ps):
+        X = p["X"]
+        lookup = {X[k].tobytes(): k for k in range(N)}
+
+        def extra(x, u, b=b):
+            k = lookup[np.asarray(x).tobytes()]
+            return c0[b, k], cx[b, k], cxx[b, k]
+
+        _, o = _oracle(p, 1.0, None, extra=extra)
+        assert _rel(res.J[b].cpu(), o["J"]) <= 1e-9
+    assert (res.status.cpu().numpy() == 0).all()
+
+
+@pytest.mark.parametrize("tag,jtol", [("DI_N50", 1e-3), ("Quad_N160", 5e-2)])
+def test_traj_real_first_select(dev, golden_dir, tag, jtol):
+    """The first select block of ilqr_timeopt on the real systems (raw
+    linearisation captured from the reference): T* equal, J at the real-capture
+    bars (the Quadrotor shape runs the fused in-kernel builder)."""
+    from time_opt_ilqr_amd import engine
+    d = _load(golden_dir, f"traj_real_{tag}.npz")
+    T_min, T_max = int(d["T_min"]), int(d["T_max"])
+    T_use = min(T_max, len(d["U"]))
+    x = lambda k: _t(d[k][None], dev)  # noqa: E731
+    res = engine.propagate_traj(x("A"), x("B"), x("a_res"), x("X"), x("U"), _t(d["xg"], dev),
+                                _t(d["u_ref"], dev), _t(d["Q"], dev), _t(d["R_inv"], dev),
+                                _t(d["P"], dev), float(d["w"]),
+                                wrap_idx=d["wrap_idx"].tolist(), n_use=T_use, t_min=T_min,
+                                t_max=T_max)
+    J = res.J[0].cpu().numpy()
+    assert np.max(np.abs(J - d["J"]) / np.abs(d["J"])) <= jtol
+    T_ref = int(np.argmin(d["J"][T_min - 1:T_max]) + T_min)
+    assert int(res.t_star[0]) == T_ref

@@ -33,6 +33,14 @@ _RIC64 = [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, 
           C.c_double, _U32, _I32, _I32, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]
 _RIC32 = list(_RIC64)
 _RIC32[19] = C.c_float
+# trajectory-form inputs shared by hop_augment_* and hop_lft_sweep_traj_*:
+# A Bm a_res X U xg xg_bs u_ref ur_bs Q q_bs P p_bs w w_bs qxx qx c wrap q_reg rho_reg
+_TRJ64 = [_P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _U32,
+          C.c_double, C.c_double]
+_TRJ32 = _TRJ64[:19] + [C.c_float, C.c_float]
+_AUG_TAIL = [_I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]
+_TRAJ_TAIL = [_P, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64,
+              _P]
 
 SIGNATURES = {
     "hop_abi_version": (C.c_int, []),
@@ -41,6 +49,11 @@ SIGNATURES = {
     "hop_lft_sweep_f32": (C.c_int, _LFT),
     "hop_select_horizon_f64": (C.c_int, _SEL),
     "hop_select_horizon_f32": (C.c_int, _SEL),
+    "hop_augment_f64": (C.c_int, _TRJ64 + _AUG_TAIL),
+    "hop_augment_f32": (C.c_int, _TRJ32 + _AUG_TAIL),
+    "hop_lft_sweep_traj_workspace_bytes": (C.c_int64, [_I64, _I32, _I32, _I32, _I32, _I32]),
+    "hop_lft_sweep_traj_f64": (C.c_int, _TRJ64 + _TRAJ_TAIL),
+    "hop_lft_sweep_traj_f32": (C.c_int, _TRJ32 + _TRAJ_TAIL),
     "hop_riccati_f64": (C.c_int, _RIC64),
     "hop_riccati_f32": (C.c_int, _RIC32),
 }

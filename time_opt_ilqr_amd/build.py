@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
-SOURCES = ["capi.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "lft_small_noslp.hip",
+SOURCES = ["capi.hip", "augment.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "lft_small_noslp.hip",
            "riccati.hip"]
 EXTRA = {"lft_small_noslp.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp"]

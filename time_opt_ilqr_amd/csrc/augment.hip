@@ -1,0 +1,147 @@
+// Batched augmented-block builders on the device:
+//   build_augmented_sequence_QR  augmented.py:10-60  -> A_aug, B_aug, Q_aug
+//   build_terminal_aug_list      augmented.py:63-87  -> QT_aug
+// for every problem of a batch, from the raw linearisation (A_k, B_k, the affine
+// residual a_k = F(x_k,u_k) - x_{k+1}) and the cost terms (Q, P = _sym(Qf), w).
+// This is the path for shapes without an in-kernel builder (lft_sweep_v2.hip
+// builds the blocks inside the sweep for s = 13, m = 4).
+//
+// HBM-bound: per step it reads n^2 + nm + 2n + m values (+ extras) and writes
+// 3 s^2 + s m.  One workgroup owns KS consecutive steps of one problem: phase 1
+// forms the per-step vectors (e_k, e_{k+1}, du_k, Q e, P e, a~) in LDS, phase 2
+// writes the blocks as contiguous, coalesced runs.
+#include "hop_device.hpp"
+#include "hop_kernels.hpp"
+
+namespace hop {
+namespace aug {
+
+constexpr int KS = 16;  // steps per workgroup (16 lanes per step in phase 1)
+constexpr int TPB = 256;
+
+template <class T>
+__global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
+  const TrajArgs<T>& t = a.t;
+  const int n = t.n, m = t.m, s = n + 1;
+  const int nchunk = (a.nbuild + KS - 1) / KS;
+  const long long b = blockIdx.x / nchunk;
+  const int k0 = (blockIdx.x % nchunk) * KS;
+  const int ks = min(KS, a.nbuild - k0);
+  const int NA = a.nalloc;
+  __shared__ T e0[KS][16], e1[KS][16], du[KS][16], qe[KS][16], pe[KS][16], at[KS][16];
+  __shared__ T eqe[KS], epe[KS];
+
+  const T* xg = t.xg + b * t.xg_bs;
+  const T* ur = t.u_ref + b * t.ur_bs;
+  const T* Q = t.Q + b * t.q_bs;
+  const T* P = t.P + b * t.p_bs;
+  const T wt = t.w[b * t.w_bs];
+  if (a.z0 && blockIdx.x == 0 && threadIdx.x < s) a.z0[threadIdx.x] = threadIdx.x == n ? T(1) : T(0);
+  const int tid = threadIdx.x, kk = tid >> 4, i = tid & 15, k = k0 + kk;
+  const bool row_ok = kk < ks;
+
+  // phase 1a: errors (wrap_error, utils.py:131-137) and control deviations
+  if (row_ok) {
+    if (i < n) {
+      T x0 = t.X[(b * (NA + 1) + k) * n + i] - xg[i];
+      T x1 = t.X[(b * (NA + 1) + k + 1) * n + i] - xg[i];
+      if ((t.wrap_mask >> i) & 1u) {
+        x0 = wrap_angle(x0);
+        x1 = wrap_angle(x1);
+      }
+      e0[kk][i] = x0;
+      e1[kk][i] = x1;
+    }
+    if (i < m) du[kk][i] = t.U[(b * NA + k) * m + i] - ur[i];
+  }
+  __syncthreads();
+  // phase 1b: Q e_k (augmented.py:35-36), P e_{k+1} (:78), a~ = a_k - B_k du_k (:50)
+  if (row_ok && i < n) {
+    T v = T(0), p = T(0), bd = T(0);
+    for (int j = 0; j < n; ++j) {
+      v += Q[i * n + j] * e0[kk][j];
+      p += P[i * n + j] * e1[kk][j];
+    }
+    const T* Bk = t.Bm + ((b * NA + k) * n + i) * m;
+    for (int q = 0; q < m; ++q) bd += Bk[q] * du[kk][q];
+    qe[kk][i] = v;
+    pe[kk][i] = p;
+    at[kk][i] = t.ares[(b * NA + k) * n + i] - bd;
+  }
+  __syncthreads();
+  // e^T Q e (:37) and e^T P e (:79; 2 * (1/2 e^T P e) is exact)
+  if (row_ok && i == 0) {
+    T v = T(0), p = T(0);
+    for (int j = 0; j < n; ++j) {
+      v += e0[kk][j] * qe[kk][j];
+      p += e1[kk][j] * pe[kk][j];
+    }
+    T corner = v + T(2) * wt + t.rho_reg;
+    if (t.c_extra) corner += T(2) * t.c_extra[b * NA + k];
+    eqe[kk] = corner;
+    epe[kk] = p + t.rho_reg;
+  }
+  __syncthreads();
+
+  // phase 2: contiguous runs of the blocks of steps k0 .. k0+ks-1
+  const long long ss = (long long)s * s, base = (b * a.nbuild + k0);
+  T* Qo = a.Q_aug + base * ss;
+  T* To = a.QT_aug + base * ss;
+  T* Ao = a.A_aug + base * ss;
+  T* Bo = a.B_aug + base * s * m;
+  const T* cx = t.qx_extra ? t.qx_extra + (b * NA + k0) * n : nullptr;
+  const int tot = ks * s * s;
+  for (int idx = tid; idx < tot; idx += TPB) {
+    const int q = idx / (s * s), r = idx - q * s * s, ii = r / s, jj = r - ii * s;
+    const int kq = k0 + q;
+    T vq, vt, va;
+    if (ii < n && jj < n) {
+      // _sym(Q) + q_reg I (+ _sym(cxx)); the final _sym of the block is exact
+      vq = T(0.5) * (Q[ii * n + jj] + Q[jj * n + ii]) + (ii == jj ? t.q_reg : T(0));
+      if (t.qxx_extra) {
+        const T* X = t.qxx_extra + (b * NA + kq) * n * n;
+        vq += T(0.5) * (X[ii * n + jj] + X[jj * n + ii]);
+      }
+      vt = P[ii * n + jj];
+      va = t.A[((b * NA + kq) * n + ii) * n + jj];
+    } else if (ii < n) {  // last column: Q e (+ cx)
+      vq = cx ? qe[q][ii] + cx[q * n + ii] : qe[q][ii];
+      vt = pe[q][ii];
+      va = at[q][ii];
+    } else if (jj < n) {  // last row
+      vq = cx ? qe[q][jj] + cx[q * n + jj] : qe[q][jj];
+      vt = pe[q][jj];
+      va = T(0);
+    } else {
+      vq = eqe[q];
+      vt = epe[q];
+      va = T(1);
+    }
+    Qo[idx] = vq;
+    To[idx] = vt;
+    Ao[idx] = va;
+  }
+  const int totb = ks * s * m;
+  for (int idx = tid; idx < totb; idx += TPB) {
+    const int q = idx / (s * m), r = idx - q * s * m, ii = r / m, jj = r - ii * m;
+    Bo[idx] = ii < n ? t.Bm[((b * NA + k0 + q) * n + ii) * m + jj] : T(0);
+  }
+}
+
+}  // namespace aug
+
+template <class T>
+hipError_t dispatch_augment(const AugArgs<T>& a, hipStream_t stream) {
+  const long long nchunk = (a.nbuild + aug::KS - 1) / aug::KS;
+  const long long blocks = a.batch * nchunk;
+  if (blocks <= 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFll) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(aug::augment_kernel<T>, dim3((unsigned)blocks), dim3(aug::TPB), 0, stream,
+                     a);
+  return hipGetLastError();
+}
+
+template hipError_t dispatch_augment<double>(const AugArgs<double>&, hipStream_t);
+template hipError_t dispatch_augment<float>(const AugArgs<float>&, hipStream_t);
+
+}  // namespace hop

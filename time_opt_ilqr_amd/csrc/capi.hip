@@ -52,13 +52,14 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
               int32_t r_inv, const T* QT, const T* z0, int64_t z_bs, int64_t batch,
               int32_t n_alloc, int32_t n_use, int32_t s, int32_t m, int32_t max_tries,
               int32_t t_min, int32_t t_max, T* J, int32_t* status, int32_t* t_star, T* j_star,
-              T* dbg_efg, T* dbg_pre, void* stream) {
+              T* dbg_efg, T* dbg_pre, void* stream,
+              const hop::TrajArgs<T>* traj = nullptr) {
   if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
   if (n_use <= 0 || batch == 0) return HOP_OK;  // reference: empty J
   if (s < 1 || s > HOP_MAX_DIM) return fail(HOP_E_SIZE, "s must be in [1, 16]");
   if (m < 1 || m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
   if (n_use > n_alloc) return fail(HOP_E_ARG, "n_use > n_alloc (reference IndexError)");
-  if (!A || !B || !Q || !R || !QT || !z0 || !J || !status)
+  if ((!traj && (!A || !B || !Q || !QT || !z0)) || !R || !J || !status)
     return fail(HOP_E_ARG, "null input/output pointer");
   if (r_bs < 0 || r_ks < 0 || z_bs < 0) return fail(HOP_E_ARG, "negative stride");
   if (max_tries < 0 || max_tries > 64) return fail(HOP_E_ARG, "max_tries out of range");
@@ -67,7 +68,7 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
       return fail(HOP_E_ARG, "need 1 <= t_min <= t_max <= n_use for the fused argmin");
     if (!t_star || !j_star) return fail(HOP_E_ARG, "t_star/j_star required when t_max > 0");
   }
-  hop::LftArgs<T> a;
+  hop::LftArgs<T> a{};
   a.A = A; a.B = B; a.Q = Q; a.R = R; a.QT = QT; a.z0 = z0;
   a.r_bstride = r_bs; a.r_kstride = r_ks; a.z_bstride = z_bs;
   a.batch = batch; a.nalloc = n_alloc; a.n = n_use; a.s = s; a.m = m;
@@ -75,6 +76,12 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
   a.t_min = t_min; a.t_max = t_max;
   a.J = J; a.status = status; a.t_star = t_star; a.j_star = j_star;
   a.dbg_efg = dbg_efg; a.dbg_pre = dbg_pre;
+  if (traj) {  // in-kernel augmentation: only the fused fast path implements it
+    a.traj = 1;
+    a.tr = *traj;
+    if constexpr (sizeof(T) == 8) return hip_status(hop::dispatch_lft_v2(a, (hipStream_t)stream));
+    return fail(HOP_E_SIZE, "no fused trajectory-form sweep for this shape");
+  }
   if (!getenv("HOP_FORCE_GENERIC")) {
     if constexpr (sizeof(T) == 8) {
       const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
@@ -131,6 +138,100 @@ int riccati_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, 
   a.reg_max_tries = reg_max_tries; a.max_tries = 8; a.wrap_mask = wrap_mask; a.w_stage = w_stage;
   a.K = K; a.k = k; a.Vxx = Vxx; a.Vx = Vx; a.V0 = V0; a.status = status;
   return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
+}
+
+// ---- trajectory form (augmented.py:10-87 on the device) -------------------
+template <class T>
+int traj_check(const hop::TrajArgs<T>& t, int64_t batch, int32_t n_alloc, int32_t n_build) {
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (t.n < 1 || t.n + 1 > HOP_MAX_DIM) return fail(HOP_E_SIZE, "n must be in [1, 15]");
+  if (t.m < 1 || t.m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
+  if (n_build > n_alloc) return fail(HOP_E_ARG, "n_use > n_alloc (reference IndexError)");
+  if (!t.A || !t.Bm || !t.ares || !t.X || !t.U || !t.xg || !t.u_ref || !t.Q || !t.P || !t.w)
+    return fail(HOP_E_ARG, "null input pointer");
+  if (t.xg_bs < 0 || t.ur_bs < 0 || t.q_bs < 0 || t.p_bs < 0 || t.w_bs < 0)
+    return fail(HOP_E_ARG, "negative stride");
+  if ((t.wrap_mask >> t.n) != 0u) return fail(HOP_E_ARG, "wrap_mask names a state >= n");
+  return HOP_OK;
+}
+
+template <class T>
+hop::TrajArgs<T> traj_args(const T* A, const T* Bm, const T* a_res, const T* X, const T* U,
+                           const T* xg, int64_t xg_bs, const T* u_ref, int64_t ur_bs,
+                           const T* Q, int64_t q_bs, const T* P, int64_t p_bs, const T* w,
+                           int64_t w_bs, const T* qxx_extra, const T* qx_extra,
+                           const T* c_extra, uint32_t wrap_mask, T q_reg, T rho_reg, int32_t n,
+                           int32_t m) {
+  hop::TrajArgs<T> t{};
+  t.A = A; t.Bm = Bm; t.ares = a_res; t.X = X; t.U = U; t.xg = xg; t.u_ref = u_ref;
+  t.Q = Q; t.P = P; t.w = w; t.qxx_extra = qxx_extra; t.qx_extra = qx_extra;
+  t.c_extra = c_extra; t.xg_bs = xg_bs; t.ur_bs = ur_bs; t.q_bs = q_bs; t.p_bs = p_bs;
+  t.w_bs = w_bs; t.wrap_mask = wrap_mask; t.q_reg = q_reg; t.rho_reg = rho_reg;
+  t.n = n; t.m = m;
+  return t;
+}
+
+// the sweep builds the blocks itself (no workspace) for these shapes
+bool traj_fused(int32_t n, int32_t m, int32_t elem_bytes, bool has_extra) {
+  if (getenv("HOP_FORCE_GENERIC") || getenv("HOP_TRAJ_UNFUSED")) return false;
+  return elem_bytes == 8 && n == 12 && m == 4 && !has_extra;
+}
+
+constexpr int64_t kWsAlign = 256;
+int64_t ws_round(int64_t b) { return (b + kWsAlign - 1) / kWsAlign * kWsAlign; }
+
+// workspace of the unfused path: A_aug, B_aug, Q_aug, QT_aug ([batch][n_use]) and z0
+int64_t traj_ws_bytes(int64_t batch, int32_t n_use, int32_t n, int32_t m, int32_t elem) {
+  const int64_t s = n + 1, steps = batch * (int64_t)n_use;
+  return 3 * ws_round(steps * s * s * elem) + ws_round(steps * s * m * elem) + ws_round(s * elem);
+}
+
+template <class T>
+int augment_entry(const hop::TrajArgs<T>& t, int64_t batch, int32_t n_alloc, int32_t n_build,
+                  T* A_aug, T* B_aug, T* Q_aug, T* QT_aug, T* z0, void* stream) {
+  const int rc = traj_check(t, batch, n_alloc, n_build);
+  if (rc != HOP_OK) return rc;
+  if (batch == 0 || n_build <= 0) return HOP_OK;
+  if (!A_aug || !B_aug || !Q_aug || !QT_aug) return fail(HOP_E_ARG, "null output pointer");
+  hop::AugArgs<T> a{};
+  a.t = t; a.batch = batch; a.nalloc = n_alloc; a.nbuild = n_build;
+  a.A_aug = A_aug; a.B_aug = B_aug; a.Q_aug = Q_aug; a.QT_aug = QT_aug; a.z0 = z0;
+  return hip_status(hop::dispatch_augment<T>(a, (hipStream_t)stream));
+}
+
+template <class T>
+int lft_traj_entry(const hop::TrajArgs<T>& t, const T* R_inv, int64_t r_bs, int64_t batch,
+                   int32_t n_alloc, int32_t n_use, int32_t max_tries, int32_t t_min,
+                   int32_t t_max, T* J, int32_t* status, int32_t* t_star, T* j_star,
+                   void* workspace, int64_t workspace_bytes, void* stream) {
+  int rc = traj_check(t, batch, n_alloc, n_use);
+  if (rc != HOP_OK) return rc;
+  if (n_use <= 0 || batch == 0) return HOP_OK;
+  if (!R_inv) return fail(HOP_E_ARG, "null R_inv");
+  const int32_t n = t.n, m = t.m, s = n + 1;
+  const bool extra = t.qxx_extra || t.qx_extra || t.c_extra;
+  if (traj_fused(n, m, (int32_t)sizeof(T), extra)) {
+    // the augmented blocks never touch HBM: the sweep builds them per step
+    return lft_entry<T>(nullptr, nullptr, nullptr, R_inv, r_bs, 0, 1, nullptr, nullptr, 0,
+                        batch, n_alloc, n_use, s, m, max_tries, t_min, t_max, J, status,
+                        t_star, j_star, nullptr, nullptr, stream, &t);
+  }
+  const int64_t need = traj_ws_bytes(batch, n_use, n, m, (int32_t)sizeof(T));
+  if (!workspace || workspace_bytes < need)
+    return fail(HOP_E_ARG, "workspace too small (hop_lft_sweep_traj_workspace_bytes)");
+  if (((uintptr_t)workspace) % kWsAlign != 0) return fail(HOP_E_ARG, "workspace not 256-B aligned");
+  const int64_t steps = batch * (int64_t)n_use;
+  unsigned char* p = (unsigned char*)workspace;
+  T* Aa = (T*)p; p += ws_round(steps * s * s * sizeof(T));
+  T* Qa = (T*)p; p += ws_round(steps * s * s * sizeof(T));
+  T* Ta = (T*)p; p += ws_round(steps * s * s * sizeof(T));
+  T* Ba = (T*)p; p += ws_round(steps * s * m * sizeof(T));
+  T* z0 = (T*)p;
+  rc = augment_entry<T>(t, batch, n_alloc, n_use, Aa, Ba, Qa, Ta, z0, stream);
+  if (rc != HOP_OK) return rc;
+  return lft_entry<T>(Aa, Ba, Qa, R_inv, r_bs, 0, 1, Ta, z0, 0, batch, n_use, n_use, s, m,
+                      max_tries, t_min, t_max, J, status, t_star, j_star, nullptr, nullptr,
+                      stream);
 }
 
 }  // namespace
@@ -196,6 +297,74 @@ int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float
                               qxx_extra, qx_extra, c_extra, horizon, lm, w_stage, wrap_mask,
                               mode, reg_max_tries, batch, n_alloc, n, m, K, k, Vxx, Vx, V0,
                               status, stream);
+}
+
+int hop_augment_f64(const double* A, const double* Bm, const double* a_res, const double* X,
+                    const double* U, const double* xg, int64_t xg_bs, const double* u_ref,
+                    int64_t ur_bs, const double* Q, int64_t q_bs, const double* P, int64_t p_bs,
+                    const double* w, int64_t w_bs, const double* qxx_extra,
+                    const double* qx_extra, const double* c_extra, uint32_t wrap_mask,
+                    double q_reg, double rho_reg, int64_t batch, int32_t n_alloc,
+                    int32_t n_build, int32_t n, int32_t m, double* A_aug, double* B_aug,
+                    double* Q_aug, double* QT_aug, double* z0, void* stream) {
+  return augment_entry<double>(
+      traj_args<double>(A, Bm, a_res, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, P, p_bs, w, w_bs,
+                        qxx_extra, qx_extra, c_extra, wrap_mask, q_reg, rho_reg, n, m),
+      batch, n_alloc, n_build, A_aug, B_aug, Q_aug, QT_aug, z0, stream);
+}
+int hop_augment_f32(const float* A, const float* Bm, const float* a_res, const float* X,
+                    const float* U, const float* xg, int64_t xg_bs, const float* u_ref,
+                    int64_t ur_bs, const float* Q, int64_t q_bs, const float* P, int64_t p_bs,
+                    const float* w, int64_t w_bs, const float* qxx_extra, const float* qx_extra,
+                    const float* c_extra, uint32_t wrap_mask, float q_reg, float rho_reg,
+                    int64_t batch, int32_t n_alloc, int32_t n_build, int32_t n, int32_t m,
+                    float* A_aug, float* B_aug, float* Q_aug, float* QT_aug, float* z0,
+                    void* stream) {
+  return augment_entry<float>(
+      traj_args<float>(A, Bm, a_res, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, P, p_bs, w, w_bs,
+                       qxx_extra, qx_extra, c_extra, wrap_mask, q_reg, rho_reg, n, m),
+      batch, n_alloc, n_build, A_aug, B_aug, Q_aug, QT_aug, z0, stream);
+}
+
+int64_t hop_lft_sweep_traj_workspace_bytes(int64_t batch, int32_t n_use, int32_t n, int32_t m,
+                                           int32_t elem_bytes, int32_t has_extra) {
+  if (batch <= 0 || n_use <= 0) return 0;
+  if (traj_fused(n, m, elem_bytes, has_extra != 0)) return 0;
+  return traj_ws_bytes(batch, n_use, n, m, elem_bytes);
+}
+
+int hop_lft_sweep_traj_f64(const double* A, const double* Bm, const double* a_res,
+                           const double* X, const double* U, const double* xg, int64_t xg_bs,
+                           const double* u_ref, int64_t ur_bs, const double* Q, int64_t q_bs,
+                           const double* P, int64_t p_bs, const double* w, int64_t w_bs,
+                           const double* qxx_extra, const double* qx_extra,
+                           const double* c_extra, uint32_t wrap_mask, double q_reg,
+                           double rho_reg, const double* R_inv, int64_t r_bs, int64_t batch,
+                           int32_t n_alloc, int32_t n_use, int32_t n, int32_t m,
+                           int32_t max_tries, int32_t t_min, int32_t t_max, double* J,
+                           int32_t* status, int32_t* t_star, double* j_star, void* workspace,
+                           int64_t workspace_bytes, void* stream) {
+  return lft_traj_entry<double>(
+      traj_args<double>(A, Bm, a_res, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, P, p_bs, w, w_bs,
+                        qxx_extra, qx_extra, c_extra, wrap_mask, q_reg, rho_reg, n, m),
+      R_inv, r_bs, batch, n_alloc, n_use, max_tries, t_min, t_max, J, status, t_star, j_star,
+      workspace, workspace_bytes, stream);
+}
+int hop_lft_sweep_traj_f32(const float* A, const float* Bm, const float* a_res, const float* X,
+                           const float* U, const float* xg, int64_t xg_bs, const float* u_ref,
+                           int64_t ur_bs, const float* Q, int64_t q_bs, const float* P,
+                           int64_t p_bs, const float* w, int64_t w_bs, const float* qxx_extra,
+                           const float* qx_extra, const float* c_extra, uint32_t wrap_mask,
+                           float q_reg, float rho_reg, const float* R_inv, int64_t r_bs,
+                           int64_t batch, int32_t n_alloc, int32_t n_use, int32_t n, int32_t m,
+                           int32_t max_tries, int32_t t_min, int32_t t_max, float* J,
+                           int32_t* status, int32_t* t_star, float* j_star, void* workspace,
+                           int64_t workspace_bytes, void* stream) {
+  return lft_traj_entry<float>(
+      traj_args<float>(A, Bm, a_res, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, P, p_bs, w, w_bs,
+                       qxx_extra, qx_extra, c_extra, wrap_mask, q_reg, rho_reg, n, m),
+      R_inv, r_bs, batch, n_alloc, n_use, max_tries, t_min, t_max, J, status, t_star, j_star,
+      workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -40,6 +40,21 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// wrap_error (utils.py:131-137) on one component
+template <class T>
+__device__ __forceinline__ T wrap_angle(T a) {
+  // NumPy: (a + pi) % (2 pi) - pi  (np.remainder: fmod, then shift into [0, 2pi))
+  const T two_pi = T(2.0 * 3.141592653589793);
+  const T pi = T(3.141592653589793);
+  T r = fmod(a + pi, two_pi);
+  if (r != T(0)) {
+    if (r < T(0)) r += two_pi;
+  } else {
+    r = T(0);
+  }
+  return r - pi;
+}
+
 template <class T, int S>
 __device__ __forceinline__ void zero(T (&x)[S]) {
 #pragma unroll

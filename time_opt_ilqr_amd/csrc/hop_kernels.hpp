@@ -5,6 +5,41 @@
 
 namespace hop {
 
+// Trajectory form of the LFT inputs (augmented.py:10-87 done on the device):
+// the raw linearisation and cost terms the augmented blocks are built from.
+template <class T>
+struct TrajArgs {
+  const T* A;      // [B][nalloc][n][n]
+  const T* Bm;     // [B][nalloc][n][m]
+  const T* ares;   // [B][nalloc][n]    a_k = F(x_k, u_k) - x_{k+1}
+  const T* X;      // [B][nalloc+1][n]
+  const T* U;      // [B][nalloc][m]
+  const T* xg;     // [B or 1][n]
+  const T* u_ref;  // [B or 1][m]
+  const T* Q;      // [B or 1][n][n]   stage weight (raw; _sym'd in the builder)
+  const T* P;      // [B or 1][n][n]   _sym(as_terminal_weight(alpha))
+  const T* w;      // [B or 1]         time weight
+  const T* qxx_extra;  // [B][nalloc][n][n] or null (extra_stage_cost)
+  const T* qx_extra;   // [B][nalloc][n] or null
+  const T* c_extra;    // [B][nalloc] or null
+  long long xg_bs, ur_bs, q_bs, p_bs, w_bs;
+  unsigned wrap_mask;
+  T q_reg, rho_reg;
+  int n, m;
+};
+
+template <class T>
+struct AugArgs {
+  TrajArgs<T> t;
+  long long batch;
+  int nalloc, nbuild;
+  T* A_aug;   // [B][nbuild][s][s]
+  T* B_aug;   // [B][nbuild][s][m]
+  T* Q_aug;   // [B][nbuild][s][s]
+  T* QT_aug;  // [B][nbuild][s][s]
+  T* z0;      // [s] or null: z0 = e_s (augmented.py:57)
+};
+
 template <class T>
 struct LftArgs {
   const T* A;    // [B][nalloc][s][s]   augmented A_k
@@ -23,6 +58,8 @@ struct LftArgs {
   T* j_star;         // [B] or null
   T* dbg_efg;        // [B][n][3][s][s] or null  (E_k, F_k, G_k)
   T* dbg_pre;        // [B][n][3][s][s] or null  (Ebar_k, Fbar_k, Gbar_k)
+  int traj;          // 1: A/B/Q/QT unused, blocks built in-kernel from `tr`
+  TrajArgs<T> tr;
 };
 
 template <class T>
@@ -61,6 +98,8 @@ template <class T>
 hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_lft_small_noslp(const LftArgs<T>& a, hipStream_t stream);
+template <class T>
+hipError_t dispatch_augment(const AugArgs<T>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream);
 

@@ -98,6 +98,16 @@ struct SchedLdl2Stamped : SchedLdl2 {
 struct SchedStamped : SchedLdl {
   static constexpr int STAMP = 1;
 };
+// trajectory form: the augmented blocks are built in LDS from the raw
+// linearisation each step (augmented.py:10-87), see the TRAJ paths below
+struct SchedLdlTraj : SchedLdl {
+  static constexpr int TRAJ = 1;
+};
+template <class C>
+constexpr bool has_traj() {
+  if constexpr (requires { C::TRAJ; }) return C::TRAJ != 0;
+  return false;
+}
 template <class C>
 constexpr bool offset_form() {
   return C::PIV == 4 || C::PIV == 5;
@@ -566,17 +576,46 @@ struct Geo {
   // has_cldl: a second tile set parks QT^-1 (NX) across the compose
   static constexpr int OFF_X = OFF_T + TILE_W;
   static constexpr int WAVE_BYTES_X = OFF_X + TILE_W;
+  // trajectory form (n = S-1): raw A_k staged in the A image area, raw B_k in
+  // the B area, then x_k|x_{k+1}, a_k and u_k after the tiles.  Per problem the
+  // staged block of a piece type is CH 16-B chunks at 16 CH g.
+  static constexpr int NN = S - 1;
+  static constexpr int CHA = (NN * NN * 8 + 15) / 16, NJA = (kProbPerWave * CHA + 63) / 64;
+  static constexpr int CHR = (NN * MM * 8 + 15) / 16, NJR = (kProbPerWave * CHR + 63) / 64;
+  static constexpr int CHX = (2 * NN * 8 + 15) / 16, NJX = (kProbPerWave * CHX + 63) / 64;
+  static constexpr int CHV = (NN * 8 + 15) / 16, NJV = (kProbPerWave * CHV + 63) / 64;
+  static constexpr int CHU = (MM * 8 + 15) / 16, NJU = (kProbPerWave * CHU + 63) / 64;
+  static_assert(NJA <= NJM && NJR <= NJB, "raw blocks must fit the augmented image areas");
+  static constexpr int OFF_VX = OFF_T + TILE_W, OFF_VA = OFF_VX + 1024 * NJX,
+                       OFF_VU = OFF_VA + 1024 * NJV;
+  // raw Q of the wave's problems, transposed (lane c reads its row as a column)
+  static constexpr int OFF_CQ = OFF_VU + 1024 * NJU;
+  static constexpr int WAVE_BYTES_T = OFF_CQ + kProbPerWave * NN * NN * 8;
 };
+
+// per-lane DMA source offset of piece j: lane q = 64 j + lane carries chunk
+// q % CH of problem q / CH of the wave (OOB sentinel for unused lanes)
+template <int CH>
+__device__ __forceinline__ unsigned chunk_voff(int j, int lane, long long wave_prob0,
+                                               long long pb0, long long batch, long long pstr) {
+  const int q = 64 * j + lane;
+  const int p = q / CH, r = q % CH;
+  const long long pe = wave_prob0 + p < batch ? wave_prob0 + p : batch - 1;
+  return (q < kProbPerWave * CH) ? (unsigned)((pe - pb0) * pstr + r * 16) : 0x7FFFFFFFu;
+}
 
 template <class C, int S, int MM>
 __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a) {
   using G = Geo<S, MM>;
   constexpr bool OFF = offset_form<C>();
+  constexpr bool TRAJ = has_traj<C>();
+  static_assert(!TRAJ || (OFF && C::ELIM && !has_cldl<C>()), "trajectory form: SchedLdl family");
+  constexpr int NN = G::NN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int WB = has_cldl<C>() ? G::WAVE_BYTES_X : G::WAVE_BYTES;
+  constexpr int WB = has_cldl<C>() ? G::WAVE_BYTES_X : (TRAJ ? G::WAVE_BYTES_T : G::WAVE_BYTES);
   unsigned char* wbase = smem_raw + w * WB;
   const unsigned wlds = (unsigned)(uintptr_t)wbase;  // LDS byte address (wave-uniform)
   double* tile = reinterpret_cast<double*>(wbase + G::OFF_T) + g * kLdsTile;
@@ -607,8 +646,15 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     return __builtin_amdgcn_make_buffer_rsrc(
         const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rQ = mk(a.Q, pstrM), rA = mk(a.A, pstrM), rT = mk(a.QT, pstrM),
-                               rB = mk(a.B, pstrB);
+  // augmented form: Q, A, QT, B images; trajectory form: A, B, x, a, u pieces
+  const long long pstA = (long long)a.nalloc * NN * NN * 8, pstR = (long long)a.nalloc * NN * MM * 8;
+  const long long pstX = (long long)(a.nalloc + 1) * NN * 8, pstV = (long long)a.nalloc * NN * 8;
+  const long long pstU = (long long)a.nalloc * MM * 8;
+  const __amdgpu_buffer_rsrc_t rQ = TRAJ ? mk(a.tr.A, pstA) : mk(a.Q, pstrM),
+                               rA = TRAJ ? mk(a.tr.Bm, pstR) : mk(a.A, pstrM),
+                               rT = TRAJ ? mk(a.tr.X, pstX) : mk(a.QT, pstrM),
+                               rB = TRAJ ? mk(a.tr.ares, pstV) : mk(a.B, pstrB),
+                               rU = TRAJ ? mk(a.tr.U, pstU) : rB;
   // per-lane chunk offsets (static over steps)
   unsigned voM[G::NJM], voB[G::NJB];
 #pragma unroll
@@ -625,7 +671,40 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     long long pe = wave_prob0 + p < a.batch ? wave_prob0 + p : a.batch - 1;
     voB[j] = (q < kProbPerWave * G::CHB) ? (unsigned)((pe - pb0) * pstrB + r * 16) : 0x7FFFFFFFu;
   }
+  unsigned voTA[G::NJA], voTR[G::NJR], voTX[G::NJX], voTV[G::NJV], voTU[G::NJU];
+  if constexpr (TRAJ) {
+#pragma unroll
+    for (int j = 0; j < G::NJA; ++j)
+      voTA[j] = chunk_voff<G::CHA>(j, lane, wave_prob0, pb0, a.batch, pstA);
+#pragma unroll
+    for (int j = 0; j < G::NJR; ++j)
+      voTR[j] = chunk_voff<G::CHR>(j, lane, wave_prob0, pb0, a.batch, pstR);
+#pragma unroll
+    for (int j = 0; j < G::NJX; ++j)
+      voTX[j] = chunk_voff<G::CHX>(j, lane, wave_prob0, pb0, a.batch, pstX);
+#pragma unroll
+    for (int j = 0; j < G::NJV; ++j)
+      voTV[j] = chunk_voff<G::CHV>(j, lane, wave_prob0, pb0, a.batch, pstV);
+#pragma unroll
+    for (int j = 0; j < G::NJU; ++j)
+      voTU[j] = chunk_voff<G::CHU>(j, lane, wave_prob0, pb0, a.batch, pstU);
+  }
   auto dma_step = [&](int k) {  // Q, A, B, QT of step k
+    if constexpr (TRAJ) {  // A_k, B_k, x_k|x_{k+1}, a_k, u_k
+      const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
+                     soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
+#pragma unroll
+      for (int j = 0; j < G::NJA; ++j) dma16(voTA[j], rQ, wlds + G::OFF_A + 1024 * j, soA);
+#pragma unroll
+      for (int j = 0; j < G::NJR; ++j) dma16(voTR[j], rA, wlds + G::OFF_B + 1024 * j, soR);
+#pragma unroll
+      for (int j = 0; j < G::NJX; ++j) dma16(voTX[j], rT, wlds + G::OFF_VX + 1024 * j, soV);
+#pragma unroll
+      for (int j = 0; j < G::NJV; ++j) dma16(voTV[j], rB, wlds + G::OFF_VA + 1024 * j, soV);
+#pragma unroll
+      for (int j = 0; j < G::NJU; ++j) dma16(voTU[j], rU, wlds + G::OFF_VU + 1024 * j, soU);
+      return;
+    }
     const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
 #pragma unroll
     for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rQ, wlds + G::OFF_Q + 1024 * j, soM);
@@ -643,7 +722,39 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   if constexpr (C::ELIM) {  // tile row S holds z0 (lane S of Ebar / X0, see quad_inverse)
     static_assert(S < kRowLanes, "bordered elimination needs a free lane");
     wave_sync();  // the zeroing loop wrote these words from other lanes
-    if (c < S) tile[S * kLdsRow + c] = zp[c];
+    if (c < S) tile[S * kLdsRow + c] = TRAJ ? (c == NN ? 1.0 : 0.0) : zp[c];  // z0 = e_s
+  }
+  // trajectory form: per-lane constants and the constant parts of the Q / QT images
+  double xg_c = 0.0, ur_c = 0.0, w2 = 0.0, qdiag = 0.0, pdiag = 0.0, pcc = 0.0;
+  bool wrap_c = false;
+  double* cq = reinterpret_cast<double*>(wbase + G::OFF_CQ) + g * NN * NN;
+  if constexpr (TRAJ) {
+    const TrajArgs<double>& t = a.tr;
+    const double* Qg = t.Q + pb * t.q_bs;
+    const double* Pg = t.P + pb * t.p_bs;
+    const int cc = c < NN ? c : 0;
+    if (c < NN) {  // raw Q (Q e, augmented.py:35), transposed
+#pragma unroll
+      for (int j = 0; j < NN; ++j) cq[j * NN + c] = Qg[c * NN + j];
+    }
+    pcc = Pg[cc * NN + cc];
+    xg_c = c < NN ? t.xg[pb * t.xg_bs + cc] : 0.0;
+    ur_c = c < MM ? t.u_ref[pb * t.ur_bs + (c < MM ? c : 0)] : 0.0;
+    w2 = 2.0 * t.w[pb * t.w_bs];
+    wrap_c = c < NN && ((t.wrap_mask >> c) & 1u);
+    // diagonals with chol_inv's first jitter and the offset form folded in
+    // (the value the augmented path reaches with diag_add)
+    qdiag = (0.5 * (Qg[cc * NN + cc] + Qg[cc * NN + cc]) + t.q_reg) + (1e-9 - 1.0);
+    pdiag = Pg[cc * NN + cc] + (1e-9 - 1.0);
+    double* wq = const_cast<double*>(imQ);
+    double* wt = const_cast<double*>(imT);
+    if (c < NN) {  // column c: _sym(Q) + q_reg I, and P (augmented.py:33, 82)
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        wq[i * S + c] = 0.5 * (Qg[i * NN + c] + Qg[c * NN + i]) + (i == c ? t.q_reg : 0.0);
+        wt[i * S + c] = Pg[i * NN + c];
+      }
+    }
   }
   unsigned st = 0;
   // R^-1 (cached, shared or per problem) as columns on lanes 0..MM-1
@@ -680,7 +791,58 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     // J of the previous step is stored only now, so that the vmcnt(0) above
     // never waits on a store issued at the end of the previous step
     if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
-    if constexpr (OFF) {
+    double atil = 0.0;  // trajectory form: a~_k = a_k - B_k du_k (augmented.py:50)
+    if constexpr (TRAJ) {
+      // build the last row / column and the diagonal of Q_aug[k] (augmented.py:31-47)
+      // and QT_aug[k] (augmented.py:77-86) in the images; the rest is constant
+      const double* sX = reinterpret_cast<const double*>(wbase + G::OFF_VX) + g * 2 * G::CHX;
+      const double* sV = reinterpret_cast<const double*>(wbase + G::OFF_VA) + g * 2 * G::CHV;
+      const double* sU = reinterpret_cast<const double*>(wbase + G::OFF_VU) + g * 2 * G::CHU;
+      const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
+      const int cc = c < NN ? c : 0;
+      double e = c < NN ? sX[cc] - xg_c : 0.0;
+      double e1 = c < NN ? sX[NN + cc] - xg_c : 0.0;
+      if (wrap_c) {
+        e = wrap_angle(e);
+        e1 = wrap_angle(e1);
+      }
+      const double du = c < MM ? sU[c < MM ? c : 0] - ur_c : 0.0;
+      double rb[MM];
+#pragma unroll
+      for (int q = 0; q < MM; ++q) rb[q] = c < NN ? sR[cc * MM + q] : 0.0;
+      const double av = c < NN ? sV[cc] : 0.0;
+      // row c of Q (constant area) and of P (= column c of the QT image: P is
+      // symmetric; its diagonal entry is kept in a register)
+      double qr[NN], pr[NN], ones[NN];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        qr[j] = c < NN ? cq[j * NN + cc] : 0.0;
+        pr[j] = c < NN ? (j == c ? pcc : imT[j * S + cc]) : 0.0;
+        ones[j] = 1.0;
+      }
+      double qe = 0.0, pe = 0.0, bd = 0.0;
+      LaneDot<NN>::fma(qe, e, qr);   // (Q e)[c]
+      LaneDot<NN>::fma(pe, e1, pr);  // (P e_{k+1})[c]
+      LaneDot<MM>::fma(bd, du, rb);  // (B du)[c]
+      atil = av - bd;
+      double eqe = 0.0, epe = 0.0;   // row sums by broadcast (every lane gets them)
+      LaneDot<NN>::fma(eqe, c < NN ? e * qe : 0.0, ones);
+      LaneDot<NN>::fma(epe, c < NN ? e1 * pe : 0.0, ones);
+      double* wq = const_cast<double*>(imQ);
+      double* wt = const_cast<double*>(imT);
+      if (c < NN) {
+        wq[c * S + NN] = qe;
+        wq[NN * S + c] = qe;
+        wq[c * S + c] = qdiag;
+        wt[c * S + NN] = pe;
+        wt[NN * S + c] = pe;
+        wt[c * S + c] = pdiag;
+      } else if (c == NN) {
+        wq[NN * S + NN] = ((eqe + w2) + a.tr.rho_reg) + (1e-9 - 1.0);
+        wt[NN * S + NN] = (epe + a.tr.rho_reg) + (1e-9 - 1.0);
+      }
+      wave_sync();
+    } else if constexpr (OFF) {
       diag_add<S, S>(imQ, c, 1e-9 - 1.0);
       diag_add<S, S>(imT, c, 1e-9 - 1.0);
     }
@@ -691,10 +853,21 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     stamp(1);
     if constexpr (has_cldl<C>()) lds_put(tileX, c, NX);  // own column, read back at the query
     double at[S], brow[MM];
+    if constexpr (TRAJ) {  // row c of A_aug = [[A_k, a~],[0, 1]], B_aug = [[B_k],[0]]
+      const double* sA = reinterpret_cast<const double*>(wbase + G::OFF_A) + g * 2 * G::CHA;
+      const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
+      const int cc = c < NN ? c : 0;
 #pragma unroll
-    for (int j = 0; j < S; ++j) at[j] = imA[c * S + j];   // row c of A
+      for (int j = 0; j < NN; ++j) at[j] = c < NN ? sA[cc * NN + j] : 0.0;
+      at[NN] = c < NN ? atil : (c == NN ? 1.0 : 0.0);
 #pragma unroll
-    for (int j = 0; j < MM; ++j) brow[j] = imB[c * MM + j];
+      for (int j = 0; j < MM; ++j) brow[j] = c < NN ? sR[cc * MM + j] : 0.0;
+    } else {
+#pragma unroll
+      for (int j = 0; j < S; ++j) at[j] = imA[c * S + j];   // row c of A
+#pragma unroll
+      for (int j = 0; j < MM; ++j) brow[j] = imB[c * MM + j];
+    }
     wave_sync();
     if (k + 1 < N) dma_step(k + 1);
     stamp(2);
@@ -862,6 +1035,14 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 // exact-size fast path: returns hipErrorNotSupported when the shape has none
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv) return hipErrorNotSupported;
+  if (a.traj) {  // in-kernel augmentation (capi routes only s = 13, m = 4 here)
+    if (a.s != 13 || a.m != 4 || a.tr.n != 12 || a.tr.m != 4) return hipErrorNotSupported;
+    const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+    hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>), dim3((unsigned)blocks),
+                       dim3(256), (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock), stream,
+                       a);
+    return hipGetLastError();
+  }
   auto go = [&](auto kern, int bytes) {
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);

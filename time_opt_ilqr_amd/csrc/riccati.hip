@@ -14,20 +14,6 @@
 
 namespace hop {
 
-template <class T>
-__device__ __forceinline__ T wrap_angle(T a) {
-  // NumPy: (a + pi) % (2 pi) - pi  (np.remainder: fmod, then shift into [0, 2pi))
-  const T two_pi = T(2.0 * 3.141592653589793);
-  const T pi = T(3.141592653589793);
-  T r = fmod(a + pi, two_pi);
-  if (r != T(0)) {
-    if (r < T(0)) r += two_pi;
-  } else {
-    r = T(0);
-  }
-  return r - pi;
-}
-
 template <class T, int S>
 __device__ __forceinline__ void rload_col(const T* M, int rows, int cols, int c, T pad, T (&x)[S]) {
   // column c of a rows x cols row-major matrix, identity(pad)/zero padded

@@ -214,3 +214,138 @@ def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
         _lib.stream_handle(dev))
     _lib.check(rc)
     return RiccatiResult(K, k, status, Vxx, Vx, V0)
+
+
+# ---------------------------------------------------------------------------
+# trajectory form: augmented.py:10-87 on the device (+ the fused sweep)
+# ---------------------------------------------------------------------------
+@dataclass
+class AugmentedBlocks:
+    A: "object"   # [B, N, s, s]
+    B: "object"   # [B, N, s, m]
+    Q: "object"   # [B, N, s, s]
+    QT: "object"  # [B, N, s, s]  (QT[t-1] <-> horizon t)
+    z0: "object"  # [s] = e_s
+
+
+def _traj_args(A, Bm, a_res, X, U, xg, u_ref, Q, P, w, wrap_idx, q_reg, rho_reg,
+               qxx_extra, qx_extra, c_extra):
+    """Validate the trajectory-form inputs; returns (args, dims, keepalive)."""
+    torch = _torch()
+    dt = A.dtype
+    A = _dev(A, "A", dt)
+    dev = A.device
+    if A.dim() != 4 or A.shape[-1] != A.shape[-2]:
+        raise ValueError(f"A must be [B, N, n, n], got {tuple(A.shape)}")
+    Bn, N, n, _ = A.shape
+    Bm = _dev(Bm, "Bm", dt, dev)
+    m = Bm.shape[-1]
+    if tuple(Bm.shape) != (Bn, N, n, m):
+        raise ValueError(f"Bm must be [B, N, n, m], got {tuple(Bm.shape)}")
+    a_res = _dev(a_res, "a_res", dt, dev)
+    X = _dev(X, "X", dt, dev)
+    U = _dev(U, "U", dt, dev)
+    if tuple(a_res.shape) != (Bn, N, n):
+        raise ValueError("a_res must be [B, N, n]")
+    if tuple(X.shape) != (Bn, N + 1, n) or tuple(U.shape) != (Bn, N, m):
+        raise ValueError("X must be [B, N+1, n] and U [B, N, m]")
+    xg = _dev(xg, "xg", dt, dev)
+    u_ref = _dev(u_ref, "u_ref", dt, dev)
+    Q = _dev(Q, "Q", dt, dev)
+    P = _dev(P, "P", dt, dev)
+    w = _dev(torch.as_tensor(w, dtype=dt, device=dev).reshape(-1), "w", dt, dev)
+    if w.numel() not in (1, Bn):
+        raise ValueError("w must be a scalar or [B]")
+    ex = [None if t is None else _dev(t, nm, dt, dev)
+          for t, nm in ((qxx_extra, "qxx_extra"), (qx_extra, "qx_extra"), (c_extra, "c_extra"))]
+    if ex[0] is not None and tuple(ex[0].shape) != (Bn, N, n, n):
+        raise ValueError("qxx_extra must be [B, N, n, n]")
+    if ex[1] is not None and tuple(ex[1].shape) != (Bn, N, n):
+        raise ValueError("qx_extra must be [B, N, n]")
+    if ex[2] is not None and tuple(ex[2].shape) != (Bn, N):
+        raise ValueError("c_extra must be [B, N]")
+    args = [_lib.ptr(A), _lib.ptr(Bm), _lib.ptr(a_res), _lib.ptr(X), _lib.ptr(U),
+            _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref),
+            _bstride(u_ref, 1, "u_ref", Bn), _lib.ptr(Q), _bstride(Q, 2, "Q", Bn),
+            _lib.ptr(P), _bstride(P, 2, "P", Bn), _lib.ptr(w), 0 if w.numel() == 1 else 1,
+            _lib.ptr(ex[0]), _lib.ptr(ex[1]), _lib.ptr(ex[2]), wrap_mask(wrap_idx, n),
+            float(q_reg), float(rho_reg)]
+    keep = (A, Bm, a_res, X, U, xg, u_ref, Q, P, w, ex)
+    return args, (Bn, N, n, m, dt, dev, any(t is not None for t in ex)), keep
+
+
+def augment(A, Bm, a_res, X, U, xg, u_ref, Q, P, w, *, wrap_idx=None,
+            n_build: Optional[int] = None, q_reg: float = 1e-9, rho_reg: float = 1e-12,
+            qxx_extra=None, qx_extra=None, c_extra=None) -> AugmentedBlocks:
+    """Batched build_augmented_sequence_QR + build_terminal_aug_list (augmented.py:10-87).
+
+    A [B,N,n,n], Bm [B,N,n,m], a_res [B,N,n] (= F(x_k,u_k) - x_{k+1}), X [B,N+1,n],
+    U [B,N,m]; xg/u_ref/Q/P shared or per problem (P = _sym(as_terminal_weight(alpha)));
+    w scalar or [B].  Returns the blocks of steps 0..n_build-1 (default N).
+    """
+    torch = _torch()
+    args, (Bn, N, n, m, dt, dev, _), keep = _traj_args(
+        A, Bm, a_res, X, U, xg, u_ref, Q, P, w, wrap_idx, q_reg, rho_reg, qxx_extra, qx_extra,
+        c_extra)
+    nb = N if n_build is None else int(n_build)
+    if nb > N:
+        raise IndexError(f"n_build={nb} exceeds the {N} stages supplied")
+    s = n + 1
+    out = AugmentedBlocks(torch.empty((Bn, nb, s, s), dtype=dt, device=dev),
+                          torch.empty((Bn, nb, s, m), dtype=dt, device=dev),
+                          torch.empty((Bn, nb, s, s), dtype=dt, device=dev),
+                          torch.empty((Bn, nb, s, s), dtype=dt, device=dev),
+                          torch.empty((s,), dtype=dt, device=dev))
+    rc = _fn("hop_augment", dt)(*args, Bn, N, nb, n, m, _lib.ptr(out.A), _lib.ptr(out.B),
+                                _lib.ptr(out.Q), _lib.ptr(out.QT), _lib.ptr(out.z0),
+                                _lib.stream_handle(dev))
+    _lib.check(rc)
+    del keep
+    return out
+
+
+def propagate_traj(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, *, wrap_idx=None,
+                   n_use: Optional[int] = None, t_min: Optional[int] = None,
+                   t_max: Optional[int] = None, max_tries: int = 8, q_reg: float = 1e-9,
+                   rho_reg: float = 1e-12, qxx_extra=None, qx_extra=None,
+                   c_extra=None) -> SweepResult:
+    """The select block of solver.py:514-522 for a batch: augmented builders +
+    propagator_all_Jt_aug (+ argmin when t_max is given), from trajectory-form
+    inputs (see ``augment``).  R_inv = chol_inv(R): [m, m] or [B, m, m].
+    For s = 13, m = 4, fp64 (no extras) the blocks are built inside the sweep
+    and never written to HBM; otherwise they go through a workspace.
+    """
+    torch = _torch()
+    args, (Bn, N, n, m, dt, dev, has_extra), keep = _traj_args(
+        A, Bm, a_res, X, U, xg, u_ref, Q, P, w, wrap_idx, q_reg, rho_reg, qxx_extra, qx_extra,
+        c_extra)
+    R_inv = _dev(R_inv, "R_inv", dt, dev)
+    if tuple(R_inv.shape[-2:]) != (m, m):
+        raise ValueError(f"R_inv blocks must be {m}x{m}")
+    r_bs = _bstride(R_inv, 2, "R_inv", Bn)
+    n_use = N if n_use is None else int(n_use)
+    if n_use > N:
+        raise IndexError(f"T_use={n_use} exceeds the {N} stages supplied")
+    n_eff = max(n_use, 0)
+    J = torch.empty((Bn, n_eff), dtype=dt, device=dev)
+    status = torch.zeros((Bn,), dtype=torch.int32, device=dev)
+    fuse = t_max is not None
+    ts = torch.empty((Bn,), dtype=torch.int32, device=dev) if fuse else None
+    js = torch.empty((Bn,), dtype=dt, device=dev) if fuse else None
+    lib = _lib.load()
+    ws_bytes = int(lib.hop_lft_sweep_traj_workspace_bytes(Bn, n_eff, n, m, A.element_size(),
+                                                          1 if has_extra else 0))
+    ws = torch.empty((ws_bytes + 256,), dtype=torch.uint8, device=dev) if ws_bytes else None
+    ws_ptr = None
+    if ws is not None:  # 256-B aligned view
+        off = (-ws.data_ptr()) % 256
+        ws_ptr = _lib.C.c_void_p(ws.data_ptr() + off)
+    rc = _fn("hop_lft_sweep_traj", dt)(
+        *args, _lib.ptr(R_inv), r_bs, Bn, N, n_use, n, m, int(max_tries),
+        int(t_min) if fuse else 0, int(t_max) if fuse else 0, _lib.ptr(J), _lib.ptr(status),
+        _lib.ptr(ts), _lib.ptr(js), ws_ptr, ws_bytes, _lib.stream_handle(dev))
+    _lib.check(rc)
+    if ws is not None:  # keep the workspace alive until the sweep has consumed it
+        ws.record_stream(torch.cuda.current_stream(dev))
+    del keep
+    return SweepResult(J, status, ts, js)
