@@ -263,3 +263,30 @@ def test_small_kernel_math_vs_golden(small_host, golden_dir, tag, dt):
 def _rel_err(got, ref):
     got, ref = np.asarray(got, float), np.asarray(ref, float)
     return float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-300))
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_wrap_angle_matches_python_remainder(small_host, dt):
+    """csrc/wrap.hpp (used by every kernel) == angle_normalize (utils.py:127-128):
+    (a + pi) % (2 pi) - pi with Python's float remainder, bit for bit in fp64."""
+    import math
+    rng = np.random.default_rng(3)
+    two_pi = 2.0 * math.pi
+    k = np.arange(-40, 41, dtype=np.float64)
+    vals = np.concatenate([
+        rng.uniform(-50, 50, 20000), rng.uniform(-1e6, 1e6, 2000), rng.standard_normal(2000),
+        k * two_pi - math.pi, k * two_pi + math.pi, k * two_pi,
+        np.nextafter(k * two_pi - math.pi, np.inf), np.nextafter(k * two_pi - math.pi, -np.inf),
+        np.array([0.0, -0.0, math.pi, -math.pi, 1e-300, -1e-300, 3 * math.pi, -3 * math.pi])])
+    vals = np.ascontiguousarray(vals.astype(dt))
+    out = np.zeros_like(vals)
+    fn = small_host.small_host_wrap_f64 if dt == np.float64 else small_host.small_host_wrap_f32
+    p = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    fn(p(vals), p(out), C.c_int64(len(vals)))
+    if dt == np.float64:
+        ref = np.array([(float(a) + math.pi) % (2.0 * math.pi) - math.pi for a in vals])
+        assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+    else:  # same formula in fp32 (np.float32 remainder has the same semantics)
+        pi32, tp32 = np.float32(math.pi), np.float32(2.0 * math.pi)
+        ref = np.remainder(vals + pi32, tp32) - pi32
+        assert np.array_equal(out, ref.astype(np.float32))

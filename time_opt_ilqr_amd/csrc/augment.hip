@@ -30,6 +30,7 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
   const int NA = a.nalloc;
   __shared__ T e0[KS][16], e1[KS][16], du[KS][16], qe[KS][16], pe[KS][16], at[KS][16];
   __shared__ T eqe[KS], epe[KS];
+  __shared__ T sQ[16 * 16], sQs[16 * 16], sP[16 * 16];
 
   const T* xg = t.xg + b * t.xg_bs;
   const T* ur = t.u_ref + b * t.ur_bs;
@@ -40,6 +41,14 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
   const int tid = threadIdx.x, kk = tid >> 4, i = tid & 15, k = k0 + kk;
   const bool row_ok = kk < ks;
 
+  // phase 0: Q, _sym(Q) + q_reg I and P into LDS (one coalesced pass)
+  for (int idx = tid; idx < n * n; idx += TPB) {
+    const int r = idx / n, c = idx - r * n;
+    const T q = Q[idx];
+    sQ[idx] = q;
+    sQs[idx] = T(0.5) * (q + Q[c * n + r]) + (r == c ? t.q_reg : T(0));
+    sP[idx] = P[idx];
+  }
   // phase 1a: errors (wrap_error, utils.py:131-137) and control deviations
   if (row_ok) {
     if (i < n) {
@@ -59,8 +68,8 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
   if (row_ok && i < n) {
     T v = T(0), p = T(0), bd = T(0);
     for (int j = 0; j < n; ++j) {
-      v += Q[i * n + j] * e0[kk][j];
-      p += P[i * n + j] * e1[kk][j];
+      v += sQ[i * n + j] * e0[kk][j];
+      p += sP[i * n + j] * e1[kk][j];
     }
     const T* Bk = t.Bm + ((b * NA + k) * n + i) * m;
     for (int q = 0; q < m; ++q) bd += Bk[q] * du[kk][q];
@@ -83,48 +92,69 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
   }
   __syncthreads();
 
-  // phase 2: contiguous runs of the blocks of steps k0 .. k0+ks-1
+  // phase 2: contiguous runs of the blocks of steps k0 .. k0+ks-1.  UNR
+  // elements per thread per pass, loads at clamped indices first (independent,
+  // in flight together), then the stores.
+  constexpr int UNR = 4;
   const long long ss = (long long)s * s, base = (b * a.nbuild + k0);
   T* Qo = a.Q_aug + base * ss;
   T* To = a.QT_aug + base * ss;
   T* Ao = a.A_aug + base * ss;
   T* Bo = a.B_aug + base * s * m;
   const T* cx = t.qx_extra ? t.qx_extra + (b * NA + k0) * n : nullptr;
+  const T* Ab = t.A + (b * NA + k0) * (long long)n * n;
   const int tot = ks * s * s;
-  for (int idx = tid; idx < tot; idx += TPB) {
-    const int q = idx / (s * s), r = idx - q * s * s, ii = r / s, jj = r - ii * s;
-    const int kq = k0 + q;
-    T vq, vt, va;
-    if (ii < n && jj < n) {
-      // _sym(Q) + q_reg I (+ _sym(cxx)); the final _sym of the block is exact
-      vq = T(0.5) * (Q[ii * n + jj] + Q[jj * n + ii]) + (ii == jj ? t.q_reg : T(0));
-      if (t.qxx_extra) {
-        const T* X = t.qxx_extra + (b * NA + kq) * n * n;
-        vq += T(0.5) * (X[ii * n + jj] + X[jj * n + ii]);
-      }
-      vt = P[ii * n + jj];
-      va = t.A[((b * NA + kq) * n + ii) * n + jj];
-    } else if (ii < n) {  // last column: Q e (+ cx)
-      vq = cx ? qe[q][ii] + cx[q * n + ii] : qe[q][ii];
-      vt = pe[q][ii];
-      va = at[q][ii];
-    } else if (jj < n) {  // last row
-      vq = cx ? qe[q][jj] + cx[q * n + jj] : qe[q][jj];
-      vt = pe[q][jj];
-      va = T(0);
-    } else {
-      vq = eqe[q];
-      vt = epe[q];
-      va = T(1);
+  for (int p0 = tid; p0 < tot; p0 += UNR * TPB) {
+    T ra[UNR];
+    int q[UNR], ii[UNR], jj[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int idx = min(p0 + u * TPB, tot - 1);
+      q[u] = idx / (s * s);
+      const int r = idx - q[u] * s * s;
+      ii[u] = r / s;
+      jj[u] = r - ii[u] * s;
+      const int ia = min(ii[u], n - 1), ja = min(jj[u], n - 1);
+      ra[u] = Ab[(q[u] * n + ia) * n + ja];
     }
-    Qo[idx] = vq;
-    To[idx] = vt;
-    Ao[idx] = va;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int idx = p0 + u * TPB;
+      if (idx >= tot) break;
+      const int qq = q[u], i2 = ii[u], j2 = jj[u];
+      T vq, vt, va;
+      if (i2 < n && j2 < n) {
+        // _sym(Q) + q_reg I (+ _sym(cxx)); the final _sym of the block is exact
+        vq = sQs[i2 * n + j2];
+        if (t.qxx_extra) {
+          const T* X = t.qxx_extra + (b * NA + k0 + qq) * n * n;
+          vq += T(0.5) * (X[i2 * n + j2] + X[j2 * n + i2]);
+        }
+        vt = sP[i2 * n + j2];
+        va = ra[u];
+      } else if (i2 < n) {  // last column: Q e (+ cx)
+        vq = cx ? qe[qq][i2] + cx[qq * n + i2] : qe[qq][i2];
+        vt = pe[qq][i2];
+        va = at[qq][i2];
+      } else if (j2 < n) {  // last row
+        vq = cx ? qe[qq][j2] + cx[qq * n + j2] : qe[qq][j2];
+        vt = pe[qq][j2];
+        va = T(0);
+      } else {
+        vq = eqe[qq];
+        vt = epe[qq];
+        va = T(1);
+      }
+      Qo[idx] = vq;
+      To[idx] = vt;
+      Ao[idx] = va;
+    }
   }
+  const T* Bb = t.Bm + (b * NA + k0) * (long long)n * m;
   const int totb = ks * s * m;
   for (int idx = tid; idx < totb; idx += TPB) {
-    const int q = idx / (s * m), r = idx - q * s * m, ii = r / m, jj = r - ii * m;
-    Bo[idx] = ii < n ? t.Bm[((b * NA + k0 + q) * n + ii) * m + jj] : T(0);
+    const int qq = idx / (s * m), r = idx - qq * s * m, i2 = r / m, j2 = r - i2 * m;
+    Bo[idx] = i2 < n ? Bb[(qq * n + i2) * m + j2] : T(0);
   }
 }
 

@@ -14,6 +14,7 @@
 #include <utility>
 
 #include "dpp_blocks.inc"
+#include "wrap.hpp"
 
 namespace hop {
 
@@ -38,21 +39,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// wrap_error (utils.py:131-137) on one component
-template <class T>
-__device__ __forceinline__ T wrap_angle(T a) {
-  // NumPy: (a + pi) % (2 pi) - pi  (np.remainder: fmod, then shift into [0, 2pi))
-  const T two_pi = T(2.0 * 3.141592653589793);
-  const T pi = T(3.141592653589793);
-  T r = fmod(a + pi, two_pi);
-  if (r != T(0)) {
-    if (r < T(0)) r += two_pi;
-  } else {
-    r = T(0);
-  }
-  return r - pi;
 }
 
 template <class T, int S>
@@ -114,6 +100,25 @@ __device__ __forceinline__ void transpose(T (&dst)[S], const T (&src)[S], T* til
   wave_sync();
   lds_get_t(tile, c, dst);
   wave_sync();
+}
+
+// Sum over the 16 lanes of a row by a row_ror butterfly of 32-bit DPP moves
+// (fp64 DPP allows only row_newbcast): no LDS round trips, 4 dependent adds.
+// Lanes may differ in the last bit (each sums in its own order): use the value
+// of one lane only.
+template <int ROR>
+__device__ __forceinline__ double ror_row(double v) {
+  const int2 w = __builtin_bit_cast(int2, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, w.x, 0x120 + ROR, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x120 + ROR, 0xf, 0xf, false);
+  return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+__device__ __forceinline__ double row_sum_dpp(double v) {
+  v += ror_row<8>(v);
+  v += ror_row<4>(v);
+  v += ror_row<2>(v);
+  v += ror_row<1>(v);
+  return v;
 }
 
 // Sum over the 16 lanes of a row (every lane of the row gets the total).

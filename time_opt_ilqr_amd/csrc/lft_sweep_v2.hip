@@ -103,6 +103,9 @@ struct SchedStamped : SchedLdl {
 struct SchedLdlTraj : SchedLdl {
   static constexpr int TRAJ = 1;
 };
+struct SchedLdlTrajStamped : SchedLdlTraj {
+  static constexpr int STAMP = 1;
+};
 template <class C>
 constexpr bool has_traj() {
   if constexpr (requires { C::TRAJ; }) return C::TRAJ != 0;
@@ -577,12 +580,12 @@ struct Geo {
   static constexpr int OFF_X = OFF_T + TILE_W;
   static constexpr int WAVE_BYTES_X = OFF_X + TILE_W;
   // trajectory form (n = S-1): raw A_k staged in the A image area, raw B_k in
-  // the B area, then x_k|x_{k+1}, a_k and u_k after the tiles.  Per problem the
+  // the B area, then x_{k+1}, a_k and u_k after the tiles.  Per problem the
   // staged block of a piece type is CH 16-B chunks at 16 CH g.
   static constexpr int NN = S - 1;
   static constexpr int CHA = (NN * NN * 8 + 15) / 16, NJA = (kProbPerWave * CHA + 63) / 64;
   static constexpr int CHR = (NN * MM * 8 + 15) / 16, NJR = (kProbPerWave * CHR + 63) / 64;
-  static constexpr int CHX = (2 * NN * 8 + 15) / 16, NJX = (kProbPerWave * CHX + 63) / 64;
+  static constexpr int CHX = (NN * 8 + 15) / 16, NJX = (kProbPerWave * CHX + 63) / 64;
   static constexpr int CHV = (NN * 8 + 15) / 16, NJV = (kProbPerWave * CHV + 63) / 64;
   static constexpr int CHU = (MM * 8 + 15) / 16, NJU = (kProbPerWave * CHU + 63) / 64;
   static_assert(NJA <= NJM && NJR <= NJB, "raw blocks must fit the augmented image areas");
@@ -690,15 +693,16 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       voTU[j] = chunk_voff<G::CHU>(j, lane, wave_prob0, pb0, a.batch, pstU);
   }
   auto dma_step = [&](int k) {  // Q, A, B, QT of step k
-    if constexpr (TRAJ) {  // A_k, B_k, x_k|x_{k+1}, a_k, u_k
+    if constexpr (TRAJ) {  // A_k, B_k, x_{k+1}, a_k, u_k
       const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
                      soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
+      const unsigned soX = soV + NN * 8;
 #pragma unroll
       for (int j = 0; j < G::NJA; ++j) dma16(voTA[j], rQ, wlds + G::OFF_A + 1024 * j, soA);
 #pragma unroll
       for (int j = 0; j < G::NJR; ++j) dma16(voTR[j], rA, wlds + G::OFF_B + 1024 * j, soR);
 #pragma unroll
-      for (int j = 0; j < G::NJX; ++j) dma16(voTX[j], rT, wlds + G::OFF_VX + 1024 * j, soV);
+      for (int j = 0; j < G::NJX; ++j) dma16(voTX[j], rT, wlds + G::OFF_VX + 1024 * j, soX);
 #pragma unroll
       for (int j = 0; j < G::NJV; ++j) dma16(voTV[j], rB, wlds + G::OFF_VA + 1024 * j, soV);
 #pragma unroll
@@ -726,8 +730,20 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   }
   // trajectory form: per-lane constants and the constant parts of the Q / QT images
   double xg_c = 0.0, ur_c = 0.0, w2 = 0.0, qdiag = 0.0, pdiag = 0.0, pcc = 0.0;
+  double qe_k = 0.0, eqe_k = 0.0;  // Q e_k and e_k^T Q e_k (carried from step k-1)
   bool wrap_c = false;
   double* cq = reinterpret_cast<double*>(wbase + G::OFF_CQ) + g * NN * NN;
+  double qr_n[NN], pr_n[NN];       // rows c of Q and P for the next step's build
+  auto load_rows = [&]() {
+    if constexpr (TRAJ) {
+      const int cc = c < NN ? c : 0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        qr_n[j] = cq[j * NN + cc];
+        pr_n[j] = imT[j * S + cc];
+      }
+    }
+  };
   if constexpr (TRAJ) {
     const TrajArgs<double>& t = a.tr;
     const double* Qg = t.Q + pb * t.q_bs;
@@ -748,6 +764,22 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     pdiag = Pg[cc * NN + cc] + (1e-9 - 1.0);
     double* wq = const_cast<double*>(imQ);
     double* wt = const_cast<double*>(imT);
+    // step 0's Q e_0 and e_0^T Q e_0; later steps carry Q e_{k+1} from step k
+    {
+      const double* X0 = t.X + pb * (long long)(a.nalloc + 1) * NN;
+      double e0 = c < NN ? X0[cc] - xg_c : 0.0;
+      if (t.wrap_mask != 0u) {
+        const double w0 = wrap_angle(e0);
+        e0 = wrap_c ? w0 : e0;
+      }
+      double q4[4] = {0.0, 0.0, 0.0, 0.0};
+      double qr0[NN];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) qr0[j] = c < NN ? Qg[cc * NN + j] : 0.0;
+      LaneDot4<NN>::fma(q4, e0, qr0);
+      qe_k = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+      eqe_k = row_sum_dpp(c < NN ? e0 * qe_k : 0.0);
+    }
     if (c < NN) {  // column c: _sym(Q) + q_reg I, and P (augmented.py:33, 82)
 #pragma unroll
       for (int i = 0; i < NN; ++i) {
@@ -755,6 +787,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
         wt[i * S + c] = Pg[i * NN + c];
       }
     }
+    load_rows();
   }
   unsigned st = 0;
   // R^-1 (cached, shared or per problem) as columns on lanes 0..MM-1
@@ -772,7 +805,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   const bool fuse_argmin = a.t_max > 0;
 
   double jprev = 0.0;
-  unsigned long long sec[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long sec[15] = {};
   unsigned long long tprev = 0;
   auto stamp = [&](int j) {
     if constexpr (C::STAMP) {
@@ -799,49 +832,72 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       const double* sV = reinterpret_cast<const double*>(wbase + G::OFF_VA) + g * 2 * G::CHV;
       const double* sU = reinterpret_cast<const double*>(wbase + G::OFF_VU) + g * 2 * G::CHU;
       const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
-      const int cc = c < NN ? c : 0;
-      double e = c < NN ? sX[cc] - xg_c : 0.0;
-      double e1 = c < NN ? sX[NN + cc] - xg_c : 0.0;
-      if (wrap_c) {
-        e = wrap_angle(e);
-        e1 = wrap_angle(e1);
-      }
-      const double du = c < MM ? sU[c < MM ? c : 0] - ur_c : 0.0;
-      double rb[MM];
+      const int cc = c < NN ? c : 0, cm = c < MM ? c : 0;
+      // Per step only e_{k+1} is new: Q e_k and e_k^T Q e_k were formed at step
+      // k-1 from the same e (carried), P e_{k+1} and Q e_{k+1} are formed now.
+      // Every LDS load first, unconditionally at clamped addresses (a load under
+      // a lane condition becomes an exec-masked branch with its own wait), then
+      // the lane selects.  Row c of Q comes from the constant area, row c of P
+      // is column c of the QT image (P symmetric; its diagonal kept in pcc).
+      stamp(9);
+      double x1 = sX[cc], av = sV[cc], uu = sU[cm];
+      double rb[MM], qr[NN], pr[NN];
 #pragma unroll
-      for (int q = 0; q < MM; ++q) rb[q] = c < NN ? sR[cc * MM + q] : 0.0;
-      const double av = c < NN ? sV[cc] : 0.0;
-      // row c of Q (constant area) and of P (= column c of the QT image: P is
-      // symmetric; its diagonal entry is kept in a register)
-      double qr[NN], pr[NN], ones[NN];
+      for (int q = 0; q < MM; ++q) rb[q] = sR[cc * MM + q];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {  // loaded at the end of the previous step
+        qr[j] = qr_n[j];
+        pr[j] = pr_n[j];
+      }
+      const bool in = c < NN;
 #pragma unroll
       for (int j = 0; j < NN; ++j) {
-        qr[j] = c < NN ? cq[j * NN + cc] : 0.0;
-        pr[j] = c < NN ? (j == c ? pcc : imT[j * S + cc]) : 0.0;
-        ones[j] = 1.0;
+        qr[j] = in ? qr[j] : 0.0;
+        pr[j] = in ? (j == c ? pcc : pr[j]) : 0.0;
       }
-      double qe = 0.0, pe = 0.0, bd = 0.0;
-      LaneDot<NN>::fma(qe, e, qr);   // (Q e)[c]
-      LaneDot<NN>::fma(pe, e1, pr);  // (P e_{k+1})[c]
+#pragma unroll
+      for (int q = 0; q < MM; ++q) rb[q] = in ? rb[q] : 0.0;
+      double e1 = in ? x1 - xg_c : 0.0;
+      stamp(10);
+      if (a.tr.wrap_mask != 0u) {  // wave-uniform: no wrap work without wrapped states
+        const double we1 = wrap_angle(e1);  // branch-free
+        e1 = wrap_c ? we1 : e1;
+      }
+      const double du = c < MM ? uu - ur_c : 0.0;
+      av = in ? av : 0.0;
+      stamp(11);
+      // Q e_{k+1}, P e_{k+1} as 4 interleaved partial sums each (a single
+      // 12-deep dependent DPP chain exposes the fp64 latency at 1 wave/SIMD)
+      double q4[4] = {0.0, 0.0, 0.0, 0.0}, p4[4] = {0.0, 0.0, 0.0, 0.0}, bd = 0.0;
+      LaneDot4<NN>::fma(q4, e1, qr);
+      LaneDot4<NN>::fma(p4, e1, pr);
       LaneDot<MM>::fma(bd, du, rb);  // (B du)[c]
+      const double qe1 = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+      const double pe = (p4[0] + p4[1]) + (p4[2] + p4[3]);
       atil = av - bd;
-      double eqe = 0.0, epe = 0.0;   // row sums by broadcast (every lane gets them)
-      LaneDot<NN>::fma(eqe, c < NN ? e * qe : 0.0, ones);
-      LaneDot<NN>::fma(epe, c < NN ? e1 * pe : 0.0, ones);
+      stamp(12);
+      // e^T Q e and e^T P e: row sums (lane NN's value is the one stored)
+      const double eqe1 = row_sum_dpp(in ? e1 * qe1 : 0.0);
+      const double epe = row_sum_dpp(in ? e1 * pe : 0.0);
+      stamp(13);
       double* wq = const_cast<double*>(imQ);
       double* wt = const_cast<double*>(imT);
       if (c < NN) {
-        wq[c * S + NN] = qe;
-        wq[NN * S + c] = qe;
+        wq[c * S + NN] = qe_k;
+        wq[NN * S + c] = qe_k;
         wq[c * S + c] = qdiag;
         wt[c * S + NN] = pe;
         wt[NN * S + c] = pe;
         wt[c * S + c] = pdiag;
       } else if (c == NN) {
-        wq[NN * S + NN] = ((eqe + w2) + a.tr.rho_reg) + (1e-9 - 1.0);
+        wq[NN * S + NN] = ((eqe_k + w2) + a.tr.rho_reg) + (1e-9 - 1.0);
         wt[NN * S + NN] = (epe + a.tr.rho_reg) + (1e-9 - 1.0);
       }
-      wave_sync();
+      qe_k = qe1;
+      eqe_k = eqe1;
+      // no wave_sync: the image reads (LdsSym) are asm with a memory clobber and
+      // one wave's LDS operations execute in order
+      stamp(14);
     } else if constexpr (OFF) {
       diag_add<S, S>(imQ, c, 1e-9 - 1.0);
       diag_add<S, S>(imT, c, 1e-9 - 1.0);
@@ -997,6 +1053,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       jk = 0.5 * row_sum((c < S) ? u * zc : 0.0);
     }
     stamp(8);
+    load_rows();  // trajectory form: next step's Q / P rows (constant LDS data)
     if (!finite_val(jk)) st |= ST_NONFINITE;
     jprev = jk;
     if (fuse_argmin) {
@@ -1016,7 +1073,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   dma_wait();
   if constexpr (C::STAMP) {
     if (lane == 0) {
-      for (int j = 0; j < 10; ++j) atomicAdd(&g_hop_stamp[j], sec[j]);
+      for (int j = 0; j < 15; ++j) atomicAdd(&g_hop_stamp[j], sec[j]);
       atomicAdd(&g_hop_stamp[15], 1ull);
     }
   }
@@ -1038,9 +1095,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (a.traj) {  // in-kernel augmentation (capi routes only s = 13, m = 4 here)
     if (a.s != 13 || a.m != 4 || a.tr.n != 12 || a.tr.m != 4) return hipErrorNotSupported;
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
-    hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>), dim3((unsigned)blocks),
-                       dim3(256), (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock), stream,
-                       a);
+    const size_t bytes = (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock);
+    const char* ev = getenv("HOP_LFT_VARIANT");
+    if (ev && atoi(ev) == 24)  // section stamps (tools/stamps.py --traj)
+      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTrajStamped, 13, 4>),
+                         dim3((unsigned)blocks), dim3(256), bytes, stream, a);
+    else
+      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>),
+                         dim3((unsigned)blocks), dim3(256), bytes, stream, a);
     return hipGetLastError();
   }
   auto go = [&](auto kern, int bytes) {

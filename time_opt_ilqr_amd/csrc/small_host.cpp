@@ -11,6 +11,7 @@ inline T small_recip(T d) { return T(1) / d; }
 }  // namespace hop
 
 #include "small_math.hpp"
+#include "wrap.hpp"
 
 using namespace hop::small;
 
@@ -66,4 +67,12 @@ extern "C" int small_host_sweep_f32(const float* A, const float* B, const float*
   if (s == 5 && m == 1) run<float, 5, 1>(A, B, Q, Rinv, QT, z0, batch, n, mt, t_min, t_max, J, status, t_star);
   else return -1;
   return 0;
+}
+
+// wrap.hpp on the host (tests/test_host_cpu.py checks it against Python's float %)
+extern "C" void small_host_wrap_f64(const double* in, double* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = hop::wrap_angle(in[i]);
+}
+extern "C" void small_host_wrap_f32(const float* in, float* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) out[i] = hop::wrap_angle(in[i]);
 }

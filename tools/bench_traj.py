@@ -65,6 +65,8 @@ def main():
 
     paths = {
         "traj_fused": lambda: engine.propagate_traj(*targs, t_min=1, t_max=N),
+        "traj_fused_wrap3": lambda: engine.propagate_traj(*targs, wrap_idx=[3, 4, 5], t_min=1,
+                                                          t_max=N),
         "sweep_prebuilt": lambda: engine.propagate(blk.A, blk.B, blk.Q, Rinv, blk.z0, blk.QT,
                                                    t_min=1, t_max=N),
         "augment_only": lambda: engine.augment(A, Bm, a_res, X, U, xg, ur, Q, P, w),
