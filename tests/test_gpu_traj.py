@@ -193,3 +193,18 @@ def test_traj_real_first_select(dev, golden_dir, tag, jtol):
     assert np.max(np.abs(J - d["J"]) / np.abs(d["J"])) <= jtol
     T_ref = int(np.argmin(d["J"][T_min - 1:T_max]) + T_min)
     assert int(res.t_star[0]) == T_ref
+
+
+def test_select_from_trajectory_dropin_DI(dev, golden_dir):
+    """The drop-in for solver.py:514-522 on the DoubleIntegrator's first select
+    (F reproduces the captured residuals on the trajectory)."""
+    from time_opt_ilqr_amd import horizon_selection as hs
+    d = _load(golden_dir, "traj_real_DI_N50.npz")
+    X, U, a_res = d["X"], d["U"], d["a_res"]
+    table = {X[k].tobytes() + U[k].tobytes(): X[k + 1] + a_res[k] for k in range(len(U))}
+    F = lambda x, u: table[np.asarray(x).tobytes() + np.asarray(u).tobytes()]  # noqa: E731
+    J, T = hs.select_from_trajectory(F, list(d["A"]), list(d["B"]), X, U, d["xg"], d["u_ref"],
+                                     d["Q"], d["R"], float(d["w"]), float(d["alpha"]),
+                                     int(d["T_min"]), int(d["T_max"]))
+    assert np.max(np.abs(J - d["J"]) / np.abs(d["J"])) <= 1e-3
+    assert T == int(np.argmin(d["J"][int(d["T_min"]) - 1:int(d["T_max"])]) + int(d["T_min"]))

@@ -9,6 +9,9 @@ that hold one problem as lists of NumPy blocks:
   backward_pass_truncated             solver.py:156-230
   bruteforce_all_Jt_backward_expansion solver.py:293-358
   select_horizon                      the argmin at solver.py:522
+  select_from_trajectory              the select block of ilqr_timeopt,
+                                      solver.py:514-522 (builders + propagator +
+                                      argmin, the builders run on the device)
 
 Each call stages the blocks into HBM and runs the batch-of-one kernels of
 libhop_amd.so; batched callers should use ``engine.propagate`` directly.
@@ -20,7 +23,8 @@ from typing import List, Optional, Tuple
 import numpy as np
 
 from . import _lib, engine
-from .utils import as_terminal_weight
+from .augmented import compute_affine_residuals
+from .utils import _sym, as_terminal_weight, chol_inv
 
 _DEVICE = None
 
@@ -94,6 +98,44 @@ def select_horizon(J, T_min: int, T_max: int) -> int:
         raise ValueError("attempt to get argmin of an empty sequence")
     ts, _ = engine.select_horizon(Jt, int(T_min), int(T_max))
     return int(ts.item()) if ts.dim() == 0 else ts
+
+
+def select_from_trajectory(F, A_list, B_list, X, U, xg, u_ref, Q, R, w, alpha,
+                           T_min: int, T_max: int, wrap_idx: Optional[List[int]] = None,
+                           extra_stage_cost=None) -> Tuple[np.ndarray, int]:
+    """The propagator branch of ilqr_timeopt's horizon selection (solver.py:514-522):
+
+        A_aug, B_aug, Q_aug, R_list, z0, R_inv = build_augmented_sequence_QR(...)
+        QT_list = build_terminal_aug_list(X, xg, alpha, wrap_idx=wrap_idx)
+        J_curve = propagator_all_Jt_aug(..., T_use=T_max, R_inv_cached=R_inv)
+        T_bar = int(np.argmin(J_curve[T_min - 1 : T_max]) + T_min)
+
+    Returns (J_curve, T_bar).  The dynamics F (affine residuals), chol_inv(R) and
+    the extra stage cost stay on the host as in the reference; the augmented
+    blocks are built on the device (inside the sweep for s = 13, m = 4)."""
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float).reshape(len(U), -1)
+    n, m = X.shape[1], U.shape[1]
+    N = len(A_list)
+    if int(T_max) > N:
+        raise IndexError("list index out of range")
+    a_res = np.stack([r.reshape(-1) for r in compute_affine_residuals(F, X, U)])
+    R_inv = chol_inv(_sym(np.asarray(R, dtype=float)))
+    P = _sym(as_terminal_weight(alpha, n))
+    A = np.stack([np.asarray(a, dtype=float) for a in A_list])[None]
+    Bm = np.stack([np.asarray(b, dtype=float).reshape(n, m) for b in B_list])[None]
+    qxx, qx, c0 = _extra_arrays(extra_stage_cost, X, U, N)
+    dv = lambda a: None if a is None else _to_dev(a)  # noqa: E731
+    res = engine.propagate_traj(
+        dv(A), dv(Bm), dv(a_res[None]), dv(X[None, :N + 1]), dv(U[None, :N]),
+        dv(np.asarray(xg, dtype=float).reshape(-1)),
+        dv(np.atleast_1d(np.asarray(u_ref, dtype=float)).reshape(-1)),
+        dv(np.asarray(Q, dtype=float)), dv(R_inv), dv(P), float(w), wrap_idx=wrap_idx,
+        n_use=int(T_max), t_min=int(T_min), t_max=int(T_max), qxx_extra=dv(qxx),
+        qx_extra=dv(qx), c_extra=dv(c0))
+    J = res.J[0].cpu().numpy()
+    _raise_for(int(res.status[0].item()), "chol_inv(A)")
+    return J, int(res.t_star[0].item())
 
 
 def _extra_arrays(extra_stage_cost, X, U, L):
