@@ -113,6 +113,18 @@ __device__ __forceinline__ double ror_row(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x120 + ROR, 0xf, 0xf, false);
   return __builtin_bit_cast(double, make_int2(lo, hi));
 }
+template <int ROR>
+__device__ __forceinline__ float ror_row(float v) {
+  const int w = __builtin_bit_cast(int, v);
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, w, 0x120 + ROR, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row_sum_dpp(float v) {
+  v += ror_row<8>(v);
+  v += ror_row<4>(v);
+  v += ror_row<2>(v);
+  v += ror_row<1>(v);
+  return v;
+}
 __device__ __forceinline__ double row_sum_dpp(double v) {
   v += ror_row<8>(v);
   v += ror_row<4>(v);
@@ -141,13 +153,24 @@ __device__ __forceinline__ T row_sum(T v) {
 // pivots are the same Schur complements).  The caller passes a symmetric
 // matrix (symmetrize() first).
 // ---------------------------------------------------------------------------
+// 1/d as v_rcp + one Newton step (the IEEE division sequence is ~10 dependent
+// instructions); d <= 0 / NaN pivots are rejected by the caller's test anyway
+__device__ __forceinline__ double recip_nr(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return __builtin_fma(r, __builtin_fma(-d, r, 1.0), r);
+}
+__device__ __forceinline__ float recip_nr(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  return __builtin_fmaf(r, __builtin_fmaf(-d, r, 1.0f), r);
+}
+
 template <class T, int S>
 __device__ __forceinline__ void sweep_neg_inverse(T (&r)[S], T eps, int c, bool& ok) {
   static_for<S>([&](auto P) {
     constexpr int p = P;
     const T d = bcast<p>(r[p]) + eps;
     ok = ok && (d > T(0));
-    const T rd = T(1) / d;
+    const T rd = recip_nr(d);
     const T t = r[p] + ((c == p) ? (eps - T(1)) : T(0));  // column p minus e_p
     const T sc = -t * rd;
     r[p] = t;
@@ -222,6 +245,72 @@ __device__ __forceinline__ bool spd_inverse_nofallback(T (&r)[S], T* tile, int c
     }
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = tile[i * kLdsRow + c];
+  }
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < S; ++i) r[i] = -r[i];
+  return good;
+}
+
+// Two independent sweeps interleaved pivot by pivot (their dependent chains
+// hide each other's latency): r1 with eps1, r2 with eps2.
+template <class T, int S>
+__device__ __forceinline__ void sweep_neg_inverse2(T (&r1)[S], T eps1, bool& ok1, T (&r2)[S],
+                                                   T eps2, bool& ok2, int c) {
+  static_for<S>([&](auto P) {
+    constexpr int p = P;
+    const T d1 = bcast<p>(r1[p]) + eps1;
+    const T d2 = bcast<p>(r2[p]) + eps2;
+    ok1 = ok1 && (d1 > T(0));
+    ok2 = ok2 && (d2 > T(0));
+    const T rd1 = recip_nr(d1), rd2 = recip_nr(d2);
+    const T t1 = r1[p] + ((c == p) ? (eps1 - T(1)) : T(0));
+    const T t2 = r2[p] + ((c == p) ? (eps2 - T(1)) : T(0));
+    const T sc1 = -t1 * rd1, sc2 = -t2 * rd2;
+    r1[p] = t1;
+    r2[p] = t2;
+    RowB<S>::template sweep<p>(r1, sc1);
+    RowB<S>::template sweep<p>(r2, sc2);
+    r1[p] = r1[p] - ((c == p) ? T(1) : T(0));
+    r2[p] = r2[p] - ((c == p) ? T(1) : T(0));
+  });
+}
+
+// backward_pass_truncated's solve (solver.py:211-219): is sym(Quu)+lam I PD
+// without jitter (np.linalg.cholesky, ok0), and its chol_solve inverse with the
+// jitter ladder (spd_inverse_nofallback semantics).  The two first attempts run
+// interleaved; retries (rare) as spd_inverse_nofallback.
+template <class T, int S>
+__device__ __forceinline__ bool spd_inverse_nofallback_chk(T (&r)[S], T* tile, int c,
+                                                           int max_tries, unsigned& st,
+                                                           bool& ok0) {
+  lds_put(tile, c, r);
+  T chk[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) chk[i] = r[i];
+  bool ok = true;
+  ok0 = true;
+  T eps = T(1e-9);
+  sweep_neg_inverse2(chk, T(0), ok0, r, eps, ok, c);
+  int tries = 1;
+  bool good = ok, done = ok || (tries >= max_tries);
+  if (__any(!done)) {
+    wave_sync();
+#pragma unroll 1
+    while (true) {
+      if (!done) {
+        eps *= T(10);
+        st |= ST_JITTER;
+      }
+#pragma unroll
+      for (int i = 0; i < S; ++i) r[i] = tile[i * kLdsRow + c];
+      ok = true;
+      sweep_neg_inverse(r, eps, c, ok);
+      ++tries;
+      good = ok;
+      done = ok || (tries >= max_tries);
+      if (!__any(!done)) break;
+    }
   }
   wave_sync();
 #pragma unroll

@@ -14,24 +14,30 @@
 
 namespace hop {
 
+// Loads at clamped (always valid) addresses first, then the padding selects: a
+// load under a lane condition becomes an exec-masked branch with its own wait.
 template <class T, int S>
 __device__ __forceinline__ void rload_col(const T* M, int rows, int cols, int c, T pad, T (&x)[S]) {
   // column c of a rows x cols row-major matrix, identity(pad)/zero padded
+  const int cc = c < cols ? c : cols - 1;
+#pragma unroll
+  for (int i = 0; i < S; ++i) x[i] = M[(i < rows ? i : rows - 1) * cols + cc];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const bool in = (i < rows) && (c < cols);
-    const T v = M[in ? i * cols + c : 0];
-    x[i] = in ? v : ((i == c) ? pad : T(0));
+    x[i] = in ? x[i] : ((i == c) ? pad : T(0));
   }
 }
 template <class T, int S>
 __device__ __forceinline__ void rload_row(const T* M, int rows, int cols, int c, T pad, T (&x)[S]) {
   // row c of a rows x cols row-major matrix
+  const int cr = c < rows ? c : rows - 1;
+#pragma unroll
+  for (int j = 0; j < S; ++j) x[j] = M[cr * cols + (j < cols ? j : cols - 1)];
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     const bool in = (c < rows) && (j < cols);
-    const T v = M[in ? c * cols + j : 0];
-    x[j] = in ? v : ((j == c) ? pad : T(0));
+    x[j] = in ? x[j] : ((j == c) ? pad : T(0));
   }
 }
 
@@ -45,8 +51,14 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   const bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
   T* tile = smem + (w * kProbPerWave + g) * kLdsTile;
+  // the problem's stage weight Q, loop-invariant, lives in a second LDS tile:
+  // held in registers it was re-loaded from HBM every step under register pressure
+  T* qt = smem + (kProbPerBlock + w * kProbPerWave + g) * kLdsTile;
 #pragma unroll 1
-  for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = T(0);
+  for (int i = c; i < kLdsTile; i += kRowLanes) {
+    tile[i] = T(0);
+    qt[i] = T(0);
+  }
   wave_sync();
 
   const int n = a.n, m = a.m, NA = a.nalloc, mode = a.mode;
@@ -68,9 +80,11 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   const T lam0 = a.lm[pb];
 
   // loop-invariant cost blocks
-  T qcol[S], qrow[S];
-  rload_col(Qp, n, n, c, T(0), qcol);
-  rload_row(Qp, n, n, c, T(0), qrow);
+  {
+    T qcol[S];
+    rload_col(Qp, n, n, c, T(0), qcol);
+    lds_put(qt, c, qcol);  // qt[i][c] = Q[i][c]
+  }
   T rcol[MM], rrow[MM];
   rload_col(Rp, m, m, c, T(1), rcol);
   rload_row(Rp, m, m, c, T(1), rrow);
@@ -99,7 +113,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
     }
     vx = T(0);
     LaneDot<S>::fma(vx, eT, qfrow);  // (Qf eT)[c]
-    v0 = T(0.5) * row_sum((c < n) ? eT * vx : T(0));
+    v0 = T(0.5) * row_sum_dpp((c < n) ? eT * vx : T(0));
     symmetrize(Vxx, tile, c);
     if (alive) {
       if (a.Vxx) {
@@ -139,15 +153,25 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
 
     // lx = Q e (+ cx), lu = R du, l0
     T lx = T(0), lu = T(0);
-    LaneDot<S>::fma(lx, e, qrow);
+    {
+      T qrow[S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) qrow[j] = qt[c * kLdsRow + j];  // row c of Q
+      LaneDot<S>::fma(lx, e, qrow);
+    }
     LaneDot<MM>::fma(lu, du, rrow);
-    T l0 = T(0.5) * row_sum((c < n) ? e * lx : T(0)) + T(0.5) * row_sum((c < m) ? du * lu : T(0)) +
-           a.w_stage;
+    T l0 = T(0.5) * row_sum_dpp((c < n) ? e * lx : T(0)) +
+           T(0.5) * row_sum_dpp((c < m) ? du * lu : T(0)) + a.w_stage;
     T qst[S];
-    copy(qst, qcol);
-    if (a.qx_extra) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) qst[i] = qt[i * kLdsRow + c];  // column c of Q
+    if (a.qx_extra) {  // wave-uniform branch; the load itself must not become a
+                       // lane-divergent one (its join would wait on every
+                       // outstanding load, the prefetch included)
       const T* xp = a.qx_extra + (pb * NA + i) * n;
-      lx += (c < n) ? xp[c < n ? c : 0] : T(0);
+      T v = xp[c < n ? c : 0];
+      asm volatile("" : "+v"(v));
+      lx += (c < n) ? v : T(0);
     }
     if (a.c_extra) l0 += a.c_extra[pb * NA + i];
     if (a.qxx_extra) {
@@ -188,12 +212,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       for (int r = 0; r < MM; ++r) Qi[r] = T(0.5) * (Quu[r] + QuuT[r]) + ((c == r) ? lam0 : T(0));
       // the reference first checks cholesky(Quu_reg) (no jitter), then solves with jitter
       bool ok = true;
-      {
-        T tmp[MM];
-        copy(tmp, Qi);
-        sweep_neg_inverse(tmp, T(0), c, ok);
-      }
-      solved = spd_inverse_nofallback(Qi, tile, c, 8, st) && ok;
+      solved = spd_inverse_nofallback_chk(Qi, tile, c, 8, st, ok) && ok;
     } else {
       T lam = lam0 > T(1e-12) ? lam0 : T(1e-12);
       int tries = 0;
@@ -239,7 +258,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
     } else {
       acc_xty<false, T, S, MM>(Vn, Qux, K);  // Qxx - Qux^T Quu^-1 Qux
       LaneDot<MM>::fma(vxn, kv, Qux);        // Qx - Qux^T Quu^-1 Qu
-      v0n = l0 + v0 + T(0.5) * row_sum((c < m) ? qu * kv : T(0));
+      v0n = l0 + v0 + T(0.5) * row_sum_dpp((c < m) ? qu * kv : T(0));
     }
     symmetrize(Vn, tile, c);
     bool vbad = !finite_val(vxn) || !finite_val(v0n);
@@ -280,7 +299,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
 template <class T, int S, int MM>
 hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
-  const size_t lds = (size_t)kProbPerBlock * kLdsTile * sizeof(T);
+  const size_t lds = (size_t)2 * kProbPerBlock * kLdsTile * sizeof(T);
   hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream, a);
   return hipGetLastError();
 }
