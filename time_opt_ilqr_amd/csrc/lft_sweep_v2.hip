@@ -106,6 +106,20 @@ struct SchedLdlTraj : SchedLdl {
 struct SchedLdlTrajStamped : SchedLdlTraj {
   static constexpr int STAMP = 1;
 };
+// software pipeline across steps: the query of step k-1 runs at the top of step
+// k, and its bordered elimination is interleaved instruction by instruction
+// with the W_k sweep (SweepElimQ): two latency-bound chains hide each other
+struct SchedPipe : SchedLdl {
+  static constexpr int PIPE = 1;
+};
+struct SchedPipeStamped : SchedPipe {
+  static constexpr int STAMP = 1;
+};
+template <class C>
+constexpr bool has_pipe() {
+  if constexpr (requires { C::PIPE; }) return C::PIPE != 0;
+  return false;
+}
 template <class C>
 constexpr bool has_traj() {
   if constexpr (requires { C::TRAJ; }) return C::TRAJ != 0;
@@ -318,6 +332,9 @@ __device__ __forceinline__ double elim_quad(double (&r)[S], double eps, bool& ok
 // z0^T (sym(X0) + eps I)^-1 z0 with the chol_inv retry ladder; X0 parked in the
 // tile whose row S holds z0 (so that sym() keeps lane S = z0).
 template <class C, int S>
+__device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c, bool ok0,
+                                             double q, int mt, unsigned& st);
+template <class C, int S>
 __device__ __forceinline__ double quad_inverse(double (&r)[S], double* tile, int c, int mt,
                                                unsigned& st) {
   lds_put(tile, c, r);
@@ -325,8 +342,16 @@ __device__ __forceinline__ double quad_inverse(double (&r)[S], double* tile, int
   sym_from<C, S, kLdsRow>(tile, c, r);
   bool ok = true;
   double q = elim_quad<C, S>(r, 1e-9, ok);
-  if (__any(!ok)) {
-    const bool ok0 = ok;
+  if (__any(!ok)) q = quad_retry<C, S>(r, tile, c, ok, q, mt, st);
+  wave_sync();
+  return q;
+}
+
+// chol_inv ladder of quad_inverse (rare path): re-form sym(X0) from the tile
+template <class C, int S>
+__device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c, bool ok0,
+                                             double q, int mt, unsigned& st) {
+  {
     double eps = ok0 ? 1e-9 : 1e-8;
     int tries = ok0 ? 0 : 1;
     bool done = ok0;
@@ -346,6 +371,27 @@ __device__ __forceinline__ double quad_inverse(double (&r)[S], double* tile, int
       }
     }
   }
+  return q;
+}
+
+// SchedPipe: W_k = -(sym(w) + eps I)^-1 (offset form, parked in tw) and the
+// bordered elimination of X0_{k-1} (parked in tile, row S = z0) in one asm block.
+template <class C, int S>
+__device__ __forceinline__ double neg_inverse_and_quad(double (&w)[S], double* tw, double* tile,
+                                                       int c, int mt, unsigned& st, double off) {
+  lds_put(tw, c, w);
+  diag_add<S, kLdsRow>(tw, c, 1e-9 - 1.0 - off);
+  wave_sync();
+  double x[S];
+  sym_from<C, S, kLdsRow>(tw, c, w);
+  sym_from<C, S, kLdsRow>(tile, c, x);
+  double dminw = 1.0, acc = 0.0, dminx = 1.0;
+  SweepElimQ<S>::run(w, dminw, x, acc, dminx, 1e-9);
+  bool okw = pivots_ok(w, dminw);
+  double q = bcast<S>(acc);
+  const bool okx = (dminx > 0.0) && (q == q);
+  if (__any(!okw)) retry_inverse<C, S, kLdsRow>(w, tw, c, okw, mt, st);
+  if (__any(!okx)) q = quad_retry<C, S>(x, tile, c, okx, q, mt, st);
   wave_sync();
   return q;
 }
@@ -613,12 +659,15 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   constexpr bool OFF = offset_form<C>();
   constexpr bool TRAJ = has_traj<C>();
   static_assert(!TRAJ || (OFF && C::ELIM && !has_cldl<C>()), "trajectory form: SchedLdl family");
+  constexpr bool PIPE = has_pipe<C>();
+  static_assert(!PIPE || (has_qldl<C>() && !has_cldl<C>() && !TRAJ), "pipelined query: SchedLdl");
   constexpr int NN = G::NN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int WB = has_cldl<C>() ? G::WAVE_BYTES_X : (TRAJ ? G::WAVE_BYTES_T : G::WAVE_BYTES);
+  constexpr int WB =
+      (has_cldl<C>() || PIPE) ? G::WAVE_BYTES_X : (TRAJ ? G::WAVE_BYTES_T : G::WAVE_BYTES);
   unsigned char* wbase = smem_raw + w * WB;
   const unsigned wlds = (unsigned)(uintptr_t)wbase;  // LDS byte address (wave-uniform)
   double* tile = reinterpret_cast<double*>(wbase + G::OFF_T) + g * kLdsTile;
@@ -800,11 +849,38 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 
   dma_step(0);
   double Eb[S], H[S], Gb[S];
+  double NXp[S];  // SchedPipe: -QT_{k-1}^-1 + I, queried at the top of step k
   double best = 0.0;
   int tbest = 0;
   const bool fuse_argmin = a.t_max > 0;
 
   double jprev = 0.0;
+  // J(t) bookkeeping: non-finite status and the fused argmin (np.argmin: the
+  // first minimiser wins, a NaN wins)
+  auto take_j = [&](int t, double jk) {
+    if (!finite_val(jk)) st |= ST_NONFINITE;
+    if (fuse_argmin) {
+      if (t == a.t_min) {
+        best = jk;
+        tbest = t;
+      } else if (t > a.t_min && t <= a.t_max) {
+        const bool bnan = best != best, jnan = jk != jk;
+        if (!bnan && (jnan || jk < best)) {
+          best = jk;
+          tbest = t;
+        }
+      }
+    }
+  };
+  // SchedPipe: query of step k-1 (horizon k), X0 parked in the tile for the
+  // bordered elimination that runs inside the W_k sweep
+  auto pipe_query = [&]() {
+    double Mq[S], X0[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) Mq[i] = Gb[i] - NXp[i];  // QT^-1 + Gbar
+    query_x0_ldl<C, S>(Mq, H, Eb, X0, tile, c, mt, st);
+    lds_put(tile, c, X0);
+  };
   unsigned long long sec[15] = {};
   unsigned long long tprev = 0;
   auto stamp = [&](int j) {
@@ -819,11 +895,19 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
     stamp(-1);
+    if constexpr (PIPE) {
+      if (k > 0) pipe_query();  // needs no new input: runs before the DMA wait
+      stamp(9);
+    }
     dma_wait();
     wave_sync();
     // J of the previous step is stored only now, so that the vmcnt(0) above
     // never waits on a store issued at the end of the previous step
-    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
+    if constexpr (PIPE) {
+      if (k > 1 && valid && c == 0) a.J[prob * N + k - 2] = jprev;  // horizon k-1
+    } else {
+      if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
+    }
     double atil = 0.0;  // trajectory form: a~_k = a_k - B_k du_k (augmented.py:50)
     if constexpr (TRAJ) {
       // build the last row / column and the diagonal of Q_aug[k] (augmented.py:31-47)
@@ -1006,7 +1090,13 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       double NW[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) NW[i] = Gb[i] - NE[i];  // E_k + Gbar
-      neg_inverse_reg<C, S>(NW, tile, c, mt, st, -1.0);     // NW = -W
+      if constexpr (PIPE) {  // NW = -W, and J(k) = 1/2 z0^T X0_{k-1}^-1 z0 alongside
+        const double jk = 0.5 * neg_inverse_and_quad<C, S>(NW, tileX, tile, c, mt, st, -1.0);
+        take_j(k, jk);
+        jprev = jk;
+      } else {
+        neg_inverse_reg<C, S>(NW, tile, c, mt, st, -1.0);     // NW = -W
+      }
       stamp(4);
       double Z[S];
       if constexpr (OFF) copy(Z, H); else zero(Z);
@@ -1022,6 +1112,11 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     stamp(5);
 
     // ---- query horizon t = k + 1
+    if constexpr (PIPE) {  // deferred to the top of step k + 1 (or after the loop)
+      copy(NXp, NX);
+      load_rows();
+      continue;
+    }
     if constexpr (has_cldl<C>()) {
 #pragma unroll
       for (int i = 0; i < S; ++i) NX[i] = tileX[i * kLdsRow + c];
@@ -1054,23 +1149,23 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     }
     stamp(8);
     load_rows();  // trajectory form: next step's Q / P rows (constant LDS data)
-    if (!finite_val(jk)) st |= ST_NONFINITE;
+    take_j(k + 1, jk);
     jprev = jk;
-    if (fuse_argmin) {
-      const int t = k + 1;
-      if (t == a.t_min) {
-        best = jk;
-        tbest = t;
-      } else if (t > a.t_min && t <= a.t_max) {
-        const bool bnan = best != best, jnan = jk != jk;
-        if (!bnan && (jnan || jk < best)) {
-          best = jk;
-          tbest = t;
-        }
-      }
-    }
   }
   dma_wait();
+  if constexpr (PIPE) {  // the last query (horizon N) has no W sweep to ride in
+    if (N > 0) {
+      if (N > 1 && valid && c == 0) a.J[prob * N + N - 2] = jprev;
+      pipe_query();
+      double X0[S];
+      wave_sync();
+#pragma unroll
+      for (int i = 0; i < S; ++i) X0[i] = tile[i * kLdsRow + c];
+      const double jk = 0.5 * quad_inverse<C, S>(X0, tile, c, mt, st);
+      take_j(N, jk);
+      jprev = jk;
+    }
+  }
   if constexpr (C::STAMP) {
     if (lane == 0) {
       for (int j = 0; j < 15; ++j) atomicAdd(&g_hop_stamp[j], sec[j]);
@@ -1125,6 +1220,12 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return go(v2::lft_sweep_v2_kernel<v2::SchedLdl2Stamped, 13, 4>,
                 v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
     if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
+    if (variant == 26)
+      return go(v2::lft_sweep_v2_kernel<v2::SchedPipe, 13, 4>,
+                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
+    if (variant == 28)
+      return go(v2::lft_sweep_v2_kernel<v2::SchedPipeStamped, 13, 4>,
+                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
     return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
   }
   return hipErrorNotSupported;
