@@ -208,3 +208,33 @@ def test_select_from_trajectory_dropin_DI(dev, golden_dir):
                                      int(d["T_min"]), int(d["T_max"]))
     assert np.max(np.abs(J - d["J"]) / np.abs(d["J"])) <= 1e-3
     assert T == int(np.argmin(d["J"][int(d["T_min"]) - 1:int(d["T_max"])]) + int(d["T_min"]))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_traj_nonfinite_and_tiny_horizons(dev, monkeypatch, fused):
+    """A NaN in one problem's trajectory flags only that problem (FloatingPointError
+    in the reference); n_use = 1 and t_min = t_max work on both paths."""
+    from time_opt_ilqr_amd import engine
+    if not fused:
+        monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
+    n, m, N = 12, 4, 20
+    ps, st = _batch(range(1100, 1105), n, m, N)
+    X = st["X"].copy()
+    X[2, 7, 3] = np.nan
+    st2 = dict(st)
+    st2["X"] = X
+    args = (*_dev_args(st2, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
+    res = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=5, t_max=5)
+    status = res.status.cpu().numpy()
+    assert status[2] & 4
+    assert (np.delete(status, 2) == 0).all()
+    assert (np.delete(res.t_star.cpu().numpy(), 2) == 5).all()
+    J = res.J.cpu().numpy()
+    for b in (0, 1, 3, 4):
+        _, o = _oracle(ps[b], 1.0)
+        assert _rel(J[b], o["J"]) <= 1e-9
+    one = engine.propagate_traj(*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev),
+                                _t(st["w"], dev), wrap_idx=st["wrap_idx"], rho_reg=1.0, n_use=1)
+    for b in range(5):
+        _, o = _oracle(ps[b], 1.0, 1)
+        assert _rel(one.J[b].cpu(), o["J"]) <= 1e-9
