@@ -238,3 +238,32 @@ def test_traj_nonfinite_and_tiny_horizons(dev, monkeypatch, fused):
     for b in range(5):
         _, o = _oracle(ps[b], 1.0, 1)
         assert _rel(one.J[b].cpu(), o["J"]) <= 1e-9
+
+
+@pytest.mark.parametrize("n,m,dt,tol", [(4, 1, "f32", 2e-3), (4, 2, "f32", 2e-3), (3, 2, "f64", 1e-9),
+                                        (2, 1, "f64", 1e-9), (1, 1, "f64", 1e-9)])
+def test_traj_small_fused_vs_unfused_and_oracle(dev, monkeypatch, n, m, dt, tol):
+    """Small s: the in-register builders of lft_small_traj_kernel against
+    hop_augment + the small-s sweep and against the oracle (tails: 67 problems)."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    dtype = torch.float64 if dt == "f64" else torch.float32
+    N = 45
+    ps, st = _batch(range(1200, 1267), n, m, N)
+    args = (*_dev_args(st, dev, dtype), _t(st["R_inv"], dev, dtype), _t(st["P"], dev, dtype),
+            _t(st["w"], dev, dtype))
+    kw = dict(wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=N)
+    a = engine.propagate_traj(*args, **kw)
+    monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
+    b = engine.propagate_traj(*args, **kw)
+    Ja, Jb = a.J.double().cpu().numpy(), b.J.double().cpu().numpy()
+    assert _rel(Ja, Jb) <= (1e-11 if dt == "f64" else 2e-3)  # fp32: the 2e-3 bar
+    for i in (0, 33, 66):
+        _, o = _oracle(ps[i], 1.0)
+        assert _rel(Ja[i], o["J"]) <= tol
+    if dt == "f64":
+        assert (a.status.cpu().numpy() == 0).all()
+        for i in range(0, 67, 11):
+            _, o = _oracle(ps[i], 1.0)
+            T, _ = orc.select_horizon(o["J"][None], 3, N)
+            assert int(a.t_star[i]) == int(T[0])

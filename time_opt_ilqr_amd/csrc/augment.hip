@@ -7,7 +7,7 @@
 // builds the blocks inside the sweep for s = 13, m = 4).
 //
 // HBM-bound: per step it reads n^2 + nm + 2n + m values (+ extras) and writes
-// 3 s^2 + s m.  One workgroup owns KS consecutive steps of one problem: phase 1
+// 3 s^2 + s m.  One workgroup owns 256/n consecutive steps of one problem: phase 1
 // forms the per-step vectors (e_k, e_{k+1}, du_k, Q e, P e, a~) in LDS, phase 2
 // writes the blocks as contiguous, coalesced runs.
 #include "hop_device.hpp"
@@ -16,20 +16,24 @@
 namespace hop {
 namespace aug {
 
-constexpr int KS = 16;  // steps per workgroup (16 lanes per step in phase 1)
 constexpr int TPB = 256;
+// steps per workgroup: phase 1 maps one thread per (step, state) pair, so a
+// workgroup covers 256 / n steps (small n: long contiguous output runs)
+__host__ __device__ inline int steps_per_block(int n) { return TPB / n; }
 
 template <class T>
 __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
   const TrajArgs<T>& t = a.t;
   const int n = t.n, m = t.m, s = n + 1;
+  const int KS = steps_per_block(n);
   const int nchunk = (a.nbuild + KS - 1) / KS;
   const long long b = blockIdx.x / nchunk;
   const int k0 = (blockIdx.x % nchunk) * KS;
   const int ks = min(KS, a.nbuild - k0);
   const int NA = a.nalloc;
-  __shared__ T e0[KS][16], e1[KS][16], du[KS][16], qe[KS][16], pe[KS][16], at[KS][16];
-  __shared__ T eqe[KS], epe[KS];
+  // per-step vectors, [step][state] with row length n (KS * n <= 256)
+  __shared__ T e0[TPB], e1[TPB], qe[TPB], pe[TPB], at[TPB];
+  __shared__ T eqe[TPB], epe[TPB];
   __shared__ T sQ[16 * 16], sQs[16 * 16], sP[16 * 16];
 
   const T* xg = t.xg + b * t.xg_bs;
@@ -38,8 +42,8 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
   const T* P = t.P + b * t.p_bs;
   const T wt = t.w[b * t.w_bs];
   if (a.z0 && blockIdx.x == 0 && threadIdx.x < s) a.z0[threadIdx.x] = threadIdx.x == n ? T(1) : T(0);
-  const int tid = threadIdx.x, kk = tid >> 4, i = tid & 15, k = k0 + kk;
-  const bool row_ok = kk < ks;
+  const int tid = threadIdx.x, kk = tid / n, i = tid - kk * n, k = k0 + kk;
+  const bool row_ok = kk < ks;  // (threads past KS * n idle in phase 1)
 
   // phase 0: Q, _sym(Q) + q_reg I and P into LDS (one coalesced pass)
   for (int idx = tid; idx < n * n; idx += TPB) {
@@ -58,32 +62,32 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
         x0 = wrap_angle(x0);
         x1 = wrap_angle(x1);
       }
-      e0[kk][i] = x0;
-      e1[kk][i] = x1;
+      e0[kk * n + i] = x0;
+      e1[kk * n + i] = x1;
     }
-    if (i < m) du[kk][i] = t.U[(b * NA + k) * m + i] - ur[i];
   }
   __syncthreads();
   // phase 1b: Q e_k (augmented.py:35-36), P e_{k+1} (:78), a~ = a_k - B_k du_k (:50)
   if (row_ok && i < n) {
     T v = T(0), p = T(0), bd = T(0);
     for (int j = 0; j < n; ++j) {
-      v += sQ[i * n + j] * e0[kk][j];
-      p += sP[i * n + j] * e1[kk][j];
+      v += sQ[i * n + j] * e0[kk * n + j];
+      p += sP[i * n + j] * e1[kk * n + j];
     }
     const T* Bk = t.Bm + ((b * NA + k) * n + i) * m;
-    for (int q = 0; q < m; ++q) bd += Bk[q] * du[kk][q];
-    qe[kk][i] = v;
-    pe[kk][i] = p;
-    at[kk][i] = t.ares[(b * NA + k) * n + i] - bd;
+    const T* Uk = t.U + (b * NA + k) * m;
+    for (int q = 0; q < m; ++q) bd += Bk[q] * (Uk[q] - ur[q]);  // B_k du_k
+    qe[kk * n + i] = v;
+    pe[kk * n + i] = p;
+    at[kk * n + i] = t.ares[(b * NA + k) * n + i] - bd;
   }
   __syncthreads();
   // e^T Q e (:37) and e^T P e (:79; 2 * (1/2 e^T P e) is exact)
   if (row_ok && i == 0) {
     T v = T(0), p = T(0);
     for (int j = 0; j < n; ++j) {
-      v += e0[kk][j] * qe[kk][j];
-      p += e1[kk][j] * pe[kk][j];
+      v += e0[kk * n + j] * qe[kk * n + j];
+      p += e1[kk * n + j] * pe[kk * n + j];
     }
     T corner = v + T(2) * wt + t.rho_reg;
     if (t.c_extra) corner += T(2) * t.c_extra[b * NA + k];
@@ -133,12 +137,12 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
         vt = sP[i2 * n + j2];
         va = ra[u];
       } else if (i2 < n) {  // last column: Q e (+ cx)
-        vq = cx ? qe[qq][i2] + cx[qq * n + i2] : qe[qq][i2];
-        vt = pe[qq][i2];
-        va = at[qq][i2];
+        vq = cx ? qe[qq * n + i2] + cx[qq * n + i2] : qe[qq * n + i2];
+        vt = pe[qq * n + i2];
+        va = at[qq * n + i2];
       } else if (j2 < n) {  // last row
-        vq = cx ? qe[qq][j2] + cx[qq * n + j2] : qe[qq][j2];
-        vt = pe[qq][j2];
+        vq = cx ? qe[qq * n + j2] + cx[qq * n + j2] : qe[qq * n + j2];
+        vt = pe[qq * n + j2];
         va = T(0);
       } else {
         vq = eqe[qq];
@@ -162,7 +166,8 @@ __global__ __launch_bounds__(TPB) void augment_kernel(AugArgs<T> a) {
 
 template <class T>
 hipError_t dispatch_augment(const AugArgs<T>& a, hipStream_t stream) {
-  const long long nchunk = (a.nbuild + aug::KS - 1) / aug::KS;
+  const int ksb = aug::steps_per_block(a.t.n);
+  const long long nchunk = (a.nbuild + ksb - 1) / ksb;
   const long long blocks = a.batch * nchunk;
   if (blocks <= 0) return hipSuccess;
   if (blocks > 0x7FFFFFFFll) return hipErrorInvalidValue;

@@ -76,10 +76,15 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
   a.t_min = t_min; a.t_max = t_max;
   a.J = J; a.status = status; a.t_star = t_star; a.j_star = j_star;
   a.dbg_efg = dbg_efg; a.dbg_pre = dbg_pre;
-  if (traj) {  // in-kernel augmentation: only the fused fast path implements it
+  if (traj) {  // in-kernel augmentation: the s = 13 and the small-s kernels
     a.traj = 1;
     a.tr = *traj;
-    if constexpr (sizeof(T) == 8) return hip_status(hop::dispatch_lft_v2(a, (hipStream_t)stream));
+    if constexpr (sizeof(T) == 8) {
+      const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
+      if (e != hipErrorNotSupported) return hip_status(e);
+    }
+    const hipError_t e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);
+    if (e != hipErrorNotSupported) return hip_status(e);
     return fail(HOP_E_SIZE, "no fused trajectory-form sweep for this shape");
   }
   if (!getenv("HOP_FORCE_GENERIC")) {
@@ -171,10 +176,15 @@ hop::TrajArgs<T> traj_args(const T* A, const T* Bm, const T* a_res, const T* X, 
   return t;
 }
 
-// the sweep builds the blocks itself (no workspace) for these shapes
+// the sweep builds the blocks itself (no workspace) for these shapes: the
+// exact-size s = 13 kernel (fp64) and the small-s instantiations (lft_small.hip)
 bool traj_fused(int32_t n, int32_t m, int32_t elem_bytes, bool has_extra) {
-  if (getenv("HOP_FORCE_GENERIC") || getenv("HOP_TRAJ_UNFUSED")) return false;
-  return elem_bytes == 8 && n == 12 && m == 4 && !has_extra;
+  if (getenv("HOP_FORCE_GENERIC") || getenv("HOP_TRAJ_UNFUSED") || has_extra) return false;
+  if (elem_bytes == 8 && n == 12 && m == 4) return true;
+  const int s = n + 1;
+  const bool both = (s == 2 && m == 1) || (s == 3 && m == 1) || (s == 4 && (m == 1 || m == 2));
+  if (elem_bytes == 8) return both;
+  return both || (s == 5 && (m == 1 || m == 2));
 }
 
 constexpr int64_t kWsAlign = 256;

@@ -205,12 +205,227 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Trajectory form (augmented.py:10-87 inside the sweep): the wave streams the
+// raw A_k, B_k, x_{k+1}, a_k, u_k (chunk-major, as above) and every lane builds
+// its augmented blocks in registers.  Only e_{k+1} is new each step: Q e_k and
+// e_k^T Q e_k are carried from the previous step.
+template <class T, int S, int MM>
+struct GeoT {
+  static constexpr int NN = S - 1, TS = (int)sizeof(T);
+  static constexpr int CA = (NN * NN * TS + 15) / 16, CB = (NN * MM * TS + 15) / 16;
+  static constexpr int CX = (NN * TS + 15) / 16, CU = (MM * TS + 15) / 16;
+  static constexpr int P_A = 0, P_B = CA, P_X = CA + CB, P_V = P_X + CX, P_U = P_V + CX;
+  static constexpr int PIECES = P_U + CU;
+  static constexpr int WAVE_BYTES = PIECES * 1024;
+  static constexpr int TPB = 256;
+};
+
+template <class T, int S, int MM>
+__global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
+  using G = GeoT<T, S, MM>;
+  constexpr int NN = G::NN, TS = G::TS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned char* wimg = smem_raw + w * G::WAVE_BYTES;
+  const unsigned wlds = (unsigned)(uintptr_t)wimg;
+  const long long wave_prob0 = (long long)blockIdx.x * G::TPB + w * 64;
+  const long long prob = wave_prob0 + lane;
+  const bool valid = prob < a.batch;
+  const long long pb = valid ? prob : a.batch - 1;
+  const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
+  const int N = a.n, mt = a.max_tries, NA = a.nalloc;
+  const TrajArgs<T>& t = a.tr;
+  const long long pA = (long long)NA * NN * NN * TS, pB = (long long)NA * NN * MM * TS;
+  const long long pX = (long long)(NA + 1) * NN * TS, pV = (long long)NA * NN * TS;
+  const long long pU = (long long)NA * MM * TS;
+  auto mk = [&](const T* base, long long pstr) {  // exact bounds (per-dword range check)
+    const long long left = (a.batch - pb0) * pstr;
+    const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base) + pb0 * (pstr / TS), (short)0,
+                                             (int)nrec, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t rA = mk(t.A, pA), rB = mk(t.Bm, pB), rX = mk(t.X, pX),
+                               rV = mk(t.ares, pV), rU = mk(t.U, pU);
+  const unsigned vA = (unsigned)((pb - pb0) * pA), vB = (unsigned)((pb - pb0) * pB),
+                 vX = (unsigned)((pb - pb0) * pX), vV = (unsigned)((pb - pb0) * pV),
+                 vU = (unsigned)((pb - pb0) * pU);
+  auto dma_step = [&](int k) {  // A_k, B_k, x_{k+1}, a_k, u_k
+    const unsigned sA = (unsigned)(k * NN * NN * TS), sB = (unsigned)(k * NN * MM * TS),
+                   sX = (unsigned)((k + 1) * NN * TS), sV = (unsigned)(k * NN * TS),
+                   sU = (unsigned)(k * MM * TS);
+#pragma unroll
+    for (int r = 0; r < G::CA; ++r) dma16(vA + 16 * r, rA, wlds + (G::P_A + r) * 1024, sA);
+#pragma unroll
+    for (int r = 0; r < G::CB; ++r) dma16(vB + 16 * r, rB, wlds + (G::P_B + r) * 1024, sB);
+#pragma unroll
+    for (int r = 0; r < G::CX; ++r) dma16(vX + 16 * r, rX, wlds + (G::P_X + r) * 1024, sX);
+#pragma unroll
+    for (int r = 0; r < G::CX; ++r) dma16(vV + 16 * r, rV, wlds + (G::P_V + r) * 1024, sV);
+#pragma unroll
+    for (int r = 0; r < G::CU; ++r) dma16(vU + 16 * r, rU, wlds + (G::P_U + r) * 1024, sU);
+  };
+  auto vm_wait = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  // per-lane constants: raw Q (for Q e), _sym(Q) + q_reg I, P, xg, u_ref, 2w
+  T Qr[NN][NN], Qt[NN][NN], Pm[NN][NN], xg[NN], ur[MM];
+  {
+    const T* Qg = t.Q + pb * t.q_bs;
+    const T* Pg = t.P + pb * t.p_bs;
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        Qr[i][j] = Qg[i * NN + j];
+        Pm[i][j] = Pg[i * NN + j];
+      }
+#pragma unroll
+    for (int i = 0; i < NN; ++i)
+#pragma unroll
+      for (int j = 0; j < NN; ++j)
+        Qt[i][j] = T(0.5) * (Qr[i][j] + Qr[j][i]) + (i == j ? t.q_reg : T(0));
+#pragma unroll
+    for (int i = 0; i < NN; ++i) xg[i] = t.xg[pb * t.xg_bs + i];
+#pragma unroll
+    for (int q = 0; q < MM; ++q) ur[q] = t.u_ref[pb * t.ur_bs + q];
+  }
+  const T w2 = T(2) * t.w[pb * t.w_bs], rho = t.rho_reg;
+  auto err = [&](const T (&x)[NN], T (&e)[NN]) {  // wrap_error(x - xg) (utils.py:131-137)
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      const T d = x[i] - xg[i];
+      e[i] = ((t.wrap_mask >> i) & 1u) ? wrap_angle(d) : d;
+    }
+  };
+  auto quad_of = [&](const T (&M)[NN][NN], const T (&e)[NN], T (&me)[NN]) {  // M e, e^T M e
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      T v = T(0);
+#pragma unroll
+      for (int j = 0; j < NN; ++j) v += M[i][j] * e[j];
+      me[i] = v;
+    }
+    T s2 = T(0);
+#pragma unroll
+    for (int j = 0; j < NN; ++j) s2 += e[j] * me[j];
+    return s2;
+  };
+  T qe[NN], eqe;  // Q e_k, e_k^T Q e_k
+  {
+    T x0[NN], e0[NN];
+    const T* Xg = t.X + pb * (long long)(NA + 1) * NN;
+#pragma unroll
+    for (int i = 0; i < NN; ++i) x0[i] = Xg[i];
+    err(x0, e0);
+    eqe = quad_of(Qr, e0, qe);
+  }
+  T z[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) z[i] = i == NN ? T(1) : T(0);  // z0 = e_s (augmented.py:57)
+  State<T, S, MM> ps;
+  ps.st = 0;
+  ps.best = T(0);
+  ps.tbest = 0;
+  T rinv[MM][MM];  // R_inv_cached
+  {
+    const T* Rp = a.R + pb * a.r_bstride;
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+      for (int j = 0; j < MM; ++j) rinv[i][j] = Rp[i * MM + j];
+  }
+  if (N > 0) dma_step(0);
+  constexpr int JR = 8;  // J ring, as lft_small_kernel
+  T jring[JR];
+#pragma unroll
+  for (int i = 0; i < JR; ++i) jring[i] = T(0);
+  auto flush = [&](int k0, int cnt) {
+    if (valid) {
+#pragma unroll
+      for (int i = 0; i < JR; ++i)
+        if (i >= JR - cnt) a.J[prob * N + k0 + i - (JR - cnt)] = jring[i];
+    }
+  };
+#pragma unroll 1
+  for (int k = 0; k < N; ++k) {
+    vm_wait();
+    wave_sync();
+    if (k >= JR && k % JR == 0) flush(k - JR, JR);
+    T Ar[NN][NN], Br[NN][MM], x1[1][NN], av[1][NN], uu[1][MM];
+    read_block<T, NN, NN, G::P_A>(wimg, lane, Ar);
+    read_block<T, NN, MM, G::P_B>(wimg, lane, Br);
+    read_block<T, 1, NN, G::P_X>(wimg, lane, x1);
+    read_block<T, 1, NN, G::P_V>(wimg, lane, av);
+    read_block<T, 1, MM, G::P_U>(wimg, lane, uu);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (k + 1 < N) dma_step(k + 1);
+    // augmented blocks of step k (augmented.py:31-56, 77-86; the final _sym is exact)
+    Gen<T, S> Qk, Ak, QTk;
+    T Bk[S][MM];
+    T e1[NN], pe[NN], qe1[NN];
+    err(x1[0], e1);
+    const T epe = quad_of(Pm, e1, pe);
+    const T eqe1 = quad_of(Qr, e1, qe1);
+    T du[MM];
+#pragma unroll
+    for (int q = 0; q < MM; ++q) du[q] = uu[0][q] - ur[q];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+#pragma unroll
+      for (int j = 0; j < NN; ++j) {
+        Qk.a[i][j] = Qt[i][j];
+        QTk.a[i][j] = Pm[i][j];
+        Ak.a[i][j] = Ar[i][j];
+      }
+      Qk.a[i][NN] = Qk.a[NN][i] = qe[i];
+      QTk.a[i][NN] = QTk.a[NN][i] = pe[i];
+      T bd = T(0);
+#pragma unroll
+      for (int q = 0; q < MM; ++q) {
+        bd += Br[i][q] * du[q];
+        Bk[i][q] = Br[i][q];
+      }
+      Ak.a[i][NN] = av[0][i] - bd;
+      Ak.a[NN][i] = T(0);
+    }
+    Qk.a[NN][NN] = (eqe + w2) + rho;
+    QTk.a[NN][NN] = epe + rho;
+    Ak.a[NN][NN] = T(1);
+#pragma unroll
+    for (int q = 0; q < MM; ++q) Bk[NN][q] = T(0);
+    stage_compose<T, S, MM>(ps, k, Qk, Ak, Bk, rinv, mt);
+    const T jk = query<T, S, MM>(ps, QTk, z, mt);
+#pragma unroll
+    for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
+    jring[JR - 1] = jk;
+    take(ps, k + 1, jk, a.t_min, a.t_max);
+#pragma unroll
+    for (int i = 0; i < NN; ++i) qe[i] = qe1[i];
+    eqe = eqe1;
+  }
+  vm_wait();
+  if (N > 0) {
+    const int tail = N % JR == 0 ? JR : N % JR;
+    flush(N - tail, tail);
+  }
+  if (valid) {
+    a.status[prob] = (int)ps.st;
+    if (a.t_max > 0 && a.t_star != nullptr) {
+      a.t_star[prob] = ps.tbest;
+      a.j_star[prob] = ps.best;
+    }
+  }
+}
+
 }  // namespace small
 
 // small-s path: returns hipErrorNotSupported when the shape has no instantiation
 template <class T>
 hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
+  if (a.traj && (a.tr.n != a.s - 1 || a.tr.m != a.m || !a.r_is_inv)) return hipErrorNotSupported;
   auto go = [&](auto kern, int bytes) {
     const long long blocks = (a.batch + 255) / 256;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
@@ -218,7 +433,9 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   };
 #define HOP_SMALL(S_, M_)                                                                 \
   if (a.s == S_ && a.m == M_)                                                             \
-    return go(small::lft_small_kernel<T, S_, M_>, small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+    return a.traj ? go(small::lft_small_traj_kernel<T, S_, M_>,                           \
+                       small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                           \
+                  : go(small::lft_small_kernel<T, S_, M_>, small::Geo<T, S_, M_>::WAVE_BYTES * 4);
   if constexpr (sizeof(T) == 4) {
     HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)
     HOP_SMALL(5, 2)  // s = 6 spills: generic kernel

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--n", type=int, default=12)
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=9)
     args = ap.parse_args()
@@ -30,8 +31,9 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(11)
     Bn, n, m, N = args.batch, args.n, args.m, args.N
-    kw = dict(device=dev, dtype=torch.float64, generator=g)
-    eye = torch.eye(n, device=dev, dtype=torch.float64)
+    fdt = torch.float64 if args.dtype == "f64" else torch.float32
+    kw = dict(device=dev, dtype=fdt, generator=g)
+    eye = torch.eye(n, device=dev, dtype=fdt)
     A = eye + 0.05 * torch.randn((Bn, N, n, n), **kw)
     Bm = 0.1 * torch.randn((Bn, N, n, m), **kw)
     X = 0.5 * torch.randn((Bn, N + 1, n), **kw)
@@ -65,8 +67,8 @@ def main():
 
     paths = {
         "traj_fused": lambda: engine.propagate_traj(*targs, t_min=1, t_max=N),
-        "traj_fused_wrap3": lambda: engine.propagate_traj(*targs, wrap_idx=[3, 4, 5], t_min=1,
-                                                          t_max=N),
+        "traj_fused_wrap": lambda: engine.propagate_traj(*targs, wrap_idx=[n - 1], t_min=1,
+                                                         t_max=N),
         "sweep_prebuilt": lambda: engine.propagate(blk.A, blk.B, blk.Q, Rinv, blk.z0, blk.QT,
                                                    t_min=1, t_max=N),
         "augment_only": lambda: engine.augment(A, Bm, a_res, X, U, xg, ur, Q, P, w),
@@ -83,7 +85,8 @@ def main():
     for name, v in samples.items():
         v = sorted(v)
         ms = v[len(v) // 2]
-        print(json.dumps({"path": name, "batch": Bn, "n": n, "m": m, "N": N, "ms_median": ms,
+        print(json.dumps({"path": name, "batch": Bn, "n": n, "m": m, "N": N, "dtype": args.dtype,
+                          "ms_median": ms,
                           "ms_min": v[0], "sweeps_per_s": Bn / (ms * 1e-3)}), flush=True)
 
 
