@@ -3,6 +3,8 @@
 Drop-in for the hot path of dmmsjtu-umich/time-opt-ilqr:
 
   engine.propagate / engine.select_horizon / engine.riccati   batched device API
+  engine.propagate_traj / engine.augment                       trajectory form (augmented.py
+                                                               builders on the device)
   horizon_selection.propagator_all_Jt_aug, ...                 reference-shaped drop-ins
 
 All arithmetic runs in libhop_amd.so (hand-written gfx950 HIP, C ABI in
@@ -11,14 +13,15 @@ calls raise.
 """
 from . import _lib
 from ._lib import HopError, ST_FAIL, ST_JITTER, ST_LU, ST_NONFINITE
-from .engine import propagate, riccati, select_horizon
+from .engine import augment, propagate, propagate_traj, riccati, select_horizon
 from .horizon_selection import (backward_pass_truncated, bruteforce_all_Jt_backward_expansion,
-                                propagator_all_Jt_aug, value_expansions_and_gains_prefix)
+                                propagator_all_Jt_aug, select_from_trajectory,
+                                value_expansions_and_gains_prefix)
 
 __all__ = [
-    "propagate", "select_horizon", "riccati",
+    "propagate", "select_horizon", "riccati", "propagate_traj", "augment",
     "propagator_all_Jt_aug", "backward_pass_truncated", "value_expansions_and_gains_prefix",
-    "bruteforce_all_Jt_backward_expansion",
+    "bruteforce_all_Jt_backward_expansion", "select_from_trajectory",
     "HopError", "ST_JITTER", "ST_LU", "ST_NONFINITE", "ST_FAIL",
 ]
 
