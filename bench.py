@@ -30,6 +30,15 @@ SMALL_SHAPES = {"f32": {(2, 1), (3, 1), (4, 1), (4, 2), (5, 1), (5, 2)},
                 "f64": {(2, 1), (3, 1), (4, 1), (4, 2)}}
 
 
+def baseline_metric():
+    """BASELINE.json's metric string (the driver compares the line against it)."""
+    try:
+        with open(os.path.join(REPO, "BASELINE.json")) as f:
+            return json.load(f)["metric"]
+    except (OSError, ValueError, KeyError):
+        return "batched iLQR backward sweeps/sec, Quadrotor n=13 N=100, at 1/2/4/8 GPU"
+
+
 def kernel_path(s, m, dtype):
     """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound."""
     if dtype == "f64" and (s, m) == (13, 4):
@@ -191,7 +200,7 @@ def main():
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(s, m, N)
         line = {
-            "metric": "batched iLQR backward sweeps/sec, Quadrotor n=13 N=100",
+            "metric": baseline_metric(),
             "value": value,
             "unit": "sweeps/s",
             "n_gpus": world,
