@@ -290,3 +290,28 @@ def test_wrap_angle_matches_python_remainder(small_host, dt):
         pi32, tp32 = np.float32(math.pi), np.float32(2.0 * math.pi)
         ref = np.remainder(vals + pi32, tp32) - pi32
         assert np.array_equal(out, ref.astype(np.float32))
+
+
+def test_traj_entry_validation_and_workspace_query(lib):
+    """hop_lft_sweep_traj_* / hop_augment_* reject bad shapes on the host; the
+    workspace query is 0 exactly for the shapes with an in-kernel builder."""
+    nul = None
+    traj_args = [nul] * 6 + [0, nul, 0, nul, 0, nul, 0, nul, 0, nul, nul, nul]
+    # n = 16 (s = 17) is over the 16-lane limit
+    rc = lib.hop_lft_sweep_traj_f64(*traj_args, 0, 1e-9, 1e-12, nul, 0, 4, 10, 10, 16, 4, 8, 0, 0,
+                                    nul, nul, nul, nul, nul, 0, nul)
+    assert rc == -2 and b"n must be" in lib.hop_last_error()
+    rc = lib.hop_lft_sweep_traj_f64(*traj_args, 0, 1e-9, 1e-12, nul, 0, 4, 10, 11, 12, 4, 8, 0, 0,
+                                    nul, nul, nul, nul, nul, 0, nul)
+    assert rc == -1 and b"n_use > n_alloc" in lib.hop_last_error()
+    rc = lib.hop_augment_f64(*traj_args, 1 << 12, 1e-9, 1e-12, 4, 10, 10, 12, 4,
+                             nul, nul, nul, nul, nul, nul)
+    assert rc == -1  # null inputs (checked before the wrap mask)
+    ws = lib.hop_lft_sweep_traj_workspace_bytes
+    assert ws(4096, 100, 12, 4, 8, 0) == 0          # Quadrotor shape, fp64: fused
+    assert ws(65536, 200, 4, 1, 4, 0) == 0          # Cartpole shape, fp32: fused (small s)
+    assert ws(4096, 100, 12, 4, 8, 1) > 0           # extra_stage_cost: builder + sweep
+    s, m, steps = 16, 6, 7 * 30
+    need = ws(7, 30, 15, 6, 8, 0)
+    assert need >= 8 * steps * (3 * s * s + s * m)
+    assert ws(0, 30, 15, 6, 8, 0) == 0
