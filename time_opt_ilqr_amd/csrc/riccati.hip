@@ -41,7 +41,10 @@ __device__ __forceinline__ void rload_row(const T* M, int rows, int cols, int c,
   }
 }
 
-template <class T, int S, int MM>
+// section stamps of the diagnostic instantiation (tools/stamps_riccati.py)
+__device__ unsigned long long g_ric_stamp[16];
+
+template <class T, int S, int MM, bool STAMP = false>
 __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
@@ -78,6 +81,17 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   Lw = max(Lw, __shfl_xor(Lw, 32));
   Lw = __builtin_amdgcn_readfirstlane(Lw);
   const T lam0 = a.lm[pb];
+  unsigned long long sec[10] = {};
+  unsigned long long tprev = 0;
+  auto stamp = [&](int j) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tt = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (j >= 0) sec[j] += tt - tprev;
+      tprev = tt;
+    }
+  };
 
   // loop-invariant cost blocks
   {
@@ -128,29 +142,46 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   }
 
   // step i's A, B, x, u are loaded one step ahead (software pipeline): the
-  // global-load latency of step i-1 hides behind step i's arithmetic
+  // global-load latency of step i-1 hides behind step i's arithmetic.
+  // MERGE (fp64, S + MM <= 16): B's columns ride on lanes S..S+m-1 of the same
+  // registers as A's ("ab" = [A | B] column per lane), so Vxx [A|B], A^T Vxx [A|B]
+  // and B^T Vxx [A|B] are three products instead of five, and one load per row.
+  constexpr bool MERGE = sizeof(T) == 8 && S + MM <= kRowLanes;
   T acol_n[S], bcol_n[S], x_n, u_n;
+  const bool lane_a = c < S, lane_in = c < S ? c < n : (c - S) < m;
+  const int col_ab = c < S ? (c < n ? c : n - 1) : (c - S < m ? c - S : m - 1);
   auto load_step = [&](int i) {
-    rload_col(Ap + (long long)i * nn, n, n, c, T(0), acol_n);
-    rload_col(Bp + (long long)i * nm, n, m, c, T(0), bcol_n);  // lanes c < m: column c of B_i
+    if constexpr (MERGE) {
+      const T* base = lane_a ? Ap + (long long)i * nn + col_ab : Bp + (long long)i * nm + col_ab;
+      const int ld = lane_a ? n : m;
+#pragma unroll
+      for (int j = 0; j < S; ++j) acol_n[j] = base[(j < n ? j : n - 1) * ld];
+#pragma unroll
+      for (int j = 0; j < S; ++j) acol_n[j] = (j < n && lane_in) ? acol_n[j] : T(0);
+    } else {
+      rload_col(Ap + (long long)i * nn, n, n, c, T(0), acol_n);
+      rload_col(Bp + (long long)i * nm, n, m, c, T(0), bcol_n);  // lanes c < m: column c of B_i
+    }
     x_n = Xp[(long long)i * n + (c < n ? c : 0)];
     u_n = Up[(long long)i * m + (c < m ? c : 0)];
   };
   if (Lw > 0) load_step(Lw - 1);
 #pragma unroll 1
   for (int i = Lw - 1; i >= 0; --i) {
+    stamp(-1);
     const bool act = alive && (i < L);
     T e = (c < n) ? x_n - xg_c : T(0);
     if (wrap_c) e = wrap_angle(e);
     const T du = (c < m) ? u_n - ur_c : T(0);
     T acol[S], bcol[S];
     copy(acol, acol_n);
-    copy(bcol, bcol_n);
+    if constexpr (!MERGE) copy(bcol, bcol_n);
     load_step(i > 0 ? i - 1 : 0);
     if (!__any(act)) continue;
     const unsigned long long badm = __ballot(!(finite_val(e) && finite_val(du)));
     const bool bad = ((badm >> (16 * g)) & 0xffffull) != 0ull;
 
+    stamp(0);
     // lx = Q e (+ cx), lu = R du, l0
     T lx = T(0), lu = T(0);
     {
@@ -182,30 +213,48 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       symmetrize(qst, tile, c);
     }
 
+    stamp(1);
     // Q-function assembly
     T qx = lx, qu = lu;
-    LaneDot<S>::fma(qx, vx, acol);  // Qx = lx + A^T Vx
-    LaneDot<S>::fma(qu, vx, bcol);  // Qu = lu + B^T Vx   (lanes < m)
-    T VA[S];
-    zero(VA);
-    acc_xy<false>(VA, Vxx, acol);   // Vxx A
-    T VB[S];
-    zero(VB);
-    acc_xy<false>(VB, Vxx, bcol);   // Vxx B          (lanes < m)
-    T Qxx[S];
+    T VA[S], Qxx[S], Quu[MM], Qux[MM];
     copy(Qxx, qst);
-    acc_xty<false>(Qxx, acol, VA);  // Qst + A^T Vxx A
-    T Quu[MM];
-    copy(Quu, rcol);
-    acc_xty<false, T, MM, S>(Quu, bcol, VB);  // R + B^T Vxx B   (lanes < m)
-    T Qux[MM];
-    zero(Qux);
-    acc_xty<false, T, MM, S>(Qux, bcol, VA);  // B^T Vxx A       (lanes < n)
+    if constexpr (MERGE) {
+      T qab = T(0);
+      LaneDot<S>::fma(qab, vx, acol);  // lanes < S: A^T Vx; lanes S..: B^T Vx
+      qx += qab;                       // Qx = lx + A^T Vx
+      qu += ror_row<kRowLanes - S>(qab);  // Qu = lu + B^T Vx, moved to lanes 0..m-1
+      zero(VA);
+      acc_xy<false>(VA, Vxx, acol);    // Vxx [A | B]
+      acc_xty<false>(Qxx, acol, VA);   // Qst + A^T Vxx A   (lanes < S)
+      T QB[MM];
+      zero(QB);
+      static_for<S>([&](auto J) { LaneBOff<MM, S>::fma(QB, acol[J], VA[J]); });  // B^T Vxx [A|B]
+#pragma unroll
+      for (int r = 0; r < MM; ++r) {
+        Qux[r] = QB[r];                                        // lanes < n: B^T Vxx A
+        Quu[r] = rcol[r] + ror_row<kRowLanes - S>(QB[r]);      // R + B^T Vxx B, lanes < m
+      }
+    } else {
+      LaneDot<S>::fma(qx, vx, acol);  // Qx = lx + A^T Vx
+      LaneDot<S>::fma(qu, vx, bcol);  // Qu = lu + B^T Vx   (lanes < m)
+      zero(VA);
+      acc_xy<false>(VA, Vxx, acol);   // Vxx A
+      T VB[S];
+      zero(VB);
+      acc_xy<false>(VB, Vxx, bcol);   // Vxx B          (lanes < m)
+      acc_xty<false>(Qxx, acol, VA);  // Qst + A^T Vxx A
+      copy(Quu, rcol);
+      acc_xty<false, T, MM, S>(Quu, bcol, VB);  // R + B^T Vxx B   (lanes < m)
+      zero(Qux);
+      acc_xty<false, T, MM, S>(Qux, bcol, VA);  // B^T Vxx A       (lanes < n)
+    }
 
     // regularised solve: Quu_reg = sym(Quu) + lam I ; (Quu_reg + eps I)^-1
+    stamp(2);
     T QuuT[MM];
     transpose(QuuT, Quu, tile, c);
     T Qi[MM];
+    stamp(3);
     bool solved = false;
     if (mode == 0) {
 #pragma unroll
@@ -231,6 +280,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
     }
     const bool fail_row = act && (bad || !solved);
 
+    stamp(4);
     // gains
     T K[MM];
     zero(K);
@@ -238,6 +288,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
     T kv = T(0);
     LaneDot<MM>::fma_neg(kv, qu, Qi);     // k = -Quu_reg^-1 Qu    (lanes < m)
 
+    stamp(5);
     // value update
     T Vn[S];
     copy(Vn, Qxx);
@@ -260,6 +311,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       LaneDot<MM>::fma(vxn, kv, Qux);        // Qx - Qux^T Quu^-1 Qu
       v0n = l0 + v0 + T(0.5) * row_sum_dpp((c < m) ? qu * kv : T(0));
     }
+    stamp(6);
     symmetrize(Vn, tile, c);
     bool vbad = !finite_val(vxn) || !finite_val(v0n);
 #pragma unroll
@@ -267,6 +319,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
     const unsigned long long vbm = __ballot(vbad && c < n);
     const bool vfail = act && (((vbm >> (16 * g)) & 0xffffull) != 0ull);
 
+    stamp(7);
     const bool commit = act && !fail_row && !vfail;
     if (act && (fail_row || vfail)) {
       st |= ST_FAIL;
@@ -278,11 +331,13 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       for (int r = 0; r < S; ++r) Vxx[r] = Vn[r];
       vx = vxn;
       v0 = v0n;
+#if !defined(HOP_RIC_EXP) || HOP_RIC_EXP != 1
       T* Ko = a.K + (pb * NA + i) * (long long)m * n;
 #pragma unroll
       for (int r = 0; r < MM; ++r)
         if (r < m && c < n) Ko[r * n + c] = K[r];
       if (c < m) a.k[(pb * NA + i) * m + c] = kv;
+#endif
       if (a.Vxx) {
         T* o = a.Vxx + (pb * (NA + 1) + i) * nn;
 #pragma unroll
@@ -292,6 +347,13 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       if (a.Vx && c < n) a.Vx[pb * (NA + 1) * n + (long long)i * n + c] = vxn;
       if (a.V0 && c == 0) a.V0[pb * (NA + 1) + i] = v0n;
     }
+    stamp(8);
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      for (int j = 0; j < 10; ++j) atomicAdd(&g_ric_stamp[j], sec[j]);
+      atomicAdd(&g_ric_stamp[15], 1ull);
+    }
   }
   if (valid && c == 0) a.status[prob] = (int)st;
 }
@@ -300,7 +362,13 @@ template <class T, int S, int MM>
 hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   const size_t lds = (size_t)2 * kProbPerBlock * kLdsTile * sizeof(T);
-  hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream, a);
+  const char* ev = getenv("HOP_RIC_STAMP");  // diagnostic: section stamps
+  if (ev && atoi(ev) == 1)
+    hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), dim3((unsigned)blocks), dim3(256), lds,
+                       stream, a);
+  else
+    hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream,
+                       a);
   return hipGetLastError();
 }
 
@@ -319,3 +387,16 @@ template hipError_t dispatch_riccati<double>(const RiccatiArgs<double>&, hipStre
 template hipError_t dispatch_riccati<float>(const RiccatiArgs<float>&, hipStream_t);
 
 }  // namespace hop
+
+// Diagnostic (not part of include/hop.h): read (and optionally reset) the Riccati
+// section stamps (HOP_RIC_STAMP=1).
+extern "C" int hop_debug_ric_stamps(unsigned long long* host16, int reset) {
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(hop::g_ric_stamp), 16 * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return -3;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hop::g_ric_stamp), z, sizeof(z)) != hipSuccess) return -3;
+  }
+  return 0;
+}
