@@ -300,12 +300,12 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       T qk = T(0);
       LaneDot<MM>::fma(qk, kv, QuuT);      // (Quu k)[c]
       LaneDot<MM>::fma(vxn, qk, K);        // + K^T Quu k
-      acc_xty<false, T, S, MM>(Vn, K, Qux);  // + K^T Qux
-      acc_xty<false, T, S, MM>(Vn, Qux, K);  // + Qux^T K
+      // K^T Qux + Qux^T K + K^T Quu K = K^T (Qux + Quu K) + Qux^T K (one product fewer)
       T QK[MM];
-      zero(QK);
-      acc_xy<false, T, MM, MM>(QK, Quu, K);  // Quu K
-      acc_xty<false, T, S, MM>(Vn, K, QK);   // + K^T Quu K
+      copy(QK, Qux);
+      acc_xy<false, T, MM, MM>(QK, Quu, K);  // Qux + Quu K
+      acc_xty<false, T, S, MM>(Vn, K, QK);   // + K^T (Qux + Quu K)
+      acc_xty<false, T, S, MM>(Vn, Qux, K);  // + Qux^T K
     } else {
       acc_xty<false, T, S, MM>(Vn, Qux, K);  // Qxx - Qux^T Quu^-1 Qux
       LaneDot<MM>::fma(vxn, kv, Qux);        // Qx - Qux^T Quu^-1 Qu
