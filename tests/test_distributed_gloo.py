@@ -45,9 +45,10 @@ def _worker(rank, world, port, total, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("total", [9, 16])
-def test_gloo_world2_shards_and_gather(tmp_path, total):
-    world = 2
+@pytest.mark.parametrize("world,total", [(2, 9), (2, 16), (4, 9), (4, 3)])
+def test_gloo_shards_and_gather(tmp_path, world, total):
+    """world 2 and a 4-rank rehearsal (uneven shards, and more ranks than
+    problems for some: 3 problems over 4 ranks leaves one rank empty)."""
     mp.spawn(_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)
     got = np.load(tmp_path / "gathered.npz")
     from oracle import hop_oracle as orc
