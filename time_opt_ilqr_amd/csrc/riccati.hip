@@ -331,13 +331,11 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       for (int r = 0; r < S; ++r) Vxx[r] = Vn[r];
       vx = vxn;
       v0 = v0n;
-#if !defined(HOP_RIC_EXP) || HOP_RIC_EXP != 1
       T* Ko = a.K + (pb * NA + i) * (long long)m * n;
 #pragma unroll
       for (int r = 0; r < MM; ++r)
         if (r < m && c < n) Ko[r * n + c] = K[r];
       if (c < m) a.k[(pb * NA + i) * m + c] = kv;
-#endif
       if (a.Vxx) {
         T* o = a.Vxx + (pb * (NA + 1) + i) * nn;
 #pragma unroll
