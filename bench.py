@@ -42,7 +42,7 @@ def baseline_metric():
 def kernel_path(s, m, dtype):
     """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound."""
     if dtype == "f64" and (s, m) == (13, 4):
-        return "lft_sweep_v2_kernel<SchedLdl,13,4>", "mfma"
+        return "lft_sweep_v2_kernel<SchedLdlDma,13,4>", "mfma"
     if (s, m) in SMALL_SHAPES[dtype]:
         return f"lft_small_kernel<{'float' if dtype == 'f32' else 'double'},{s},{m}>", "hbm"
     return "lft_sweep_kernel", "mfma"

@@ -64,13 +64,13 @@ __device__ __forceinline__ double sel_lane(double a, double b) {
 
 // Schedules.  PIV: 0 select pivots, 4 short C++ chain, 5 whole-sweep asm.
 struct Select {
-  static constexpr int PIV = 0, NR = 1, LDSASM = 0, ELIM = 0, STAMP = 0, XYROW = 0;
+  static constexpr int PIV = 0, NR = 1, LDSASM = 0, ELIM = 0, STAMP = 0, XYROW = 0, DMA1 = 0;
 };
 struct Chain {
-  static constexpr int PIV = 4, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0, XYROW = 0;
+  static constexpr int PIV = 4, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0, XYROW = 0, DMA1 = 0;
 };
 struct Sched {
-  static constexpr int PIV = 5, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0, XYROW = 0;
+  static constexpr int PIV = 5, NR = 1, LDSASM = 1, ELIM = 1, STAMP = 0, XYROW = 0, DMA1 = 0;
 };
 struct SchedRow : Sched {  // X*Y products as one dependent chain per output row
   static constexpr int XYROW = 1;
@@ -113,6 +113,13 @@ struct SchedPipe : SchedLdl {
   static constexpr int PIPE = 1;
 };
 struct SchedPipeStamped : SchedPipe {
+  static constexpr int STAMP = 1;
+};
+// the step's 20 LDS-DMA pieces issued from one asm block (dma_step20)
+struct SchedLdlDma : SchedLdl {
+  static constexpr int DMA1 = 1;
+};
+struct SchedLdlDmaStamped : SchedLdlDma {
   static constexpr int STAMP = 1;
 };
 template <class C>
@@ -605,6 +612,43 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
 
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// One step's 20 LDS-DMA pieces (Q, A, B, QT images of s = 13, m = 4) in one asm
+// block: M0 saved once and set per piece from the wave's LDS base plus an
+// immediate (no per-piece SGPR, no readlane of spilled addresses, no save /
+// restore pair per piece).
+template <int OQ, int OA, int OB, int OT>
+__device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsigned (&vb)[2],
+                                           __amdgpu_buffer_rsrc_t rQ, __amdgpu_buffer_rsrc_t rA,
+                                           __amdgpu_buffer_rsrc_t rB, __amdgpu_buffer_rsrc_t rT,
+                                           unsigned wlds, unsigned soM, unsigned soB) {
+  unsigned keep;
+#define HOP_P(R, V, OFF, SO)                                                  \
+  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
+  "], %[" #SO "] offen lds\n\t"
+  asm volatile(
+      "s_mov_b32 %[keep], m0\n\t"
+      HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
+      HOP_P(rq, v3, %[q3], sm) HOP_P(rq, v4, %[q4], sm) HOP_P(rq, v5, %[q5], sm)
+      HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
+      HOP_P(ra, v3, %[a3], sm) HOP_P(ra, v4, %[a4], sm) HOP_P(ra, v5, %[a5], sm)
+      HOP_P(rb, u0, %[b0], sb) HOP_P(rb, u1, %[b1], sb)
+      HOP_P(rt, v0, %[t0], sm) HOP_P(rt, v1, %[t1], sm) HOP_P(rt, v2, %[t2], sm)
+      HOP_P(rt, v3, %[t3], sm) HOP_P(rt, v4, %[t4], sm) HOP_P(rt, v5, %[t5], sm)
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [w] "s"(wlds), [sm] "s"(soM), [sb] "s"(soB), [rq] "s"(rQ), [ra] "s"(rA), [rb] "s"(rB),
+        [rt] "s"(rT), [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]),
+        [v4] "v"(vm[4]), [v5] "v"(vm[5]), [u0] "v"(vb[0]), [u1] "v"(vb[1]),
+        [q0] "i"(OQ), [q1] "i"(OQ + 1024), [q2] "i"(OQ + 2048), [q3] "i"(OQ + 3072),
+        [q4] "i"(OQ + 4096), [q5] "i"(OQ + 5120), [a0] "i"(OA), [a1] "i"(OA + 1024),
+        [a2] "i"(OA + 2048), [a3] "i"(OA + 3072), [a4] "i"(OA + 4096), [a5] "i"(OA + 5120),
+        [b0] "i"(OB), [b1] "i"(OB + 1024), [t0] "i"(OT), [t1] "i"(OT + 1024),
+        [t2] "i"(OT + 2048), [t3] "i"(OT + 3072), [t4] "i"(OT + 4096), [t5] "i"(OT + 5120)
+      : "memory", "scc");
+#undef HOP_P
+}
+
+
 template <int S, int MM>
 struct Geo {
   static constexpr int SS = S * S;
@@ -759,6 +803,12 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       return;
     }
     const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
+    if constexpr (C::DMA1 && G::NJM == 6 && G::NJB == 2) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
+                                                         soB);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rQ, wlds + G::OFF_Q + 1024 * j, soM);
 #pragma unroll
@@ -1206,7 +1256,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return hipGetLastError();
   };
   const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
-  const int variant = ev ? atoi(ev) : 14;
+  const int variant = ev ? atoi(ev) : 30;
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
     if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes);
@@ -1223,10 +1273,13 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     if (variant == 26)
       return go(v2::lft_sweep_v2_kernel<v2::SchedPipe, 13, 4>,
                 v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
+    if (variant == 30) return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes);
+    if (variant == 32) return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDmaStamped, 13, 4>, bytes);
     if (variant == 28)
       return go(v2::lft_sweep_v2_kernel<v2::SchedPipeStamped, 13, 4>,
                 v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
-    return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
+    if (variant == 14) return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
+    return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes);
   }
   return hipErrorNotSupported;
 }

@@ -1,4 +1,4 @@
-"""Per-section cycle breakdown of the LFT kernel (diagnostic variant 20 = Sched + stamps).
+"""Per-section cycle breakdown of the LFT kernel (diagnostic variant 32 = default + stamps; 20 = SchedLdl).
 
     python tools/stamps.py [--batch 4096] [--N 100]
 
@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=100)
-    ap.add_argument("--variant", type=int, default=20)
+    ap.add_argument("--variant", type=int, default=32)
     ap.add_argument("--traj", action="store_true",
                     help="trajectory-form sweep (in-kernel builders, variant 24)")
     args = ap.parse_args()
