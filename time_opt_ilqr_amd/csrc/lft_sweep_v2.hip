@@ -612,6 +612,37 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
 
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Trajectory form: the step's 10 raw pieces (A 5, B 2, x, a, u) in one asm block
+template <int OA, int OB, int OX, int OV, int OU>
+__device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsigned (&vb)[2],
+                                           unsigned vx, unsigned vv, unsigned vu,
+                                           __amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
+                                           __amdgpu_buffer_rsrc_t rX, __amdgpu_buffer_rsrc_t rV,
+                                           __amdgpu_buffer_rsrc_t rU, unsigned wlds, unsigned sA,
+                                           unsigned sB, unsigned sX, unsigned sV, unsigned sU) {
+  unsigned keep;
+#define HOP_P(R, V, OFF, SO)                                                  \
+  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
+  "], %[" #SO "] offen lds\n\t"
+  asm volatile(
+      "s_mov_b32 %[keep], m0\n\t"
+      HOP_P(ra, a0, %[o0], sa) HOP_P(ra, a1, %[o1], sa) HOP_P(ra, a2, %[o2], sa)
+      HOP_P(ra, a3, %[o3], sa) HOP_P(ra, a4, %[o4], sa)
+      HOP_P(rb, b0, %[p0], sb) HOP_P(rb, b1, %[p1], sb)
+      HOP_P(rx, x0, %[ox], sx) HOP_P(rv, x1, %[ov], sv) HOP_P(ru, x2, %[ou], su)
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [w] "s"(wlds), [sa] "s"(sA), [sb] "s"(sB), [sx] "s"(sX), [sv] "s"(sV), [su] "s"(sU),
+        [ra] "s"(rA), [rb] "s"(rB), [rx] "s"(rX), [rv] "s"(rV), [ru] "s"(rU),
+        [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]), [a4] "v"(va[4]),
+        [b0] "v"(vb[0]), [b1] "v"(vb[1]), [x0] "v"(vx), [x1] "v"(vv), [x2] "v"(vu),
+        [o0] "i"(OA), [o1] "i"(OA + 1024), [o2] "i"(OA + 2048), [o3] "i"(OA + 3072),
+        [o4] "i"(OA + 4096), [p0] "i"(OB), [p1] "i"(OB + 1024), [ox] "i"(OX), [ov] "i"(OV),
+        [ou] "i"(OU)
+      : "memory", "scc");
+#undef HOP_P
+}
+
 // One step's 20 LDS-DMA pieces (Q, A, B, QT images of s = 13, m = 4) in one asm
 // block: M0 saved once and set per piece from the wave's LDS base plus an
 // immediate (no per-piece SGPR, no readlane of spilled addresses, no save /
@@ -790,6 +821,13 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
                      soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
       const unsigned soX = soV + NN * 8;
+      if constexpr (G::NJA == 5 && G::NJR == 2 && G::NJX == 1 && G::NJV == 1 && G::NJU == 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
+            voTA, voTR, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR, soX, soV,
+            soU);
+        return;
+      }
 #pragma unroll
       for (int j = 0; j < G::NJA; ++j) dma16(voTA[j], rQ, wlds + G::OFF_A + 1024 * j, soA);
 #pragma unroll
