@@ -42,6 +42,8 @@ def baseline_metric():
 def kernel_path(s, m, dtype):
     """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound."""
     if dtype == "f64" and (s, m) == (13, 4):
+        if os.environ.get("HOP_LFT_VARIANT", "40") in ("40", "41"):
+            return "lft_cond_kernel<SchedLdlDma,13,4>", "mfma"
         return "lft_sweep_v2_kernel<SchedLdlDma,13,4>", "mfma"
     if (s, m) in SMALL_SHAPES[dtype]:
         return f"lft_small_kernel<{'float' if dtype == 'f32' else 'double'},{s},{m}>", "hbm"
@@ -51,6 +53,14 @@ def kernel_path(s, m, dtype):
 def lft_flops(N, s, m):
     """Algorithmic FLOPs of one sweep."""
     return N * (23 * s ** 3 + 2 * s * m * m + 2 * s * s * m) - 11 * s ** 3
+
+
+def cond_flops(N, s, m):
+    """FLOPs the conditioned-prefix kernel executes per sweep: two
+    SPD inverses (2 s^3), the update LDL^T with its (s+1)-wide forward substitution
+    and rank-1 streams (~10/3 s^3), the predict products (4 s^3 + B R^-1 B^T) and
+    the bordered query elimination (s^3 / 3)."""
+    return N * (29 * s ** 3 // 3 + 2 * s * m * m + 2 * s * s * m)
 
 
 def lft_bytes(N, s, m, w=8):
@@ -221,6 +231,12 @@ def main():
                          "traffic": traffic,
                          "kernel": kname, "kernel_ms": kern_ms,
                          "flops_per_sweep": lft_flops(N, s, m),
+                         **({"executed_flops_per_sweep": cond_flops(N, s, m),
+                             "executed_tflops": cond_flops(N, s, m) * (hi - lo)
+                             / (kern_ms * 1e-3) / 1e12,
+                             "executed_frac": cond_flops(N, s, m) * (hi - lo)
+                             / (kern_ms * 1e-3) / 1e12 / peak}
+                            if kname.startswith("lft_cond") else {}),
                          "alg_bytes_per_sweep": lft_bytes(N, s, m, 8 if dtype == torch.float64 else 4)},
             "cpu_baseline": cpu,
             "status_ok": status_ok,

@@ -137,14 +137,15 @@ def test_traj_sweep_batch_vs_oracle(dev, monkeypatch, n, m, N):
 
 
 def test_traj_fused_equals_unfused(dev, monkeypatch):
-    """The fused builder and hop_augment + the augmented-form sweep agree."""
+    """The fused builder and hop_augment + the augmented-form sweep agree (1e-10:
+    the s=13 augmented-form sweep runs the conditioned-prefix association)."""
     from time_opt_ilqr_amd import engine
     ps, st = _batch(range(970, 1003), 12, 4, 50)
     args = (*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
     a = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
     monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
     b = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
-    assert _rel(a, b) <= 1e-11
+    assert _rel(a, b) <= 1e-10
 
 
 def test_traj_extra_stage_cost(dev):

@@ -224,6 +224,103 @@ def test_query_ldl_block_emulated(n):
     assert regs[3 * n][0] > 0
 
 
+@pytest.mark.parametrize("n", [3, 13])
+def test_cond_ldl_block_emulated(n):
+    """CondLdl<n> (the conditioned-prefix update of SchedCond): from the offset-form
+    S - I and Psi = [Sigma | m] (m on lane n), stream Sigma' = Sigma - Sigma S^-1 Sigma,
+    m' = m - Sigma S^-1 m on lane n, and gamma' = gamma - m^T S^-1 m on lane n of
+    the extra row n."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(200 + n)
+    Sg = rng.standard_normal((n, n))
+    Sg = Sg @ Sg.T
+    Ek = rng.standard_normal((n, n))
+    Ek = Ek @ Ek.T / n + np.eye(n)
+    S = Sg + Ek
+    m = rng.standard_normal(n)
+    gam = -0.7
+    regs = {}
+    for i in range(n):
+        col = rng.standard_normal(16)
+        col[:n] = S[i]
+        col[i] -= 1.0
+        regs[i] = col
+        for base in (n, 2 * n):
+            col = np.zeros(16)
+            col[:n] = Sg[i]
+            col[n] = m[i]
+            regs[base + i] = col
+    regs[3 * n] = np.zeros(16)
+    regs[3 * n][n] = gam
+    regs[3 * n + 1] = np.ones(16)
+    for j in range(10):
+        regs[3 * n + 2 + j] = np.full(16, np.nan)
+    E.run(E.extract(inc, "CondLdl", n), regs)
+    X = np.array([regs[2 * n + i] for i in range(n)])
+    Si = np.linalg.inv(S)
+    want = Sg - Sg @ Si @ Sg
+    assert np.abs(X[:, :n] - want).max() <= 1e-12 * np.abs(want).max()
+    mw = m - Sg @ Si @ m
+    assert np.abs(X[:, n] - mw).max() <= 1e-12 * np.abs(mw).max()
+    gw = gam - m @ Si @ m
+    assert abs(regs[3 * n][n] - gw) <= 1e-12 * abs(gw)
+    assert regs[3 * n + 1][0] > 0
+
+
+def _cond_model(A, Bm, Q, Ri, z0, QT, N):
+    """NumPy model of lft_cond_kernel: the J curve by the
+    conditioned prefix (Sigma, m, gamma) with the reference's jitters placed as
+    Sigma + eps I (W and X0 jitters) and Sigma + X_t + eps I (Wt jitter)."""
+    s = A.shape[1]
+    eps = 1e-9 * np.eye(s)
+    Sig, m, gam = np.zeros((s, s)), np.asarray(z0, float).copy(), 0.0
+    J = np.zeros(N)
+    for k in range(N):
+        E, _ = orc.spd_inverse(Q[k])
+        Se = Sig + eps
+        Sinv = np.linalg.inv(Se + E)
+        Sig1 = Se - Se @ Sinv @ Se
+        m1 = m - Se @ Sinv @ m
+        gam -= m @ Sinv @ m
+        Sig = A[k] @ Sig1 @ A[k].T + Bm[k] @ Ri @ Bm[k].T
+        m = A[k] @ m1
+        X, _ = orc.spd_inverse(QT[k])
+        J[k] = 0.5 * (m @ np.linalg.solve(Sig + eps + X, m) - gam)
+    return J
+
+
+@pytest.mark.parametrize("tag", ["s13_m4_N100", "s5_m1_N200", "s3_m1_N50", "s16_m6_N40"])
+def test_conditioned_prefix_model_vs_golden(golden_dir, tag):
+    """The association the fast s=13 kernel uses (z0 folded into the prefix first,
+    the reference's jitters moved onto Sigma) reproduces the reference's J curves
+    (golden vectors made by importing the reference) to 1e-11."""
+    d = np.load(os.path.join(golden_dir, f"lft_synth_{tag}.npz"))
+    s, m, N, bs, cnt = (int(d[k]) for k in ("s", "m", "N", "base_seed", "count"))
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(bs, min(cnt, 2), s, m, N)
+    for b in range(min(cnt, 2)):
+        r = Ri if Ri.ndim == 2 else Ri[b]
+        J = _cond_model(A[b], Bm[b], Q[b], r, z0[b] if z0.ndim == 2 else z0, QT[b], N)
+        assert _rel_err(J, d["J"][b]) <= 1e-11
+
+
+@pytest.mark.parametrize("tag,tol", [("real_DI_N50", 1e-3), ("real_Quad_N160", 5e-2)])
+def test_conditioned_prefix_model_real_captures(golden_dir, tag, tol):
+    """Same model on the reference's own first/last select linearisations
+    (ill-conditioned terminal blocks): same T*, J within the real-capture bars."""
+    d = np.load(os.path.join(golden_dir, f"{tag}.npz"))
+    for p in ("pfirst", "plast"):
+        N = int(d[p + "_T_use"])
+        J = _cond_model(d[p + "_A"], d[p + "_B"], d[p + "_Q"], d[p + "_R_inv"], d[p + "_z0"],
+                        d[p + "_QT"], N)
+        Jr = d[p + "_J"]
+        assert _rel_err(J, Jr) <= tol
+        lo, hi = int(d["T_min"]), min(int(d["T_max"]), N)
+        assert int(np.argmin(J[lo - 1:hi])) == int(np.argmin(Jr[lo - 1:hi]))
+
+
 @pytest.fixture(scope="module")
 def small_host(tmp_path_factory):
     """g++ build of csrc/small_math.hpp (the small-s kernel's per-problem math)."""

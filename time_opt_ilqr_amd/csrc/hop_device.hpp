@@ -27,6 +27,8 @@ constexpr int kLdsTile = 272;     // 16*17; == 16 (mod 32) -> conflict-free b64 
 
 // status bits (include/hop.h)
 constexpr unsigned ST_JITTER = 1u, ST_LU = 2u, ST_NONFINITE = 4u, ST_FAIL = 8u;
+// internal: the conditioned-prefix kernel hands the problem to the rerun launch
+constexpr unsigned ST_RERUN = 16u;
 
 template <int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {

@@ -59,6 +59,7 @@ struct LftArgs {
   T* dbg_efg;        // [B][n][3][s][s] or null  (E_k, F_k, G_k)
   T* dbg_pre;        // [B][n][3][s][s] or null  (Ebar_k, Fbar_k, Gbar_k)
   int traj;          // 1: A/B/Q/QT unused, blocks built in-kernel from `tr`
+  int cond;          // SchedCond: bit 0 rerun launch (only ST_RERUN problems), bit 1 flag all
   TrajArgs<T> tr;
 };
 
