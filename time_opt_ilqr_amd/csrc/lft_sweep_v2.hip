@@ -122,6 +122,10 @@ struct SchedLdlDma : SchedLdl {
 struct SchedLdlDmaStamped : SchedLdlDma {
   static constexpr int STAMP = 1;
 };
+// conditioned-prefix kernel on the trajectory form (lft_cond_kernel)
+struct SchedCondTraj : SchedLdlDma {
+  static constexpr int TRAJ = 1;
+};
 template <class C>
 constexpr bool has_pipe() {
   if constexpr (requires { C::PIPE; }) return C::PIPE != 0;
@@ -1325,16 +1329,136 @@ __device__ __forceinline__ void sym_from_z(const double* img, unsigned zaddr, in
   for (int i = 0; i < S; ++i) r[i] = 0.5 * (r[i] + t[i]);
 }
 
+// Trajectory form of the conditioned-prefix kernel (SchedCondTraj): the
+// augmented Q / QT images are built in LDS from the raw linearisation exactly
+// as in lft_sweep_v2_kernel's TRAJ path (augmented.py:10-87): constant parts
+// once, per step only the last row / column and the diagonal, Q e_k carried.
+template <int S, int MM>
+struct CondTraj {
+  static constexpr int NN = S - 1;
+  double xg_c = 0.0, ur_c = 0.0, w2 = 0.0, qdiag = 0.0, pdiag = 0.0, pcc = 0.0;
+  double qe_k = 0.0, eqe_k = 0.0;
+  bool wrap_c = false;
+  double qr_n[NN], pr_n[NN];
+
+  __device__ __forceinline__ void load_rows(const double* cq, const double* imT, int c) {
+    const int cc = c < NN ? c : 0;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      qr_n[j] = cq[j * NN + cc];
+      pr_n[j] = imT[j * S + cc];
+    }
+  }
+
+  __device__ __forceinline__ void init(const LftArgs<double>& a, long long pb, int c, double* cq,
+                                       double* wq, double* wt) {
+    const TrajArgs<double>& t = a.tr;
+    const double* Qg = t.Q + pb * t.q_bs;
+    const double* Pg = t.P + pb * t.p_bs;
+    const int cc = c < NN ? c : 0;
+    if (c < NN) {  // raw Q (Q e, augmented.py:35), transposed
+#pragma unroll
+      for (int j = 0; j < NN; ++j) cq[j * NN + c] = Qg[c * NN + j];
+    }
+    pcc = Pg[cc * NN + cc];
+    xg_c = c < NN ? t.xg[pb * t.xg_bs + cc] : 0.0;
+    ur_c = c < MM ? t.u_ref[pb * t.ur_bs + (c < MM ? c : 0)] : 0.0;
+    w2 = 2.0 * t.w[pb * t.w_bs];
+    wrap_c = c < NN && ((t.wrap_mask >> c) & 1u);
+    qdiag = (0.5 * (Qg[cc * NN + cc] + Qg[cc * NN + cc]) + t.q_reg) + (1e-9 - 1.0);
+    pdiag = Pg[cc * NN + cc] + (1e-9 - 1.0);
+    {
+      const double* X0 = t.X + pb * (long long)(a.nalloc + 1) * NN;
+      double e0 = c < NN ? X0[cc] - xg_c : 0.0;
+      if (t.wrap_mask != 0u) {
+        const double w0 = wrap_angle(e0);
+        e0 = wrap_c ? w0 : e0;
+      }
+      double q4[4] = {0.0, 0.0, 0.0, 0.0};
+      double qr0[NN];
+#pragma unroll
+      for (int j = 0; j < NN; ++j) qr0[j] = c < NN ? Qg[cc * NN + j] : 0.0;
+      LaneDot4<NN>::fma(q4, e0, qr0);
+      qe_k = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+      eqe_k = row_sum_dpp(c < NN ? e0 * qe_k : 0.0);
+    }
+    if (c < NN) {  // column c: _sym(Q) + q_reg I, and P (augmented.py:33, 82)
+#pragma unroll
+      for (int i = 0; i < NN; ++i) {
+        wq[i * S + c] = 0.5 * (Qg[i * NN + c] + Qg[c * NN + i]) + (i == c ? t.q_reg : 0.0);
+        wt[i * S + c] = Pg[i * NN + c];
+      }
+    }
+  }
+
+  // last row / column and diagonal of Q_aug[k], QT_aug[k]; returns a~_k[c]
+  __device__ __forceinline__ double step(const LftArgs<double>& a, int c, const double* sX,
+                                         const double* sV, const double* sU, const double* sR,
+                                         double* wq, double* wt) {
+    const int cc = c < NN ? c : 0, cm = c < MM ? c : 0;
+    double x1 = sX[cc], av = sV[cc], uu = sU[cm];
+    double rb[MM], qr[NN], pr[NN];
+#pragma unroll
+    for (int q = 0; q < MM; ++q) rb[q] = sR[cc * MM + q];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      qr[j] = qr_n[j];
+      pr[j] = pr_n[j];
+    }
+    const bool in = c < NN;
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+      qr[j] = in ? qr[j] : 0.0;
+      pr[j] = in ? (j == c ? pcc : pr[j]) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < MM; ++q) rb[q] = in ? rb[q] : 0.0;
+    double e1 = in ? x1 - xg_c : 0.0;
+    if (a.tr.wrap_mask != 0u) {
+      const double we1 = wrap_angle(e1);
+      e1 = wrap_c ? we1 : e1;
+    }
+    const double du = c < MM ? uu - ur_c : 0.0;
+    av = in ? av : 0.0;
+    double q4[4] = {0.0, 0.0, 0.0, 0.0}, p4[4] = {0.0, 0.0, 0.0, 0.0}, bd = 0.0;
+    LaneDot4<NN>::fma(q4, e1, qr);
+    LaneDot4<NN>::fma(p4, e1, pr);
+    LaneDot<MM>::fma(bd, du, rb);
+    const double qe1 = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+    const double pe = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+    const double atil = av - bd;
+    const double eqe1 = row_sum_dpp(in ? e1 * qe1 : 0.0);
+    const double epe = row_sum_dpp(in ? e1 * pe : 0.0);
+    if (c < NN) {
+      wq[c * S + NN] = qe_k;
+      wq[NN * S + c] = qe_k;
+      wq[c * S + c] = qdiag;
+      wt[c * S + NN] = pe;
+      wt[NN * S + c] = pe;
+      wt[c * S + c] = pdiag;
+    } else if (c == NN) {
+      wq[NN * S + NN] = ((eqe_k + w2) + a.tr.rho_reg) + (1e-9 - 1.0);
+      wt[NN * S + NN] = (epe + a.tr.rho_reg) + (1e-9 - 1.0);
+    }
+    qe_k = qe1;
+    eqe_k = eqe1;
+    return atil;
+  }
+};
+
 template <class C, int S, int MM>
 __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
   using G = Geo<S, MM>;
+  constexpr bool TRAJ = has_traj<C>();
+  constexpr int NN = G::NN;
   static_assert(S < kRowLanes, "m rides on lane S");
   static_assert(G::TILE_W >= 8 * S * S + 64, "zero area in the tile slot");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  unsigned char* wbase = smem_raw + w * G::WAVE_BYTES;
+  constexpr int WB = TRAJ ? G::WAVE_BYTES_T : G::WAVE_BYTES;
+  unsigned char* wbase = smem_raw + w * WB;
   const unsigned wlds = (unsigned)(uintptr_t)wbase;
   double* zarea = reinterpret_cast<double*>(wbase + G::OFF_T);
   const unsigned zaddr = wlds + G::OFF_T;
@@ -1359,48 +1483,77 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     return __builtin_amdgcn_make_buffer_rsrc(
         const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);
   };
-  const __amdgpu_buffer_rsrc_t rQ = mk(a.Q, pstrM), rA = mk(a.A, pstrM), rT = mk(a.QT, pstrM),
-                               rB = mk(a.B, pstrB);
+  const long long pstA = (long long)a.nalloc * NN * NN * 8, pstR = (long long)a.nalloc * NN * MM * 8;
+  const long long pstX = (long long)(a.nalloc + 1) * NN * 8, pstV = (long long)a.nalloc * NN * 8;
+  const long long pstU = (long long)a.nalloc * MM * 8;
+  const __amdgpu_buffer_rsrc_t rQ = TRAJ ? mk(a.tr.A, pstA) : mk(a.Q, pstrM),
+                               rA = TRAJ ? mk(a.tr.Bm, pstR) : mk(a.A, pstrM),
+                               rT = TRAJ ? mk(a.tr.X, pstX) : mk(a.QT, pstrM),
+                               rB = TRAJ ? mk(a.tr.ares, pstV) : mk(a.B, pstrB),
+                               rU = TRAJ ? mk(a.tr.U, pstU) : rB;
   unsigned voM[G::NJM], voB[G::NJB];
+  unsigned voTA[G::NJA], voTR[G::NJR], voTX[G::NJX], voTV[G::NJV], voTU[G::NJU];
+  if constexpr (TRAJ) {
+    static_assert(G::NJA == 5 && G::NJR == 2 && G::NJX == 1 && G::NJV == 1 && G::NJU == 1,
+                  "trajectory pieces of the s = 13, m = 4 shape");
 #pragma unroll
-  for (int j = 0; j < G::NJM; ++j)
-    voM[j] = chunk_voff<G::CHM>(j, lane, wave_prob0, pb0, a.batch, pstrM);
+    for (int j = 0; j < G::NJA; ++j)
+      voTA[j] = chunk_voff<G::CHA>(j, lane, wave_prob0, pb0, a.batch, pstA);
 #pragma unroll
-  for (int j = 0; j < G::NJB; ++j)
-    voB[j] = chunk_voff<G::CHB>(j, lane, wave_prob0, pb0, a.batch, pstrB);
+    for (int j = 0; j < G::NJR; ++j)
+      voTR[j] = chunk_voff<G::CHR>(j, lane, wave_prob0, pb0, a.batch, pstR);
+    voTX[0] = chunk_voff<G::CHX>(0, lane, wave_prob0, pb0, a.batch, pstX);
+    voTV[0] = chunk_voff<G::CHV>(0, lane, wave_prob0, pb0, a.batch, pstV);
+    voTU[0] = chunk_voff<G::CHU>(0, lane, wave_prob0, pb0, a.batch, pstU);
+  } else {
+#pragma unroll
+    for (int j = 0; j < G::NJM; ++j)
+      voM[j] = chunk_voff<G::CHM>(j, lane, wave_prob0, pb0, a.batch, pstrM);
+#pragma unroll
+    for (int j = 0; j < G::NJB; ++j)
+      voB[j] = chunk_voff<G::CHB>(j, lane, wave_prob0, pb0, a.batch, pstrB);
+  }
   auto dma_step = [&](int k) {
-    const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
-    if constexpr (G::NJM == 6 && G::NJB == 2) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (TRAJ) {  // A_k, B_k, x_{k+1}, a_k, u_k
+      const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
+                     soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
+      dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
+          voTA, voTR, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR,
+          soV + NN * 8, soV, soU);
+    } else {
+      static_assert(TRAJ || (G::NJM == 6 && G::NJB == 2), "augmented pieces of s = 13, m = 4");
+      const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
       dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
                                                          soB);
-    } else {
-#pragma unroll
-      for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rQ, wlds + G::OFF_Q + 1024 * j, soM);
-#pragma unroll
-      for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rA, wlds + G::OFF_A + 1024 * j, soM);
-#pragma unroll
-      for (int j = 0; j < G::NJB; ++j) dma16(voB[j], rB, wlds + G::OFF_B + 1024 * j, soB);
-#pragma unroll
-      for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rT, wlds + G::OFF_QT + 1024 * j, soM);
     }
   };
 
   const long long pb = valid ? prob : a.batch - 1;
-  const double* zp = a.z0 + pb * a.z_bstride;
   double rinv[MM];
   {
     const double* Rp = a.R + pb * a.r_bstride;
 #pragma unroll
     for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
   }
-  // X = [Sigma_0 + eps I | z0], gamma_0 = 0 (Sigma_0 = 0: z0 known exactly)
+  double* cq = reinterpret_cast<double*>(wbase + G::OFF_CQ) + g * NN * NN;
+  CondTraj<S, MM> tb;
+  if constexpr (TRAJ) {
+    tb.init(a, pb, c, cq, const_cast<double*>(imQ), const_cast<double*>(imT));
+    wave_sync();
+    tb.load_rows(cq, imT, c);
+  }
+  // X = [Sigma_0 + eps I | z0], gamma_0 = 0 (Sigma_0 = 0: z0 known exactly);
+  // the trajectory form's z0 is e_s (augmented.py:57)
+  const double* zp = a.z0 + pb * a.z_bstride;
   double X[S + 1];
-  static_for<S>([&](auto I) { X[I] = (c == S) ? zp[I] : sel_lane<I>(0.0, 1e-9); });
+  static_for<S>([&](auto I) {
+    const double z = TRAJ ? (I == NN ? 1.0 : 0.0) : zp[I];
+    X[I] = (c == S) ? z : sel_lane<I>(0.0, 1e-9);
+  });
   X[S] = 0.0;
   const double e_s = (c == S) ? 1.0 : 0.0;  // row S of A~^T: carries m through the first product
-  const bool force = (a.cond & 2) != 0;
-  bool bad = force;
+  bool bad = (a.cond & 2) != 0;
 
   dma_step(0);
   double best = 0.0, jprev = 0.0;
@@ -1411,8 +1564,17 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     dma_wait();
     wave_sync();
     if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
-    diag_add<S, S>(imQ, c, 1e-9 - 1.0);
-    diag_add<S, S>(imT, c, 1e-9 - 1.0);
+    double atil = 0.0;
+    if constexpr (TRAJ) {
+      const double* sX = reinterpret_cast<const double*>(wbase + G::OFF_VX) + g * 2 * G::CHX;
+      const double* sV = reinterpret_cast<const double*>(wbase + G::OFF_VA) + g * 2 * G::CHV;
+      const double* sU = reinterpret_cast<const double*>(wbase + G::OFF_VU) + g * 2 * G::CHU;
+      const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
+      atil = tb.step(a, c, sX, sV, sU, sR, const_cast<double*>(imQ), const_cast<double*>(imT));
+    } else {
+      diag_add<S, S>(imQ, c, 1e-9 - 1.0);
+      diag_add<S, S>(imT, c, 1e-9 - 1.0);
+    }
     // ---- NE = -(Q_k + eps I)^-1 + I, NX = -(QT_k + eps I)^-1 + I (first attempt only)
     double NE[S], NX[S];
     sym_from_z<S>(imQ, zaddr, c, NE);
@@ -1423,8 +1585,17 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       SweepQ<S>::run(NX, d2);
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
     }
-    double at[S + 1], brow[MM];  // at[j] = column j of A_k (lanes > S-1: 0), at[S] = e_S
-    {
+    double at[S + 1], brow[MM];  // at[j] = column j of A~ (lanes > S-1: 0), at[S] = e_S
+    if constexpr (TRAJ) {  // row c of A_aug = [[A_k, a~],[0, 1]], B_aug = [[B_k],[0]]
+      const double* sA = reinterpret_cast<const double*>(wbase + G::OFF_A) + g * 2 * G::CHA;
+      const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
+      const int cc = c < NN ? c : 0;
+#pragma unroll
+      for (int j = 0; j < NN; ++j) at[j] = c < NN ? sA[cc * NN + j] : 0.0;
+      at[NN] = c < NN ? atil : (c == NN ? 1.0 : 0.0);
+#pragma unroll
+      for (int j = 0; j < MM; ++j) brow[j] = c < NN ? sR[cc * MM + j] : 0.0;
+    } else {
       const bool in = c < S;
       const double* pa = in ? imA + S * c : zarea;  // branch-free: lanes > S-1 read zeros
       const double* pbm = in ? imB + MM * c : zarea;
@@ -1432,8 +1603,8 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       for (int j = 0; j < S; ++j) at[j] = pa[j];
 #pragma unroll
       for (int j = 0; j < MM; ++j) brow[j] = pbm[j];
-      at[S] = e_s;
     }
+    at[S] = e_s;
     wave_sync();
     if (k + 1 < N) dma_step(k + 1);
     // ---- update: condition the prefix on stage k's cost
@@ -1476,6 +1647,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       bad = bad || !(dmin > 0.0) || (q != q);
       jk = 0.5 * (q - gam);
     }
+    if constexpr (TRAJ) tb.load_rows(cq, imT, c);
     bad = bad || !finite_val(jk);
     if (fuse_argmin) {
       const int t = k + 1;
@@ -1513,6 +1685,20 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
     const size_t bytes = (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock);
     const char* ev = getenv("HOP_LFT_VARIANT");
+    const int tv = ev ? atoi(ev) : 40;
+    if (tv == 40 || tv == 41) {  // conditioned prefix + rerun of the flagged problems
+      LftArgs<double> c = a;
+      const char* fv = getenv("HOP_COND_FORCE");
+      c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
+      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondTraj, 13, 4>), dim3((unsigned)blocks),
+                         dim3(256), bytes, stream, c);
+      if (tv == 41) return hipGetLastError();
+      LftArgs<double> r = a;
+      r.cond = 1;
+      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>),
+                         dim3((unsigned)blocks), dim3(256), bytes, stream, r);
+      return hipGetLastError();
+    }
     if (ev && atoi(ev) == 24)  // section stamps (tools/stamps.py --traj)
       hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTrajStamped, 13, 4>),
                          dim3((unsigned)blocks), dim3(256), bytes, stream, a);
