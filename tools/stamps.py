@@ -23,6 +23,10 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=100)
     ap.add_argument("--variant", type=int, default=32)
+    ap.add_argument("--cond2", action="store_true",
+                    help="two-waves-per-SIMD conditioned-prefix kernel (variant 46)")
+    ap.add_argument("--cond", action="store_true",
+                    help="conditioned-prefix kernel (variant 42)")
     ap.add_argument("--traj", action="store_true",
                     help="trajectory-form sweep (in-kernel builders, variant 24)")
     args = ap.parse_args()
@@ -47,6 +51,18 @@ def main():
                  0.1 * torch.randn((m,), **kw), M @ M.T / n + 0.5 * eye,
                  torch.eye(m, device=dev, dtype=torch.float64), 5.0 * eye, 0.5)
         run = lambda: engine.propagate_traj(*targs)  # noqa: E731
+    if args.cond:
+        args.variant = 42
+        NAMES[:8] = ["top wait (DMA of step k)", "J store + diag offsets", "Q/QT image reads (sym)",
+                     "E/Xt sweeps", "A/B reads + DMA issue", "update (CondLdl)", "predict products",
+                     "query (ElimQ)"]
+    if args.cond2:
+        args.variant = 46
+        args.cond = True
+        NAMES[:10] = ["S: hand-off read + barrier A", "S: DMA wait, A/B reads, DMA issue",
+                      "S: update (CondLdl)", "S: predict", "S: hand-off write + barrier B",
+                      "T: hand-off read + barrier A", "T: DMA wait, image reads, DMA issue",
+                      "T: query", "T: sweeps", "T: hand-off write + barrier B"]
     os.environ["HOP_LFT_VARIANT"] = str(args.variant)
     buf = (C.c_ulonglong * 16)()
     run()
@@ -58,7 +74,7 @@ def main():
     waves = buf[15]
     tot = 0.0
     for j in range(15):
-        if j == 7 or (j >= 9 and buf[j] == 0):
+        if (j == 7 and not args.cond) or (j >= 8 and buf[j] == 0):
             continue
         cyc = buf[j] / waves / args.N
         tot += cyc
