@@ -1706,390 +1706,6 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
 }
 
 
-// ===========================================================================
-// SchedCond2: the conditioned-prefix step split over TWO waves per SIMD.
-//
-// B = 4096 gives one wave per SIMD, and one wave issues an fp64 VALU
-// instruction only every ~5.1-5.6 cycles; two waves on the SIMD reach ~4.4
-// (tools/ubench_2wave.hip).  Each group of four problems is therefore served
-// by a PAIR of waves on the same SIMD (512-thread workgroups: waves w and
-// w + 4), splitting the step by data dependence:
-//   S-wave (state):    update_k (CondLdl) and predict_k  -> Sigma_{k+1}
-//   T-wave (terminal): E_{k+1} and X_k sweeps, the query of horizon k with
-//                      Sigma_k and X_{k-1}, the J stores and the argmin.
-// Hand-offs through LDS (one register = 64 lanes x 8 B, conflict-free):
-// NE_{k+1} (T -> S) and [Sigma_{k+1} | m], gamma (S -> T).  Each iteration
-// is [phase 1: hand-off reads] barrier [phase 2: compute, hand-off writes]
-// barrier, so single buffers suffice.  Each wave streams its own blocks by
-// LDS-DMA: S the A_k / B_k images, T the Q_{k+1} / QT_k images.
-// ===========================================================================
-template <int OA, int OB>
-__device__ __forceinline__ void dma_ab8(const unsigned (&vm)[6], const unsigned (&vb)[2],
-                                        __amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
-                                        unsigned wlds, unsigned soM, unsigned soB) {
-  unsigned keep;
-#define HOP_P(R, V, OFF, SO)                                                  \
-  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
-  "], %[" #SO "] offen lds\n\t"
-  asm volatile(
-      "s_mov_b32 %[keep], m0\n\t"
-      HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
-      HOP_P(ra, v3, %[a3], sm) HOP_P(ra, v4, %[a4], sm) HOP_P(ra, v5, %[a5], sm)
-      HOP_P(rb, u0, %[b0], sb) HOP_P(rb, u1, %[b1], sb)
-      "s_mov_b32 m0, %[keep]"
-      : [keep] "=&s"(keep)
-      : [w] "s"(wlds), [sm] "s"(soM), [sb] "s"(soB), [ra] "s"(rA), [rb] "s"(rB),
-        [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]), [v4] "v"(vm[4]),
-        [v5] "v"(vm[5]), [u0] "v"(vb[0]), [u1] "v"(vb[1]), [a0] "i"(OA), [a1] "i"(OA + 1024),
-        [a2] "i"(OA + 2048), [a3] "i"(OA + 3072), [a4] "i"(OA + 4096), [a5] "i"(OA + 5120),
-        [b0] "i"(OB), [b1] "i"(OB + 1024)
-      : "memory", "scc");
-#undef HOP_P
-}
-
-// Q pieces of step kq and QT pieces of step kt (T-wave; Q runs one step ahead)
-template <int OQ, int OT, bool WITH_T>
-__device__ __forceinline__ void dma_qt12(const unsigned (&vm)[6], __amdgpu_buffer_rsrc_t rQ,
-                                         __amdgpu_buffer_rsrc_t rT, unsigned wlds, unsigned soQ,
-                                         unsigned soT) {
-  unsigned keep;
-#define HOP_P(R, V, OFF, SO)                                                  \
-  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
-  "], %[" #SO "] offen lds\n\t"
-  if constexpr (WITH_T)
-    asm volatile(
-        "s_mov_b32 %[keep], m0\n\t"
-        HOP_P(rq, v0, %[q0], sq) HOP_P(rq, v1, %[q1], sq) HOP_P(rq, v2, %[q2], sq)
-        HOP_P(rq, v3, %[q3], sq) HOP_P(rq, v4, %[q4], sq) HOP_P(rq, v5, %[q5], sq)
-        HOP_P(rt, v0, %[t0], st) HOP_P(rt, v1, %[t1], st) HOP_P(rt, v2, %[t2], st)
-        HOP_P(rt, v3, %[t3], st) HOP_P(rt, v4, %[t4], st) HOP_P(rt, v5, %[t5], st)
-        "s_mov_b32 m0, %[keep]"
-        : [keep] "=&s"(keep)
-        : [w] "s"(wlds), [sq] "s"(soQ), [st] "s"(soT), [rq] "s"(rQ), [rt] "s"(rT),
-          [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]), [v4] "v"(vm[4]),
-          [v5] "v"(vm[5]), [q0] "i"(OQ), [q1] "i"(OQ + 1024), [q2] "i"(OQ + 2048),
-          [q3] "i"(OQ + 3072), [q4] "i"(OQ + 4096), [q5] "i"(OQ + 5120), [t0] "i"(OT),
-          [t1] "i"(OT + 1024), [t2] "i"(OT + 2048), [t3] "i"(OT + 3072), [t4] "i"(OT + 4096),
-          [t5] "i"(OT + 5120)
-        : "memory", "scc");
-  else
-    asm volatile(
-        "s_mov_b32 %[keep], m0\n\t"
-        HOP_P(rq, v0, %[q0], sq) HOP_P(rq, v1, %[q1], sq) HOP_P(rq, v2, %[q2], sq)
-        HOP_P(rq, v3, %[q3], sq) HOP_P(rq, v4, %[q4], sq) HOP_P(rq, v5, %[q5], sq)
-        "s_mov_b32 m0, %[keep]"
-        : [keep] "=&s"(keep)
-        : [w] "s"(wlds), [sq] "s"(soQ), [rq] "s"(rQ), [v0] "v"(vm[0]), [v1] "v"(vm[1]),
-          [v2] "v"(vm[2]), [v3] "v"(vm[3]), [v4] "v"(vm[4]), [v5] "v"(vm[5]), [q0] "i"(OQ),
-          [q1] "i"(OQ + 1024), [q2] "i"(OQ + 2048), [q3] "i"(OQ + 3072), [q4] "i"(OQ + 4096),
-          [q5] "i"(OQ + 5120)
-        : "memory", "scc");
-#undef HOP_P
-}
-
-// hand-off buffer: register i of every lane at base + 512 i + 8 lane
-template <int R>
-__device__ __forceinline__ void hand_put(double* buf, int lane, const double (&x)[R]) {
-#pragma unroll
-  for (int i = 0; i < R; ++i) buf[i * 64 + lane] = x[i];
-}
-template <int R>
-__device__ __forceinline__ void hand_get(const double* buf, int lane, double (&x)[R]) {
-#pragma unroll
-  for (int i = 0; i < R; ++i) x[i] = buf[i * 64 + lane];
-}
-
-__device__ __forceinline__ void wg_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-template <int S, int MM>
-struct Geo2 {
-  using G = Geo<S, MM>;
-  static constexpr int OFF_Q = 0, OFF_A = G::IMGM_W, OFF_QT = 2 * G::IMGM_W,
-                       OFF_B = 3 * G::IMGM_W;
-  static constexpr int OFF_Z = OFF_B + G::IMGB_W;
-  static constexpr int ZB = ((S * S + 8) * 8 + 255) / 256 * 256;
-  static constexpr int OFF_NE = OFF_Z + ZB;
-  static constexpr int OFF_SG = OFF_NE + S * 512;
-  static constexpr int OFF_FL = OFF_SG + (S + 1) * 512;  // S-wave flags (64 ints)
-  static constexpr int PAIR_BYTES = OFF_FL + 256;
-};
-
-template <class C, int S, int MM>
-__global__ __launch_bounds__(512, 1) void lft_cond2_kernel(LftArgs<double> a) {
-  using G = Geo<S, MM>;
-  using P = Geo2<S, MM>;
-  static_assert(S < kRowLanes, "m rides on lane S");
-  static_assert(G::NJM == 6 && G::NJB == 2, "pieces of the s = 13, m = 4 shape");
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, c = lane & 15, g = lane >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pair = w & 3;
-  const bool tw = w >= 4;  // T-wave (wave-uniform role)
-  unsigned char* pbase = smem_raw + pair * P::PAIR_BYTES;
-  const unsigned plds = (unsigned)(uintptr_t)pbase;
-  double* zarea = reinterpret_cast<double*>(pbase + P::OFF_Z);
-  const unsigned zaddr = plds + P::OFF_Z;
-  double* nebuf = reinterpret_cast<double*>(pbase + P::OFF_NE);
-  double* sgbuf = reinterpret_cast<double*>(pbase + P::OFF_SG);
-  int* flbuf = reinterpret_cast<int*>(pbase + P::OFF_FL);
-  if (tw) {
-#pragma unroll 1
-    for (int i = lane; i < S * S + 8; i += 64) zarea[i] = 0.0;
-  }
-  const double* imQ = reinterpret_cast<const double*>(pbase + P::OFF_Q + g * G::IMGM);
-  const double* imA = reinterpret_cast<const double*>(pbase + P::OFF_A + g * G::IMGM);
-  const double* imT = reinterpret_cast<const double*>(pbase + P::OFF_QT + g * G::IMGM);
-  const double* imB = reinterpret_cast<const double*>(pbase + P::OFF_B + g * G::IMGB);
-
-  const long long wave_prob0 = ((long long)blockIdx.x * 4 + pair) * kProbPerWave;
-  const long long prob = wave_prob0 + g;
-  const bool valid = prob < a.batch;
-  const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
-  const int N = a.n;
-  constexpr int SS = S * S, SM = S * MM;
-  const long long pstrM = (long long)a.nalloc * SS * 8;
-  const long long pstrB = (long long)a.nalloc * SM * 8;
-  auto mk = [&](const double* base, long long pstr) {
-    const long long left = (a.batch - pb0) * pstr;
-    const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
-    return __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);
-  };
-  unsigned voM[G::NJM], voB[G::NJB];
-#pragma unroll
-  for (int j = 0; j < G::NJM; ++j)
-    voM[j] = chunk_voff<G::CHM>(j, lane, wave_prob0, pb0, a.batch, pstrM);
-#pragma unroll
-  for (int j = 0; j < G::NJB; ++j)
-    voB[j] = chunk_voff<G::CHB>(j, lane, wave_prob0, pb0, a.batch, pstrB);
-  const long long pb = valid ? prob : a.batch - 1;
-  const bool force = (a.cond & 2) != 0;
-  unsigned long long sec[5] = {};
-  unsigned long long tprev = 0;
-  auto stamp = [&](int j) {
-    if constexpr (C::STAMP) {
-      __builtin_amdgcn_sched_barrier(0);
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      __builtin_amdgcn_sched_barrier(0);
-      if (j >= 0) sec[j] += t - tprev;
-      tprev = t;
-    }
-  };
-  auto stamp_flush = [&](int base) {
-    if constexpr (C::STAMP) {
-      if (lane == 0) {
-        for (int j = 0; j < 5; ++j) atomicAdd(&g_hop_stamp[base + j], sec[j]);
-        if (base == 0) atomicAdd(&g_hop_stamp[15], 1ull);
-      }
-    }
-  };
-
-  if (!tw) {
-    // ======================= S-wave: update + predict =======================
-    const __amdgpu_buffer_rsrc_t rA = mk(a.A, pstrM), rB = mk(a.B, pstrB);
-    auto dma = [&](int k) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      dma_ab8<P::OFF_A, P::OFF_B>(voM, voB, rA, rB, plds, (unsigned)(k * SS * 8),
-                                  (unsigned)(k * SM * 8));
-    };
-    double rinv[MM];
-    {
-      const double* Rp = a.R + pb * a.r_bstride;
-#pragma unroll
-      for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
-    }
-    const double* zp = a.z0 + pb * a.z_bstride;
-    double X[S + 1];
-    static_for<S>([&](auto I) { X[I] = (c == S) ? zp[I] : sel_lane<I>(0.0, 1e-9); });
-    X[S] = 0.0;
-    const double e_s = (c == S) ? 1.0 : 0.0;
-    bool bad = force;
-    dma(0);
-    wg_barrier();  // P: NE_0 in nebuf
-#pragma unroll 1
-    for (int k = 0; k < N; ++k) {
-      stamp(-1);
-      // phase 1: NE_k; phase 2: A_k / B_k rows, DMA of step k+1, update_k, predict_k
-      double NE[S];
-      hand_get<S>(nebuf, lane, NE);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wg_barrier();  // A_k: hand-off reads done
-      stamp(0);
-      dma_wait();
-      wave_sync();
-      double at[S + 1], brow[MM];
-      {
-        const bool in = c < S;
-        const double* pa = in ? imA + S * c : zarea;
-        const double* pbm = in ? imB + MM * c : zarea;
-#pragma unroll
-        for (int j = 0; j < S; ++j) at[j] = pa[j];
-#pragma unroll
-        for (int j = 0; j < MM; ++j) brow[j] = pbm[j];
-        at[S] = e_s;
-      }
-      wave_sync();
-      if (k + 1 < N) dma(k + 1);
-      stamp(1);
-      {
-        double r[S], Ht[S];
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-          r[i] = X[i] - NE[i];
-          Ht[i] = X[i];
-        }
-        double dmin = 1.0;
-        CondLdl<S>::run(r, Ht, X, dmin);
-        const double x = bcast<S - 1>(r[S - 1]);
-        bad = bad || !(dmin > 0.0) || (x != x);
-      }
-      stamp(2);
-      {
-        double T[S];
-        zero(T);
-        double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
-        gxy<C, false, S, S + 1>(T, Xs, at);
-        static_for<S>([&](auto I) { X[I] = sel_lane<I>(0.0, 1e-9); });
-        double (&at13)[S] = reinterpret_cast<double (&)[S]>(at);
-        gxty<C, false>(Xs, at13, T);
-        double y[MM];
-        zero(y);
-        acc_xy<false, double, MM, MM>(y, rinv, brow);
-        acc_xty<false, double, S, MM>(Xs, brow, y);
-      }
-      stamp(3);
-      hand_put<S + 1>(sgbuf, lane, X);
-      wg_barrier();  // B_k: Sigma_{k+1}, NE_{k+1} written
-      stamp(4);
-    }
-    stamp_flush(0);
-    dma_wait();
-    if (c == 0) flbuf[g] = bad ? 1 : 0;
-    wg_barrier();  // E: flags, Sigma_N
-  } else {
-    // ================= T-wave: sweeps, queries, J, argmin ==================
-    const __amdgpu_buffer_rsrc_t rQ = mk(a.Q, pstrM), rT = mk(a.QT, pstrM);
-    bool bad = false;
-    double best = 0.0;
-    int tbest = 0;
-    const bool fuse_argmin = a.t_max > 0;
-    auto take = [&](int t, double jk) {
-      bad = bad || !finite_val(jk);
-      if (valid && c == 0) a.J[prob * N + t - 1] = jk;
-      if (fuse_argmin) {
-        if (t == a.t_min) {
-          best = jk;
-          tbest = t;
-        } else if (t > a.t_min && t <= a.t_max) {
-          const bool bnan = best != best, jnan = jk != jk;
-          if (!bnan && (jnan || jk < best)) {
-            best = jk;
-            tbest = t;
-          }
-        }
-      }
-    };
-    // query of horizon t: [Sigma_t + eps I + X_{t-1} - I | m_t], gamma_t (Sg from sgbuf)
-    auto query = [&](double (&Sg)[S + 1], const double (&NXq)[S]) {
-      double rq[S];
-#pragma unroll
-      for (int i = 0; i < S; ++i) rq[i] = Sg[i] - NXq[i];
-      double acc = 0.0, dmin = 1.0;
-      ElimQ<S>::run(rq, acc, dmin, 1.0);
-      const double q = bcast<S>(acc);
-      const double gam = bcast<S>(Sg[S]);
-      bad = bad || !(dmin > 0.0) || (q != q);
-      return 0.5 * (q - gam);
-    };
-    // the T-wave carries the longer dependent chain (image reads -> sweeps, query):
-    // let it win the SIMD's issue arbitration (HOP_COND2_PRIO=0 turns this off)
-    if (a.cond & 4) __builtin_amdgcn_s_setprio(1);
-    // prologue: NE_0 from Q_0
-    wave_sync();  // zero area written by this wave
-    dma_qt12<P::OFF_Q, P::OFF_QT, false>(voM, rQ, rT, plds, 0u, 0u);
-    dma_wait();
-    wave_sync();
-    double NX[S];
-    {
-      diag_add<S, S>(imQ, c, 1e-9 - 1.0);
-      double NE[S];
-      sym_from_z<S>(imQ, zaddr, c, NE);
-      double d1 = 1.0;
-      SweepQ<S>::run(NE, d1);
-      bad = bad || !pivots_ok(NE, d1);
-      hand_put<S>(nebuf, lane, NE);
-    }
-    wave_sync();
-    // step 0: Q_1 (if any) and QT_0
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    dma_qt12<P::OFF_Q, P::OFF_QT, true>(voM, rQ, rT, plds, (unsigned)(N > 1 ? SS * 8 : 0), 0u);
-    wg_barrier();  // P
-#pragma unroll 1
-    for (int k = 0; k < N; ++k) {
-      stamp(-1);
-      // phase 1: Sigma_k (k >= 1); phase 2: images Q_{k+1} / QT_k, query, sweeps
-      double Sg[S + 1];
-      if (k > 0) hand_get<S + 1>(sgbuf, lane, Sg);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wg_barrier();  // A_k
-      stamp(0);
-      dma_wait();
-      wave_sync();
-      diag_add<S, S>(imQ, c, 1e-9 - 1.0);
-      diag_add<S, S>(imT, c, 1e-9 - 1.0);
-      double NE[S], NXn[S];
-      sym_from_z<S>(imQ, zaddr, c, NE);
-      sym_from_z<S>(imT, zaddr, c, NXn);
-      wave_sync();
-      if (k + 1 < N) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        dma_qt12<P::OFF_Q, P::OFF_QT, true>(voM, rQ, rT, plds,
-                                            (unsigned)((k + 2 < N ? k + 2 : k + 1) * SS * 8),
-                                            (unsigned)((k + 1) * SS * 8));
-      }
-      stamp(1);
-      // query of horizon k (Sigma_k, X_{k-1}), sweeps NE_{k+1}, NX_k
-      if (k > 0) take(k, query(Sg, NX));
-      stamp(2);
-      {
-        double d1 = 1.0, d2 = 1.0;
-        if (k + 1 < N) {
-          SweepQ<S>::run(NE, d1);
-          bad = bad || !pivots_ok(NE, d1);
-        }
-        SweepQ<S>::run(NXn, d2);
-        bad = bad || !pivots_ok(NXn, d2);
-      }
-      copy(NX, NXn);
-      stamp(3);
-      if (k + 1 < N) hand_put<S>(nebuf, lane, NE);
-      wg_barrier();  // B_k
-      stamp(4);
-    }
-    stamp_flush(5);
-    dma_wait();
-    wg_barrier();  // E: Sigma_N and the S-wave's flags
-    if (N > 0) {
-      double Sg[S + 1];
-      hand_get<S + 1>(sgbuf, lane, Sg);
-      take(N, query(Sg, NX));
-    }
-    const bool sbad = flbuf[g] != 0;
-    if (valid && c == 0) {
-      a.status[prob] = (bad || sbad || force) ? (int)ST_RERUN : 0;
-      if (fuse_argmin && a.t_star != nullptr) {
-        a.t_star[prob] = tbest;
-        a.j_star[prob] = best;
-      }
-    }
-  }
-}
-
 }  // namespace v2
 
 // exact-size fast path: returns hipErrorNotSupported when the shape has none
@@ -2131,33 +1747,6 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   const int variant = ev ? atoi(ev) : 40;
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
-    if (variant == 46) {  // two waves per SIMD + stamps (tools/stamps.py --cond2), no rerun
-      LftArgs<double> c = a;
-      const char* pv = getenv("HOP_COND2_PRIO");
-      c.cond = (pv && atoi(pv) == 0) ? 0 : 4;
-      hipLaunchKernelGGL((v2::lft_cond2_kernel<v2::SchedCondStamped, 13, 4>),
-                         dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
-                         dim3(512), (size_t)(v2::Geo2<13, 4>::PAIR_BYTES * 4), stream, c);
-      return hipGetLastError();
-    }
-    if (variant == 44 || variant == 45) {  // two waves per SIMD (+ rerun unless 45)
-      LftArgs<double> c = a;
-      const char* fv = getenv("HOP_COND_FORCE");
-      c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
-      const char* pv = getenv("HOP_COND2_PRIO");
-      if (!(pv && atoi(pv) == 0)) c.cond |= 4;
-      constexpr int b2 = v2::Geo2<13, 4>::PAIR_BYTES * 4;
-      hipLaunchKernelGGL((v2::lft_cond2_kernel<v2::SchedLdlDma, 13, 4>),
-                         dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
-                         dim3(512), (size_t)b2, stream, c);
-      if (variant == 45) return hipGetLastError();
-      LftArgs<double> r = a;
-      r.cond = 1;
-      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>),
-                         dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
-                         dim3(256), (size_t)bytes, stream, r);
-      return hipGetLastError();
-    }
     if (variant == 42)  // stamps (tools/stamps.py --cond), no rerun
       return go(v2::lft_cond_kernel<v2::SchedCondStamped, 13, 4>, bytes);
     if (variant == 40 || variant == 41) {

@@ -23,8 +23,6 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=100)
     ap.add_argument("--variant", type=int, default=32)
-    ap.add_argument("--cond2", action="store_true",
-                    help="two-waves-per-SIMD conditioned-prefix kernel (variant 46)")
     ap.add_argument("--cond", action="store_true",
                     help="conditioned-prefix kernel (variant 42)")
     ap.add_argument("--traj", action="store_true",
@@ -56,13 +54,6 @@ def main():
         NAMES[:8] = ["top wait (DMA of step k)", "J store + diag offsets", "Q/QT image reads (sym)",
                      "E/Xt sweeps", "A/B reads + DMA issue", "update (CondLdl)", "predict products",
                      "query (ElimQ)"]
-    if args.cond2:
-        args.variant = 46
-        args.cond = True
-        NAMES[:10] = ["S: hand-off read + barrier A", "S: DMA wait, A/B reads, DMA issue",
-                      "S: update (CondLdl)", "S: predict", "S: hand-off write + barrier B",
-                      "T: hand-off read + barrier A", "T: DMA wait, image reads, DMA issue",
-                      "T: query", "T: sweeps", "T: hand-off write + barrier B"]
     os.environ["HOP_LFT_VARIANT"] = str(args.variant)
     buf = (C.c_ulonglong * 16)()
     run()
