@@ -72,6 +72,10 @@ const char* hop_last_error(void);
  *          to t_star [batch] / j_star [batch] (both may be NULL otherwise).
  *   dbg_efg [batch][n_use][3][s][s] nullable: E_k, F_k, G_k (stage blocks)
  *   dbg_prefix [batch][n_use][3][s][s] nullable: Ebar_k, Fbar_k, Gbar_k
+ *   s = 13, m = 4, fp64, no debug outputs: two stream-ordered launches, the
+ *          conditioned-prefix kernel (z0 folded into the prefix first, same J to
+ *          ~1e-12) and a rerun of the problems it could not take with the
+ *          reference association (status and failure semantics unchanged).
  */
 int hop_lft_sweep_f64(const double* A_aug, const double* B_aug, const double* Q_aug,
                       const double* R, int64_t r_batch_stride, int64_t r_step_stride,
