@@ -122,8 +122,18 @@ struct SchedLdlDma : SchedLdl {
 struct SchedLdlDmaStamped : SchedLdlDma {
   static constexpr int STAMP = 1;
 };
+// conditioned-prefix kernel, augmented form (default): Sigma_{k+1} = A T as one
+// dependent DPP chain per output row, rows of A_k read from the image with A^T's
+struct SchedCond : SchedLdlDma {
+  static constexpr int AROW = 1;
+};
+template <class C>
+constexpr bool has_arow() {
+  if constexpr (requires { C::AROW; }) return C::AROW != 0;
+  return false;
+}
 // conditioned-prefix kernel + per-section s_memtime stamps (diagnostic, tools/stamps.py --cond)
-struct SchedCondStamped : SchedLdlDma {
+struct SchedCondStamped : SchedCond {
   static constexpr int STAMP = 1;
 };
 // conditioned-prefix kernel on the trajectory form (lft_cond_kernel)
@@ -1321,7 +1331,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 // own association and every chol_inv ladder, so status bits and the failure
 // semantics stay the reference's.
 // ===========================================================================
-template <int S>
+template <class C, int S>
 __device__ __forceinline__ void sym_from_z(const double* img, unsigned zaddr, int c,
                                            double (&r)[S]) {
   const bool in = c < S;
@@ -1595,8 +1605,8 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     // ---- NE = -(Q_k + eps I)^-1 + I, NX = -(QT_k + eps I)^-1 + I (first attempt only)
     double NE[S], NX[S];
     stamp(1);
-    sym_from_z<S>(imQ, zaddr, c, NE);
-    sym_from_z<S>(imT, zaddr, c, NX);
+    sym_from_z<C, S>(imQ, zaddr, c, NE);
+    sym_from_z<C, S>(imT, zaddr, c, NX);
     stamp(2);
     {
       double d1 = 1.0, d2 = 1.0;
@@ -1606,6 +1616,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     }
     stamp(3);
     double at[S + 1], brow[MM];  // at[j] = column j of A~ (lanes > S-1: 0), at[S] = e_S
+    double ar[has_arow<C>() ? S : 1];  // AROW: rows of A_k, read before the image is refilled
+    if constexpr (has_arow<C>()) {
+      const double* pr = imA + c;  // lanes > S-1 read the next row: unused (bcast_j, j < S)
+#pragma unroll
+      for (int i = 0; i < S; ++i) ar[i] = pr[i * S];
+    }
     if constexpr (TRAJ) {  // row c of A_aug = [[A_k, a~],[0, 1]], B_aug = [[B_k],[0]]
       const double* sA = reinterpret_cast<const double*>(wbase + G::OFF_A) + g * 2 * G::CHA;
       const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
@@ -1649,8 +1665,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
       gxy<C, false, S, S + 1>(T, Xs, at);  // T = [Sigma' | m'] A~^T
       static_for<S>([&](auto I) { X[I] = sel_lane<I>(0.0, 1e-9); });
-      double (&at13)[S] = reinterpret_cast<double (&)[S]>(at);
-      gxty<C, false>(Xs, at13, T);  // + A T
+      if constexpr (has_arow<C>()) {
+        gxy<C, false, S, S>(Xs, ar, T);  // + A T, one chain per row
+      } else {
+        double (&at13)[S] = reinterpret_cast<double (&)[S]>(at);
+        gxty<C, false>(Xs, at13, T);  // + A T
+      }
       double y[MM];
       zero(y);
       acc_xy<false, double, MM, MM>(y, rinv, brow);
@@ -1749,13 +1769,15 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
     if (variant == 42)  // stamps (tools/stamps.py --cond), no rerun
       return go(v2::lft_cond_kernel<v2::SchedCondStamped, 13, 4>, bytes);
+    if (variant == 43)  // A/B: A T by lane broadcasts (independent accumulators), no rerun
+      return go(v2::lft_cond_kernel<v2::SchedLdlDma, 13, 4>, bytes);
     if (variant == 40 || variant == 41) {
       // conditioned prefix, then the reference association for the problems it
       // flagged (ST_RERUN); HOP_COND_FORCE=1 flags every problem (tests)
       LftArgs<double> c = a;
       const char* fv = getenv("HOP_COND_FORCE");
       c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
-      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedLdlDma, 13, 4>),
+      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4>),
                          dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
                          dim3(256), (size_t)bytes, stream, c);
       if (variant == 41) return hipGetLastError();  // no rerun (A/B timing of the kernel alone)
