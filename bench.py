@@ -43,7 +43,7 @@ def kernel_path(s, m, dtype):
     """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound."""
     if dtype == "f64" and (s, m) == (13, 4):
         if os.environ.get("HOP_LFT_VARIANT", "40") in ("40", "41"):
-            return "lft_cond_kernel<SchedCond,13,4>", "mfma"
+            return "lft_cond_kernel<SchedCondL,13,4>", "mfma"
         return "lft_sweep_v2_kernel<SchedLdlDma,13,4>", "mfma"
     if (s, m) in SMALL_SHAPES[dtype]:
         return f"lft_small_kernel<{'float' if dtype == 'f32' else 'double'},{s},{m}>", "hbm"

@@ -224,6 +224,37 @@ def test_query_ldl_block_emulated(n):
     assert regs[3 * n][0] > 0
 
 
+@pytest.mark.parametrize("block", ["SweepQSym", "SweepQAB"])
+def test_sweep_blocks_with_lds_reads_emulated(block):
+    """SweepQSym / SweepQAB (the conditioned kernel's sweeps with LDS reads riding
+    in the same asm statement) compute exactly SweepQ<13> (reads are skipped by
+    the emulator; their destinations are outputs only)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    n = 13
+    rng = np.random.default_rng(7)
+    M = rng.standard_normal((n, n))
+    M = M @ M.T + n * np.eye(n)
+    out = []
+    for name in ("SweepQ", block):
+        regs = {}
+        for i in range(n):
+            col = np.zeros(16)
+            col[:n] = M[i]
+            col[i] += 1e-9 - 1.0
+            regs[i] = col
+        regs[n] = np.ones(16)
+        for j in range(7):
+            regs[n + 1 + j] = np.full(16, np.nan)
+        E.run(E.extract(inc, name, n), regs)
+        out.append(np.array([regs[i] for i in range(n + 1)]))
+    assert np.array_equal(out[0], out[1])
+    want = np.eye(n) - np.linalg.inv(M + 1e-9 * np.eye(n))
+    assert np.abs(out[1][:n, :n] - want).max() < 1e-12
+
+
 @pytest.mark.parametrize("n", [3, 13])
 def test_cond_ldl_block_emulated(n):
     """CondLdl<n> (the conditioned-prefix update of SchedCond): from the offset-form

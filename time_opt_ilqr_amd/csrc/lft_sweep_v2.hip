@@ -127,15 +127,26 @@ struct SchedLdlDmaStamped : SchedLdlDma {
 struct SchedCond : SchedLdlDma {
   static constexpr int AROW = 1;
 };
+// + the QT image reads under the E sweep, the A/B reads under the X sweep
+struct SchedCondL : SchedCond {
+  static constexpr int LDSPIPE = 1;
+};
+template <class C>
+constexpr bool has_ldspipe() {
+  if constexpr (requires { C::LDSPIPE; }) return C::LDSPIPE != 0;
+  return false;
+}
+struct SchedCondLStamped : SchedCondL {
+  static constexpr int STAMP = 1;
+};
+
 template <class C>
 constexpr bool has_arow() {
   if constexpr (requires { C::AROW; }) return C::AROW != 0;
   return false;
 }
 // conditioned-prefix kernel + per-section s_memtime stamps (diagnostic, tools/stamps.py --cond)
-struct SchedCondStamped : SchedCond {
-  static constexpr int STAMP = 1;
-};
+
 // conditioned-prefix kernel on the trajectory form (lft_cond_kernel)
 struct SchedCondTraj : SchedLdlDma {
   static constexpr int TRAJ = 1;
@@ -1604,7 +1615,35 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     }
     // ---- NE = -(Q_k + eps I)^-1 + I, NX = -(QT_k + eps I)^-1 + I (first attempt only)
     double NE[S], NX[S];
+    double at[S + 1], brow[MM];  // at[j] = column j of A~ (lanes > S-1: 0), at[S] = e_S
+    double ar[has_arow<C>() ? S : 1];  // AROW: rows of A_k, read before the image is refilled
     stamp(1);
+    if constexpr (has_ldspipe<C>() && !TRAJ) {
+      // QT's sym reads ride under the E sweep, A_k / B_k's under the X sweep
+      sym_from_z<C, S>(imQ, zaddr, c, NE);
+      stamp(2);
+      const bool in = c < S;
+      double o[2 * S];
+      const unsigned aq[2] = {in ? lds_addr(imT) + 8u * c : zaddr,
+                              in ? lds_addr(imT) + 8u * S * c : zaddr};
+      double d1 = 1.0, d2 = 1.0;
+      SweepQSym<S>::run(NE, d1, o, aq);
+#pragma unroll
+      for (int i = 0; i < S; ++i) NX[i] = 0.5 * (o[i] + o[S + i]);
+      double o2[2 * S + MM];
+      const unsigned ab[3] = {in ? lds_addr(imA) + 8u * S * c : zaddr, lds_addr(imA) + 8u * c,
+                              in ? lds_addr(imB) + 8u * MM * c : zaddr};
+      SweepQAB<S>::run(NX, d2, o2, ab);
+      bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        at[j] = o2[j];
+        if constexpr (has_arow<C>()) ar[j] = o2[S + j];
+      }
+#pragma unroll
+      for (int q = 0; q < MM; ++q) brow[q] = o2[2 * S + q];
+      stamp(3);
+    } else {
     sym_from_z<C, S>(imQ, zaddr, c, NE);
     sym_from_z<C, S>(imT, zaddr, c, NX);
     stamp(2);
@@ -1615,8 +1654,6 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
     }
     stamp(3);
-    double at[S + 1], brow[MM];  // at[j] = column j of A~ (lanes > S-1: 0), at[S] = e_S
-    double ar[has_arow<C>() ? S : 1];  // AROW: rows of A_k, read before the image is refilled
     if constexpr (has_arow<C>()) {
       const double* pr = imA + c;  // lanes > S-1 read the next row: unused (bcast_j, j < S)
 #pragma unroll
@@ -1639,6 +1676,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       for (int j = 0; j < S; ++j) at[j] = pa[j];
 #pragma unroll
       for (int j = 0; j < MM; ++j) brow[j] = pbm[j];
+    }
     }
     at[S] = e_s;
     wave_sync();
@@ -1768,16 +1806,16 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (a.s == 13 && a.m == 4) {
     constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
     if (variant == 42)  // stamps (tools/stamps.py --cond), no rerun
-      return go(v2::lft_cond_kernel<v2::SchedCondStamped, 13, 4>, bytes);
-    if (variant == 43)  // A/B: A T by lane broadcasts (independent accumulators), no rerun
-      return go(v2::lft_cond_kernel<v2::SchedLdlDma, 13, 4>, bytes);
+      return go(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes);
+    if (variant == 43)  // A/B: image reads not overlapped with the sweeps, no rerun
+      return go(v2::lft_cond_kernel<v2::SchedCond, 13, 4>, bytes);
     if (variant == 40 || variant == 41) {
       // conditioned prefix, then the reference association for the problems it
       // flagged (ST_RERUN); HOP_COND_FORCE=1 flags every problem (tests)
       LftArgs<double> c = a;
       const char* fv = getenv("HOP_COND_FORCE");
       c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
-      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4>),
+      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondL, 13, 4>),
                          dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
                          dim3(256), (size_t)bytes, stream, c);
       if (variant == 41) return hipGetLastError();  // no rerun (A/B timing of the kernel alone)

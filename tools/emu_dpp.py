@@ -27,8 +27,8 @@ def run(asm_lines, regs):
     """regs: dict operand index -> np.array(16) (modified in place)."""
     for line in asm_lines:
         line = line.split(" row_mask")[0].strip()
-        if not line or line.startswith("s_nop"):
-            continue
+        if not line or line.startswith(("s_nop", "s_waitcnt", "ds_read")):
+            continue  # LDS reads riding in a block are checked on the GPU
         op, rest = line.split(None, 1)
         bc = None
         m = re.search(r"row_newbcast:(\d+)", rest)
