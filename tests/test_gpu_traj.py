@@ -60,6 +60,14 @@ def _oracle(p, rho, n_use=None, extra=None):
     return (Aa, Ba, Qa, Ri, z0, QT), orc.lft_sweep(Aa, Ba, Qa, Ri, z0, QT, n_use)
 
 
+@pytest.fixture(params=["40", "53"])
+def traj_variant(request, monkeypatch):
+    """Fused s=13 trajectory kernels: 53 (default) closed-form stage inverses, 40 stage
+    inverses by Gauss-Jordan sweeps on the built images (both + the rerun launch)."""
+    monkeypatch.setenv("HOP_LFT_VARIANT", request.param)
+    return request.param
+
+
 def _dev_args(st, dev, dtype=None):
     return [_t(st[k], dev, dtype) for k in ("A", "B", "a_res", "X", "U", "xg", "u_ref", "Q")]
 
@@ -91,7 +99,7 @@ def test_augment_kernel_matches_oracle_builders(dev, n, m, N, dt):
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_traj_sweep_vs_reference_goldens(dev, golden_dir, monkeypatch, fused):
+def test_traj_sweep_vs_reference_goldens(dev, golden_dir, monkeypatch, fused, traj_variant):
     """s = 13, m = 4: in-kernel builders (fused) and hop_augment + sweep (unfused)
     against the reference's builders + propagator (traj_synth_n12_m4_N100)."""
     from time_opt_ilqr_amd import engine
@@ -118,7 +126,7 @@ def test_traj_sweep_vs_reference_goldens(dev, golden_dir, monkeypatch, fused):
 
 
 @pytest.mark.parametrize("n,m,N", [(4, 1, 60), (12, 4, 37), (2, 1, 25)])
-def test_traj_sweep_batch_vs_oracle(dev, monkeypatch, n, m, N):
+def test_traj_sweep_batch_vs_oracle(dev, monkeypatch, n, m, N, traj_variant):
     """Batch tails (7 problems), n_use < N, the small-s and generic kernels behind
     the unfused path, and the fused path when the shape has it."""
     from time_opt_ilqr_amd import engine
@@ -176,7 +184,7 @@ def test_traj_extra_stage_cost(dev):
 
 
 @pytest.mark.parametrize("tag,jtol", [("DI_N50", 1e-3), ("Quad_N160", 5e-2)])
-def test_traj_real_first_select(dev, golden_dir, tag, jtol):
+def test_traj_real_first_select(dev, golden_dir, tag, jtol, traj_variant):
     """The first select block of ilqr_timeopt on the real systems (raw
     linearisation captured from the reference): T* equal, J at the real-capture
     bars (the Quadrotor shape runs the fused in-kernel builder)."""
@@ -212,7 +220,7 @@ def test_select_from_trajectory_dropin_DI(dev, golden_dir):
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_traj_nonfinite_and_tiny_horizons(dev, monkeypatch, fused):
+def test_traj_nonfinite_and_tiny_horizons(dev, monkeypatch, fused, traj_variant):
     """A NaN in one problem's trajectory flags only that problem (FloatingPointError
     in the reference); n_use = 1 and t_min = t_max work on both paths."""
     from time_opt_ilqr_amd import engine
@@ -268,3 +276,22 @@ def test_traj_small_fused_vs_unfused_and_oracle(dev, monkeypatch, n, m, dt, tol)
             _, o = _oracle(ps[i], 1.0)
             T, _ = orc.select_horizon(o["J"][None], 3, N)
             assert int(a.t_star[i]) == int(T[0])
+
+
+def test_traj_closed_form_kernel_alone(dev, monkeypatch):
+    """The closed-form trajectory kernel by itself (variant 54, no rerun) against
+    the Gauss-Jordan one (41): nothing handed over at rho_reg = 1, J within 1e-10
+    (their only difference is how Q_aug^-1 and QT_aug^-1 are formed), same T*."""
+    from time_opt_ilqr_amd import engine
+    ps, st = _batch(range(1200, 1237), 12, 4, 60)
+    args = (*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
+    monkeypatch.setenv("HOP_LFT_VARIANT", "54")
+    cf = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=60)
+    monkeypatch.setenv("HOP_LFT_VARIANT", "41")
+    gj = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=60)
+    assert (cf.status.cpu().numpy() == 0).all()
+    assert _rel(cf.J.cpu().numpy(), gj.J.cpu().numpy()) <= 1e-10
+    assert cf.t_star.cpu().tolist() == gj.t_star.cpu().tolist()
+    for b in (0, 36):
+        _, o = _oracle(ps[b], 1.0)
+        assert _rel(cf.J[b].cpu().numpy(), o["J"]) <= 1e-9

@@ -255,8 +255,8 @@ def test_sweep_blocks_with_lds_reads_emulated(block):
     assert np.abs(out[1][:n, :n] - want).max() < 1e-12
 
 
-@pytest.mark.parametrize("n", [3, 13])
-def test_cond_ldl_block_emulated(n):
+@pytest.mark.parametrize("n,block", [(3, "CondLdl"), (13, "CondLdl"), (13, "CondLdlN")])
+def test_cond_ldl_block_emulated(n, block):
     """CondLdl<n> (the conditioned-prefix update of SchedCond): from the offset-form
     S - I and Psi = [Sigma | m] (m on lane n), stream Sigma' = Sigma - Sigma S^-1 Sigma,
     m' = m - Sigma S^-1 m on lane n, and gamma' = gamma - m^T S^-1 m on lane n of
@@ -277,7 +277,8 @@ def test_cond_ldl_block_emulated(n):
     for i in range(n):
         col = rng.standard_normal(16)
         col[:n] = S[i]
-        col[i] -= 1.0
+        if block == "CondLdl":  # offset form; CondLdlN takes S itself
+            col[i] -= 1.0
         regs[i] = col
         for base in (n, 2 * n):
             col = np.zeros(16)
@@ -289,7 +290,7 @@ def test_cond_ldl_block_emulated(n):
     regs[3 * n + 1] = np.ones(16)
     for j in range(10):
         regs[3 * n + 2 + j] = np.full(16, np.nan)
-    E.run(E.extract(inc, "CondLdl", n), regs)
+    E.run(E.extract(inc, block, n), regs)
     X = np.array([regs[2 * n + i] for i in range(n)])
     Si = np.linalg.inv(S)
     want = Sg - Sg @ Si @ Sg

@@ -1764,6 +1764,298 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
 }
 
 
+
+// ===========================================================================
+// SchedCondCF: trajectory form of the conditioned kernel with CLOSED-FORM stage
+// inverses (Q and P are time-invariant).
+//   Q_aug,k + eps I = [[Qs + eps I, q],[q^T, c]],  q = Q e_k, c = e_k^T Q e_k + 2w + rho + eps
+//   (Qs = _sym(Q) + q_reg I, augmented.py:31-47) has the inverse
+//   Qi_ext + w' v'^T with Qi = (Qs + eps I)^-1 (once per problem), v = Qi q,
+//   v' = [v; -1], sigma = c - q.v, w' = v' / sigma.
+//   QT_aug,t + eps I = [[P + eps I, P e],[e^T P, e^T P e + rho + eps]] likewise, with
+//   u = Pi P e = e - eps Pi e and the Schur complement in its cancellation-free
+//   form sigma_T = rho + eps + eps e.u (augmented.py:63-87).
+// So each step needs two matrix-vector products and two rank-1 updates instead
+// of two 13 x 13 Gauss-Jordan sweeps, and S = Sigma_eps + E_k comes out
+// directly (non-offset: CondLdlN).  Qs + eps I or P + eps I not PD, sigma <= 0,
+// a bad pivot or a non-finite J hand the problem to the rerun launch.
+// ===========================================================================
+template <int NN>
+__device__ __forceinline__ void lane_matvec(double& out, double x, const double (&rows)[NN]) {
+  double q4[4] = {0.0, 0.0, 0.0, 0.0};
+  LaneDot4<NN>::fma(q4, x, rows);  // sum_j bcast_j(x) rows[j]
+  out = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+}
+
+template <class C, int S, int MM>
+__global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) {
+  using G = Geo<S, MM>;
+  constexpr int NN = G::NN;
+  static_assert(S < kRowLanes && G::NJA == 5 && G::NJR == 2 && G::NJX == 1 && G::NJV == 1 &&
+                    G::NJU == 1,
+                "trajectory pieces of the s = 13, m = 4 shape");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, c = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned char* wbase = smem_raw + w * G::WAVE_BYTES_T;
+  const unsigned wlds = (unsigned)(uintptr_t)wbase;
+  const long long wave_prob0 = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave;
+  const long long prob = wave_prob0 + g;
+  const bool valid = prob < a.batch;
+  const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
+  const long long pb = valid ? prob : a.batch - 1;
+  const int N = a.n;
+  const TrajArgs<double>& t = a.tr;
+  auto mk = [&](const double* base, long long pstr) {
+    const long long left = (a.batch - pb0) * pstr;
+    const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
+    return __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);
+  };
+  const long long pstA = (long long)a.nalloc * NN * NN * 8, pstR = (long long)a.nalloc * NN * MM * 8;
+  const long long pstX = (long long)(a.nalloc + 1) * NN * 8, pstV = (long long)a.nalloc * NN * 8;
+  const long long pstU = (long long)a.nalloc * MM * 8;
+  const __amdgpu_buffer_rsrc_t rA = mk(t.A, pstA), rB = mk(t.Bm, pstR), rX = mk(t.X, pstX),
+                               rV = mk(t.ares, pstV), rU = mk(t.U, pstU);
+  unsigned voTA[G::NJA], voTR[G::NJR], voTX[1], voTV[1], voTU[1];
+#pragma unroll
+  for (int j = 0; j < G::NJA; ++j)
+    voTA[j] = chunk_voff<G::CHA>(j, lane, wave_prob0, pb0, a.batch, pstA);
+#pragma unroll
+  for (int j = 0; j < G::NJR; ++j)
+    voTR[j] = chunk_voff<G::CHR>(j, lane, wave_prob0, pb0, a.batch, pstR);
+  voTX[0] = chunk_voff<G::CHX>(0, lane, wave_prob0, pb0, a.batch, pstX);
+  voTV[0] = chunk_voff<G::CHV>(0, lane, wave_prob0, pb0, a.batch, pstV);
+  voTU[0] = chunk_voff<G::CHU>(0, lane, wave_prob0, pb0, a.batch, pstU);
+  auto dma_step = [&](int k) {  // A_k, B_k, x_{k+1}, a_k, u_k
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
+                   soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
+    dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
+        voTA, voTR, voTX[0], voTV[0], voTU[0], rA, rB, rX, rV, rU, wlds, soA, soR, soV + NN * 8,
+        soV, soU);
+  };
+  dma_step(0);
+
+  // ---- per-problem constants (lane c = column c; lanes > NN-1 zero)
+  const double* Qg = t.Q + pb * t.q_bs;
+  const double* Pg = t.P + pb * t.p_bs;
+  const bool in = c < NN;
+  const int cc = in ? c : 0;
+  const double eps = 1e-9;
+  bool bad = (a.cond & 2) != 0;
+  // raw Q rows (Q e), (Qs + eps I)^-1 and (P + eps I)^-1 rows, parked per wave in
+  // LDS as register images (row i of lane l at [i][l]; the Q / QT image areas
+  // and the tile slot are free in this kernel) and re-read each step
+  double* lq = reinterpret_cast<double*>(wbase + G::OFF_T);
+  double* lqi = reinterpret_cast<double*>(wbase + G::OFF_Q);
+  double* lpi = reinterpret_cast<double*>(wbase + G::OFF_QT);
+  static_assert(G::TILE_W >= NN * 512 && G::IMGM_W >= NN * 512, "constant images");
+  {
+    double qr[NN], Qi[NN], Pi[NN];
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      qr[i] = in ? Qg[cc * NN + i] : 0.0;  // lane c: Q[c][i], so sum_i bcast_i(e) qr[i] = (Q e)[c]
+      const double qs = 0.5 * (Qg[i * NN + cc] + Qg[cc * NN + i]) + (i == c ? t.q_reg : 0.0);
+      Qi[i] = in ? qs : 0.0;
+      Pi[i] = in ? Pg[i * NN + cc] : 0.0;
+    }
+    // offset form (diag - 1 + eps), swept: -M^-1 + I; back to M^-1 with the lane selects
+    static_for<NN>([&](auto I) {
+      Qi[I] = Qi[I] + sel_lane<I>(0.0, eps - 1.0);
+      Pi[I] = Pi[I] + sel_lane<I>(0.0, eps - 1.0);
+    });
+    double d1 = 1.0, d2 = 1.0;
+    SweepQ<NN>::run(Qi, d1);
+    SweepQ<NN>::run(Pi, d2);
+    bad = bad || !pivots_ok(Qi, d1) || !pivots_ok(Pi, d2);
+    static_for<NN>([&](auto I) {
+      Qi[I] = sel_lane<I>(0.0, 1.0) - Qi[I];
+      Pi[I] = sel_lane<I>(0.0, 1.0) - Pi[I];
+    });
+#pragma unroll
+    for (int i = 0; i < NN; ++i) {
+      lq[i * 64 + lane] = qr[i];
+      lqi[i * 64 + lane] = Qi[i];
+      lpi[i * 64 + lane] = Pi[i];
+    }
+  }
+  auto rows = [&](const double* img, double (&o)[NN]) {
+#pragma unroll
+    for (int i = 0; i < NN; ++i) o[i] = img[i * 64 + lane];
+  };
+  const double xg_c = in ? t.xg[pb * t.xg_bs + cc] : 0.0;
+  const double ur_c = c < MM ? t.u_ref[pb * t.ur_bs + (c < MM ? c : 0)] : 0.0;
+  const double w2 = 2.0 * t.w[pb * t.w_bs];
+  const bool wrap_c = in && ((t.wrap_mask >> c) & 1u);
+  auto err = [&](double x) {  // wrap_error(x - xg) on lane c (utils.py:131-137)
+    double e = in ? x - xg_c : 0.0;
+    if (t.wrap_mask != 0u) {
+      const double we = wrap_angle(e);
+      e = wrap_c ? we : e;
+    }
+    return e;
+  };
+  // e_0, Q e_0, e_0^T Q e_0 (carried: step k's stage block uses e_k)
+  double qe_k, eqe_k;
+  {
+    const double e0 = err(t.X[pb * (long long)(a.nalloc + 1) * NN + cc]);
+    double qr[NN];
+    rows(lq, qr);
+    lane_matvec<NN>(qe_k, e0, qr);
+    eqe_k = row_sum_dpp(in ? e0 * qe_k : 0.0);
+  }
+  double rinv[MM];
+  {
+    const double* Rp = a.R + pb * a.r_bstride;
+#pragma unroll
+    for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
+  }
+  double X[S + 1];  // [Sigma_eps | m], gamma on lane S of X[S]; z0 = e_s (augmented.py:57)
+  static_for<S>([&](auto I) { X[I] = (c == S) ? (I == NN ? 1.0 : 0.0) : sel_lane<I>(0.0, eps); });
+  X[S] = 0.0;
+  const double e_s = (c == S) ? 1.0 : 0.0;
+  const double m1 = (c == NN) ? -1.0 : 0.0;  // lane NN of v' / u'
+
+  double best = 0.0, jprev = 0.0;
+  int tbest = 0;
+  const bool fuse_argmin = a.t_max > 0;
+#pragma unroll 1
+  for (int k = 0; k < N; ++k) {
+    dma_wait();
+    wave_sync();
+    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
+    const double* sX = reinterpret_cast<const double*>(wbase + G::OFF_VX) + g * 2 * G::CHX;
+    const double* sV = reinterpret_cast<const double*>(wbase + G::OFF_VA) + g * 2 * G::CHV;
+    const double* sU = reinterpret_cast<const double*>(wbase + G::OFF_VU) + g * 2 * G::CHU;
+    const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
+    const double* sA = reinterpret_cast<const double*>(wbase + G::OFF_A) + g * 2 * G::CHA;
+    // raw pieces of step k: x_{k+1}, a_k, u_k, row c of A_k and B_k
+    const int cm = c < MM ? c : 0;
+    const double x1 = sX[cc], av = in ? sV[cc] : 0.0, uu = sU[cm];
+    double at[S + 1], brow[MM];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) at[j] = in ? sA[cc * NN + j] : 0.0;
+#pragma unroll
+    for (int j = 0; j < MM; ++j) brow[j] = in ? sR[cc * MM + j] : 0.0;
+    wave_sync();
+    if (k + 1 < N) dma_step(k + 1);
+    // a~_k = a_k - B_k du_k (augmented.py:50); A~ = [[A_k, a~],[0, 1]]
+    const double du = c < MM ? uu - ur_c : 0.0;
+    double bd;
+    {
+      double rb[MM];
+#pragma unroll
+      for (int q = 0; q < MM; ++q) rb[q] = brow[q];
+      bd = 0.0;
+      LaneDot<MM>::fma(bd, du, rb);
+    }
+    const double atil = av - bd;
+    at[NN] = in ? atil : (c == NN ? 1.0 : 0.0);
+    at[S] = e_s;
+    // ---- stage inverse E_k in closed form, S = Sigma_eps + E_k (non-offset)
+    double r[S];
+    {
+      double Qi[NN];
+      rows(lqi, Qi);
+      double v;
+      lane_matvec<NN>(v, qe_k, Qi);  // Qi q
+      const double qv = row_sum_dpp(in ? qe_k * v : 0.0);
+      const double sig = (((eqe_k + w2) + t.rho_reg) + eps) - qv;
+      bad = bad || !(sig > 0.0);
+      const double vp = in ? v : m1;
+      const double wp = vp * recip_nr(sig);
+#pragma unroll
+      for (int i = 0; i < NN; ++i) r[i] = X[i] + Qi[i];
+      r[NN] = X[NN];
+      LaneB<S>::fma(r, wp, vp);  // + w' v'^T
+    }
+    // ---- e_{k+1}: the terminal block of horizon k+1 and the next stage block
+    const double e1 = err(x1);
+    double qe1;
+    {
+      double qr[NN];
+      rows(lq, qr);
+      lane_matvec<NN>(qe1, e1, qr);
+    }
+    const double eqe1 = row_sum_dpp(in ? e1 * qe1 : 0.0);
+    // ---- update: condition the prefix on stage k's cost
+    {
+      double Ht[S];
+      copy(Ht, reinterpret_cast<double (&)[S]>(X));
+      double dmin = 1.0;
+      CondLdlN<S>::run(r, Ht, X, dmin);
+      const double x = bcast<S - 1>(r[S - 1]);
+      bad = bad || !(dmin > 0.0) || (x != x);
+    }
+    // ---- predict
+    {
+      double T[S];
+      zero(T);
+      double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
+      gxy<C, false, S, S + 1>(T, Xs, at);  // T = [Sigma' | m'] A~^T
+      static_for<S>([&](auto I) { X[I] = sel_lane<I>(0.0, eps); });
+      double (&at13)[S] = reinterpret_cast<double (&)[S]>(at);
+      gxty<C, false>(Xs, at13, T);  // + A~ T
+      double y[MM];
+      zero(y);
+      acc_xy<false, double, MM, MM>(y, rinv, brow);
+      acc_xty<false, double, S, MM>(Xs, brow, y);  // + B R^-1 B^T
+    }
+    // ---- query of horizon k+1 with QT_aug[k] (e_{k+1}) in closed form
+    double jk;
+    {
+      double Pi[NN];
+      rows(lpi, Pi);
+      double z;
+      lane_matvec<NN>(z, e1, Pi);  // Pi e
+      const double u = in ? e1 - eps * z : m1;  // Pi P e = e - eps Pi e
+      const double eu = row_sum_dpp(in ? e1 * u : 0.0);
+      const double sig = (t.rho_reg + eps) + eps * eu;
+      bad = bad || !(sig > 0.0);
+      const double wq = u * recip_nr(sig);
+      double rq[S];
+#pragma unroll
+      for (int i = 0; i < NN; ++i) rq[i] = X[i] + Pi[i];
+      rq[NN] = X[NN];
+      LaneB<S>::fma(rq, wq, u);
+      double acc = 0.0, dmin = 1.0;
+      ElimQ<S>::run(rq, acc, dmin, 0.0);
+      const double q = bcast<S>(acc);
+      const double gam = bcast<S>(X[S]);
+      bad = bad || !(dmin > 0.0) || (q != q);
+      jk = 0.5 * (q - gam);
+    }
+    qe_k = qe1;
+    eqe_k = eqe1;
+    bad = bad || !finite_val(jk);
+    if (fuse_argmin) {
+      const int tt = k + 1;
+      if (tt == a.t_min) {
+        best = jk;
+        tbest = tt;
+      } else if (tt > a.t_min && tt <= a.t_max) {
+        const bool bnan = best != best, jnan = jk != jk;
+        if (!bnan && (jnan || jk < best)) {
+          best = jk;
+          tbest = tt;
+        }
+      }
+    }
+    jprev = jk;
+  }
+  dma_wait();
+  if (valid && c == 0) {
+    if (N > 0) a.J[prob * N + N - 1] = jprev;
+    a.status[prob] = bad ? (int)ST_RERUN : 0;
+    if (fuse_argmin && a.t_star != nullptr) {
+      a.t_star[prob] = tbest;
+      a.j_star[prob] = best;
+    }
+  }
+}
+
 }  // namespace v2
 
 // exact-size fast path: returns hipErrorNotSupported when the shape has none
@@ -1774,7 +2066,20 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
     const size_t bytes = (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock);
     const char* ev = getenv("HOP_LFT_VARIANT");
-    const int tv = ev ? atoi(ev) : 40;
+    const int tv = ev ? atoi(ev) : 53;  // default: closed-form stage inverses
+    if (tv == 53 || tv == 54) {  // closed-form stage inverses (+ rerun unless 54)
+      LftArgs<double> c = a;
+      const char* fv = getenv("HOP_COND_FORCE");
+      c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
+      hipLaunchKernelGGL((v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>),
+                         dim3((unsigned)blocks), dim3(256), bytes, stream, c);
+      if (tv == 54) return hipGetLastError();
+      LftArgs<double> r = a;
+      r.cond = 1;
+      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>),
+                         dim3((unsigned)blocks), dim3(256), bytes, stream, r);
+      return hipGetLastError();
+    }
     if (tv == 40 || tv == 41) {  // conditioned prefix + rerun of the flagged problems
       LftArgs<double> c = a;
       const char* fv = getenv("HOP_COND_FORCE");

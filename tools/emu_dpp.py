@@ -39,6 +39,9 @@ def run(asm_lines, regs):
         dst = int(args[0][1:])
         if op == "v_mov_b64":
             regs[dst] = _val(args[1], regs)
+        elif op == "v_mov_b64_dpp":
+            x = _val(args[1], regs)
+            regs[dst] = np.full(LANES, x[bc]) if bc is not None else x
         elif op == "v_fmac_f64_dpp":
             x = _val(args[1], regs)
             if bc is not None:
