@@ -433,3 +433,36 @@ def test_cond_forced_handover_is_the_lft_kernel(dev, monkeypatch):
     assert torch.equal(f.J, r.J) and torch.equal(f.status, r.status)
     assert torch.equal(f.t_star, r.t_star) and torch.equal(f.j_star, r.j_star)
     assert int(r.status[4]) & orc.ST_LU
+
+
+@pytest.mark.parametrize("s,m,dt", [(5, 1, "f32"), (3, 1, "f64"), (4, 2, "f64")])
+def test_small_cond_kernel(dev, monkeypatch, s, m, dt):
+    """Small-s COND kernels (opt-in): alone (HOP_SMALL_COND=2) no problem is handed
+    over and J matches the LFT instantiation (HOP_SMALL_COND=0, the default); with
+    HOP_COND_FORCE=1 the rerun launch recomputes every problem bitwise like the LFT
+    instantiation; cond + rerun (1) keeps chol_inv's status bits on a bad block."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    Bn, N = 131, 40
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(5150 + s, Bn, s, m, N)
+    Q = Q.copy()
+    Q[7, 11] = -np.eye(s)  # LU slot on the LFT path
+    args = [_t(x, dev, tdt) for x in (A, Bm, Q, Ri, z0[0], QT)]
+    monkeypatch.setenv("HOP_SMALL_COND", "0")
+    ref = engine.propagate(*args, t_min=4, t_max=N)
+    monkeypatch.setenv("HOP_SMALL_COND", "2")
+    alone = engine.propagate(*args, t_min=4, t_max=N)
+    st = alone.status.cpu().numpy()
+    assert st[7] == 16 and (np.delete(st, 7) == 0).all()
+    ok = [i for i in range(Bn) if i != 7]
+    tol = 1e-10 if dt == "f64" else 1e-3
+    assert _elem_rel(alone.J.cpu().numpy()[ok], ref.J.cpu().numpy()[ok]) <= tol
+    monkeypatch.setenv("HOP_SMALL_COND", "1")  # cond + rerun (not the default)
+    dflt = engine.propagate(*args, t_min=4, t_max=N)
+    assert torch.equal(dflt.status, ref.status) and int(dflt.status[7]) & orc.ST_LU
+    assert torch.equal(dflt.J[7], ref.J[7])
+    monkeypatch.setenv("HOP_COND_FORCE", "1")
+    forced = engine.propagate(*args, t_min=4, t_max=N)
+    assert torch.equal(forced.J, ref.J) and torch.equal(forced.status, ref.status)
+    assert torch.equal(forced.t_star, ref.t_star)

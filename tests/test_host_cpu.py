@@ -434,6 +434,32 @@ def small_host(tmp_path_factory):
 
 @pytest.mark.parametrize("tag,dt", [("s5_m1_N200", np.float64), ("s3_m1_N50", np.float64),
                                     ("s5_m1_N200", np.float32)])
+def test_small_cond_math_vs_golden(small_host, golden_dir, tag, dt):
+    """The conditioned-prefix arithmetic of the small-s COND kernels (small_math.hpp
+    cond_*), run on the CPU: the reference's J curves and T*, nothing handed over."""
+    d = np.load(os.path.join(golden_dir, f"lft_synth_{tag}.npz"))
+    s, m, N, bs, cnt = (int(d[k]) for k in ("s", "m", "N", "base_seed", "count"))
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(bs, cnt, s, m, N)
+    cast = lambda x: np.ascontiguousarray(x, dtype=dt)  # noqa: E731
+    J = np.zeros((cnt, N), dt)
+    st = np.zeros(cnt, np.int32)
+    ts = np.zeros(cnt, np.int32)
+    fn = (small_host.small_host_cond_sweep_f64 if dt == np.float64
+          else small_host.small_host_cond_sweep_f32)
+    args = [cast(x) for x in (A, Bm, Q, Ri, QT, np.broadcast_to(z0[0], (cnt, s)))]
+    p = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    rc = fn(*[p(x) for x in args], C.c_int64(cnt), N, s, m, int(d["T_min"]), int(d["T_max"]),
+            p(J), p(st), p(ts))
+    assert rc == 0
+    tol = 1e-10 if dt == np.float64 else 2e-3
+    assert _rel_err(J, d["J"]) <= tol
+    assert (st == 0).all()
+    if dt == np.float64:
+        assert ts.tolist() == d["T_star"].tolist()
+
+
+@pytest.mark.parametrize("tag,dt", [("s5_m1_N200", np.float64), ("s3_m1_N50", np.float64),
+                                    ("s5_m1_N200", np.float32)])
 def test_small_kernel_math_vs_golden(small_host, golden_dir, tag, dt):
     """The packed-symmetric sweep-operator arithmetic of lft_small.hip, run on the
     CPU, reproduces the reference's J curves and T* (golden vectors)."""

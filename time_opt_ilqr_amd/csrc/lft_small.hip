@@ -10,6 +10,8 @@
 // Pieces are chunk-major: piece r holds the r-th 16-byte chunk of every lane's
 // block, so a lane reads its own chunk at base + 1024 r + 16 lane (conflict-free
 // ds_read_b128) and the DMA source of lane l is simply block(l) + 16 r.
+#include <stdlib.h>
+
 #include "hop_device.hpp"
 #include "hop_kernels.hpp"
 
@@ -82,7 +84,10 @@ __device__ __forceinline__ void read_block(const unsigned char* wimg, int lane, 
     for (int j = 0; j < C; ++j) out[i][j] = buf[i * C + j];
 }
 
-template <class T, int S, int MM>
+// COND: the conditioned-prefix association (small_math.hpp cond_*; DESIGN.md
+// 3.0) with first-attempt inverses; problems it cannot take get status 16 and
+// are recomputed by the LFT instantiation in rerun mode (a.cond & 1).
+template <class T, int S, int MM, bool COND = false>
 __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
   using G = Geo<T, S, MM>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
@@ -92,9 +97,14 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
   const unsigned wlds = (unsigned)(uintptr_t)wimg;
   const long long wave_prob0 = (long long)blockIdx.x * G::TPB + w * 64;
   const long long prob = wave_prob0 + lane;
-  const bool valid = prob < a.batch;
+  bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
   const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
+  if (!COND && (a.cond & 1)) {  // rerun launch: only the problems the COND kernel handed over
+    const bool need = valid && (a.status[prob] & 16);
+    if (!__any(need)) return;  // wave-uniform; no workgroup barrier in this kernel
+    valid = need;
+  }
   const int N = a.n, mt = a.max_tries;
   constexpr int SS = S * S, SM = S * MM, TS = (int)sizeof(T);
   const long long pstrM = (long long)a.nalloc * SS * TS, pstrB = (long long)a.nalloc * SM * TS;
@@ -132,6 +142,11 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
   ps.st = 0;
   ps.best = T(0);
   ps.tbest = 0;
+  CondState<T, S, MM> cs;
+  if constexpr (COND) {
+    cond_init(cs, z);
+    cs.bad = (a.cond & 2) != 0;
+  }
   T rinv[MM][MM];
   {
     const T* Rp = a.R + pb * a.r_bstride;
@@ -179,17 +194,27 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
       read_block<T, S, MM, G::P_B>(wimg, lane, Bk);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (k + 1 < N) dma_stage(k + 1);
-      stage_compose<T, S, MM>(ps, k, Q, A, Bk, rinv, mt);
+      if constexpr (COND) {
+        Sym<T, S> E;
+        sym_of(E, Q);
+        cs.bad = cs.bad || !spd_inverse_once(E);
+        cond_step<T, S, MM>(cs, E, A, Bk, rinv);
+      } else {
+        stage_compose<T, S, MM>(ps, k, Q, A, Bk, rinv, mt);
+      }
     }
     Gen<T, S> QT;
     read_block<T, S, S, G::P_T>(wimg, lane, QT.a);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (k + 1 < N) dma_query(k + 1);
-    const T jk = query<T, S, MM>(ps, QT, z, mt);
+    T jk;
+    if constexpr (COND) jk = cond_query<T, S, MM>(cs, QT);
+    else jk = query<T, S, MM>(ps, QT, z, mt);
 #pragma unroll
     for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
     jring[JR - 1] = jk;
-    take(ps, k + 1, jk, a.t_min, a.t_max);
+    if constexpr (COND) take(cs, k + 1, jk, a.t_min, a.t_max);
+    else take(ps, k + 1, jk, a.t_min, a.t_max);
   }
   vm_wait();
   if (N > 0) {
@@ -197,10 +222,18 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
     flush(N - tail, tail);
   }
   if (valid) {
-    a.status[prob] = (int)ps.st;
-    if (a.t_max > 0 && a.t_star != nullptr) {
-      a.t_star[prob] = ps.tbest;
-      a.j_star[prob] = ps.best;
+    if constexpr (COND) {
+      a.status[prob] = (cs.bad || (cs.st & kStNonfinite)) ? 16 : 0;
+      if (a.t_max > 0 && a.t_star != nullptr) {
+        a.t_star[prob] = cs.tbest;
+        a.j_star[prob] = cs.best;
+      }
+    } else {
+      a.status[prob] = (int)ps.st;
+      if (a.t_max > 0 && a.t_star != nullptr) {
+        a.t_star[prob] = ps.tbest;
+        a.j_star[prob] = ps.best;
+      }
     }
   }
 }
@@ -222,7 +255,7 @@ struct GeoT {
   static constexpr int TPB = 256;
 };
 
-template <class T, int S, int MM>
+template <class T, int S, int MM, bool COND = false>
 __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
   using G = GeoT<T, S, MM>;
   constexpr int NN = G::NN, TS = G::TS;
@@ -233,9 +266,14 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
   const unsigned wlds = (unsigned)(uintptr_t)wimg;
   const long long wave_prob0 = (long long)blockIdx.x * G::TPB + w * 64;
   const long long prob = wave_prob0 + lane;
-  const bool valid = prob < a.batch;
+  bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
   const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
+  if (!COND && (a.cond & 1)) {  // rerun launch (see lft_small_kernel)
+    const bool need = valid && (a.status[prob] & 16);
+    if (!__any(need)) return;
+    valid = need;
+  }
   const int N = a.n, mt = a.max_tries, NA = a.nalloc;
   const TrajArgs<T>& t = a.tr;
   const long long pA = (long long)NA * NN * NN * TS, pB = (long long)NA * NN * MM * TS;
@@ -328,6 +366,11 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
   ps.st = 0;
   ps.best = T(0);
   ps.tbest = 0;
+  CondState<T, S, MM> cs;
+  if constexpr (COND) {
+    cond_init(cs, z);
+    cs.bad = (a.cond & 2) != 0;
+  }
   T rinv[MM][MM];  // R_inv_cached
   {
     const T* Rp = a.R + pb * a.r_bstride;
@@ -395,12 +438,22 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
     Ak.a[NN][NN] = T(1);
 #pragma unroll
     for (int q = 0; q < MM; ++q) Bk[NN][q] = T(0);
-    stage_compose<T, S, MM>(ps, k, Qk, Ak, Bk, rinv, mt);
-    const T jk = query<T, S, MM>(ps, QTk, z, mt);
+    T jk;
+    if constexpr (COND) {
+      Sym<T, S> E;
+      sym_of(E, Qk);
+      cs.bad = cs.bad || !spd_inverse_once(E);
+      cond_step<T, S, MM>(cs, E, Ak, Bk, rinv);
+      jk = cond_query<T, S, MM>(cs, QTk);
+    } else {
+      stage_compose<T, S, MM>(ps, k, Qk, Ak, Bk, rinv, mt);
+      jk = query<T, S, MM>(ps, QTk, z, mt);
+    }
 #pragma unroll
     for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
     jring[JR - 1] = jk;
-    take(ps, k + 1, jk, a.t_min, a.t_max);
+    if constexpr (COND) take(cs, k + 1, jk, a.t_min, a.t_max);
+    else take(ps, k + 1, jk, a.t_min, a.t_max);
 #pragma unroll
     for (int i = 0; i < NN; ++i) qe[i] = qe1[i];
     eqe = eqe1;
@@ -411,10 +464,18 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
     flush(N - tail, tail);
   }
   if (valid) {
-    a.status[prob] = (int)ps.st;
-    if (a.t_max > 0 && a.t_star != nullptr) {
-      a.t_star[prob] = ps.tbest;
-      a.j_star[prob] = ps.best;
+    if constexpr (COND) {
+      a.status[prob] = (cs.bad || (cs.st & kStNonfinite)) ? 16 : 0;
+      if (a.t_max > 0 && a.t_star != nullptr) {
+        a.t_star[prob] = cs.tbest;
+        a.j_star[prob] = cs.best;
+      }
+    } else {
+      a.status[prob] = (int)ps.st;
+      if (a.t_max > 0 && a.t_star != nullptr) {
+        a.t_star[prob] = ps.tbest;
+        a.j_star[prob] = ps.best;
+      }
     }
   }
 }
@@ -426,16 +487,37 @@ template <class T>
 hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
   if (a.traj && (a.tr.n != a.s - 1 || a.tr.m != a.m || !a.r_is_inv)) return hipErrorNotSupported;
-  auto go = [&](auto kern, int bytes) {
+  // HOP_SMALL_COND=1: the conditioned-prefix kernel, then the LFT instantiation in
+  // rerun mode for the problems it flagged (2: the COND kernel alone, A/B).  Off by
+  // default: one problem per lane at one wave per SIMD is latency-bound, and the
+  // conditioned step measured slower here (config 3: 30.5 M vs 39.7 M sweeps/s)
+  // although it issues half the FLOPs
+  const char* cv = getenv("HOP_SMALL_COND");
+  const int cmode = cv ? atoi(cv) : 0;
+  auto go2 = [&](auto kc, auto kl, int bytes) {
     const long long blocks = (a.batch + 255) / 256;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+    if (cmode == 0) {
+      hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+      return hipGetLastError();
+    }
+    LftArgs<T> c = a;
+    const char* fv = getenv("HOP_COND_FORCE");
+    c.cond = (fv && atoi(fv) == 1) ? 2 : 0;  // 2: hand every problem over (tests)
+    hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
+    if (cmode == 2) return hipGetLastError();
+    LftArgs<T> r = a;
+    r.cond = 1;
+    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
     return hipGetLastError();
   };
 #define HOP_SMALL(S_, M_)                                                                 \
   if (a.s == S_ && a.m == M_)                                                             \
-    return a.traj ? go(small::lft_small_traj_kernel<T, S_, M_>,                           \
-                       small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                           \
-                  : go(small::lft_small_kernel<T, S_, M_>, small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+    return a.traj ? go2(small::lft_small_traj_kernel<T, S_, M_, true>,                    \
+                        small::lft_small_traj_kernel<T, S_, M_, false>,                   \
+                        small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                          \
+                  : go2(small::lft_small_kernel<T, S_, M_, true>,                         \
+                        small::lft_small_kernel<T, S_, M_, false>,                        \
+                        small::Geo<T, S_, M_>::WAVE_BYTES * 4);
   if constexpr (sizeof(T) == 4) {
     HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)
     HOP_SMALL(5, 2)  // s = 6 spills: generic kernel

@@ -50,6 +50,63 @@ static void run(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, 
   }
 }
 
+// conditioned-prefix path (lft_small.hip COND kernels): status = 16 when the
+// problem would be handed to the rerun launch
+template <class T, int S, int MM>
+static void run_cond(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, const T* z0,
+                     int64_t batch, int n, int t_min, int t_max, T* J, int32_t* status,
+                     int32_t* t_star) {
+  for (int64_t b = 0; b < batch; ++b) {
+    CondState<T, S, MM> cs;
+    T z[S], rinv[MM][MM];
+    for (int i = 0; i < S; ++i) z[i] = z0[b * S + i];
+    for (int i = 0; i < MM; ++i)
+      for (int j = 0; j < MM; ++j) rinv[i][j] = Rinv[b * MM * MM + i * MM + j];
+    cond_init(cs, z);
+    for (int k = 0; k < n; ++k) {
+      Gen<T, S> Qk, Ak, QTk;
+      T Bk[S][MM];
+      const int64_t o = (b * n + k) * S * S, ob = (b * n + k) * S * MM;
+      for (int i = 0; i < S; ++i)
+        for (int j = 0; j < S; ++j) {
+          Qk.a[i][j] = Q[o + i * S + j];
+          Ak.a[i][j] = A[o + i * S + j];
+          QTk.a[i][j] = QT[o + i * S + j];
+        }
+      for (int i = 0; i < S; ++i)
+        for (int j = 0; j < MM; ++j) Bk[i][j] = B[ob + i * MM + j];
+      Sym<T, S> E;
+      sym_of(E, Qk);
+      cs.bad = cs.bad || !spd_inverse_once(E);
+      cond_step<T, S, MM>(cs, E, Ak, Bk, rinv);
+      const T jk = cond_query<T, S, MM>(cs, QTk);
+      J[b * n + k] = jk;
+      take(cs, k + 1, jk, t_min, t_max);
+    }
+    status[b] = (cs.bad || (cs.st & kStNonfinite)) ? 16 : 0;
+    t_star[b] = cs.tbest;
+  }
+}
+
+extern "C" int small_host_cond_sweep_f64(const double* A, const double* B, const double* Q,
+                                         const double* Rinv, const double* QT, const double* z0,
+                                         int64_t batch, int n, int s, int m, int t_min, int t_max,
+                                         double* J, int32_t* status, int32_t* t_star) {
+  if (s == 3 && m == 1) run_cond<double, 3, 1>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
+  else if (s == 5 && m == 1) run_cond<double, 5, 1>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
+  else return -1;
+  return 0;
+}
+
+extern "C" int small_host_cond_sweep_f32(const float* A, const float* B, const float* Q,
+                                         const float* Rinv, const float* QT, const float* z0,
+                                         int64_t batch, int n, int s, int m, int t_min, int t_max,
+                                         float* J, int32_t* status, int32_t* t_star) {
+  if (s == 5 && m == 1) run_cond<float, 5, 1>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
+  else return -1;
+  return 0;
+}
+
 extern "C" int small_host_sweep_f64(const double* A, const double* B, const double* Q,
                                     const double* Rinv, const double* QT, const double* z0,
                                     int64_t batch, int n, int s, int m, int mt, int t_min,

@@ -283,14 +283,164 @@ HOP_HD inline T query(State<T, S, MM>& s, const Gen<T, S>& QT, const T (&z)[S], 
   return T(0.5) * quad_inverse(X0, z, mt, s.st);
 }
 
+// ---- conditioned prefix (lft_sweep_v2.hip, SchedCond) ------
+// The same J(t) with z0 folded into the prefix first: state (Sigma + eps I, m,
+// gamma); per stage an LDL^T of S = Sigma_eps + E_k with the rank-1 streams of
+// Sigma', m', gamma', the predict A Sigma' A^T + B R^-1 B^T, and per horizon a
+// bordered elimination of Sigma_eps + X_t.  First attempts only: anything that
+// would need chol_inv's ladder sets `bad` and the problem is recomputed by the
+// LFT path (rerun launch).
+template <class T, int S, int MM>
+struct CondState {
+  Sym<T, S> Sg;  // Sigma + eps I (upper triangle)
+  T m[S];
+  T gam;
+  T best;
+  int tbest;
+  unsigned st;
+  bool bad;
+};
+
+template <class T, int S, int MM>
+HOP_HD inline void cond_init(CondState<T, S, MM>& c, const T (&z)[S]) {
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) c.Sg.v[k] = T(0);
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    c.Sg.at(i, i) = T(1e-9);
+    c.m[i] = z[i];
+  }
+  c.gam = T(0);
+  c.best = T(0);
+  c.tbest = 0;
+  c.st = 0;
+  c.bad = false;
+}
+
+// (sym(M) + 1e-9 I)^-1 on the first attempt only (utils.py:69-93 without the ladder)
+template <class T, int S>
+HOP_HD inline bool spd_inverse_once(Sym<T, S>& m) {
+  const bool ok = sweep_neg_inverse(m, T(1e-9));
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = -m.v[k];
+  return ok;
+}
+
+// condition on stage k (E = (Q_k + eps I)^-1), then predict through A_k, B_k
+template <class T, int S, int MM>
+HOP_HD inline void cond_step(CondState<T, S, MM>& c, const Sym<T, S>& E, const Gen<T, S>& A,
+                             const T (&Bk)[S][MM], const T (&rinv)[MM][MM]) {
+  Sym<T, S> M;
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) M.v[k] = c.Sg.v[k] + E.v[k];
+  T Y[S][S + 1];  // L^-1 [Sigma_eps | m]
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) Y[i][j] = c.Sg.at(i, j);
+    Y[i][S] = c.m[i];
+  }
+  T rd[S];
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    const T d = M.at(p, p);
+    c.bad = c.bad || !(d > T(0));
+    const T r = small_recip(d);
+    rd[p] = r;
+#pragma unroll
+    for (int i = p + 1; i < S; ++i) {
+      const T l = M.at(p, i) * r;
+#pragma unroll
+      for (int j = i; j < S; ++j) M.at(i, j) -= l * M.at(p, j);
+#pragma unroll
+      for (int j = 0; j <= S; ++j) Y[i][j] -= l * Y[p][j];
+    }
+  }
+  Sym<T, S> Sp = c.Sg;  // Sigma' = Sigma_eps - sum_p y_p y_p^T / d_p, m' and gamma' alike
+  T mp[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) mp[i] = c.m[i];
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const T yi = Y[p][i] * rd[p];
+#pragma unroll
+      for (int j = i; j < S; ++j) Sp.at(i, j) -= yi * Y[p][j];
+      mp[i] -= yi * Y[p][S];
+    }
+    c.gam -= Y[p][S] * Y[p][S] * rd[p];
+  }
+  Gen<T, S> Tm;
+  mul_sym_gt(Tm, Sp, A);  // Sigma' A^T
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) c.Sg.v[k] = T(0);
+  acc_sym_xy<false>(c.Sg, A, Tm);  // A Sigma' A^T (upper)
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    T y[MM];
+#pragma unroll
+    for (int q = 0; q < MM; ++q) {
+      T v = T(0);
+#pragma unroll
+      for (int l = 0; l < MM; ++l) v += Bk[i][l] * rinv[l][q];
+      y[q] = v;
+    }
+#pragma unroll
+    for (int j = i; j < S; ++j) {
+      T v = T(0);
+#pragma unroll
+      for (int q = 0; q < MM; ++q) v += y[q] * Bk[j][q];
+      c.Sg.at(i, j) += v;
+    }
+    c.Sg.at(i, i) += T(1e-9);
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    T v = T(0);
+#pragma unroll
+    for (int j = 0; j < S; ++j) v += A.a[i][j] * mp[j];
+    c.m[i] = v;
+  }
+}
+
+// J of horizon k+1: 1/2 (m^T (Sigma_eps + X_t)^-1 m - gamma), X_t = (QT_k + eps I)^-1
+template <class T, int S, int MM>
+HOP_HD inline T cond_query(CondState<T, S, MM>& c, const Gen<T, S>& QT) {
+  Sym<T, S> x;
+  sym_of(x, QT);
+  c.bad = c.bad || !spd_inverse_once(x);
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) x.v[k] += c.Sg.v[k];
+  T b[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) b[i] = c.m[i];
+  T acc = T(0);
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    const T d = x.at(p, p);
+    c.bad = c.bad || !(d > T(0));
+    const T r = small_recip(d);
+    acc += b[p] * b[p] * r;
+#pragma unroll
+    for (int i = p + 1; i < S; ++i) {
+      const T l = x.at(p, i) * r;
+      b[i] -= l * b[p];
+#pragma unroll
+      for (int j = i; j < S; ++j) x.at(i, j) -= l * x.at(p, j);
+    }
+  }
+  return T(0.5) * (acc - c.gam);
+}
+
 template <class T>
 HOP_HD inline bool finite_t(T x) {
   return x == x && x - x == T(0);
 }
 
 // argmin over [t_min, t_max] with np.argmin semantics (first minimiser, a NaN wins)
-template <class T, int S, int MM>
-HOP_HD inline void take(State<T, S, MM>& s, int t, T jk, int t_min, int t_max) {
+template <class T, class St>
+HOP_HD inline void take(St& s, int t, T jk, int t_min, int t_max) {
   if (!finite_t(jk)) s.st |= kStNonfinite;
   if (t_max <= 0) return;
   if (t == t_min) {
