@@ -45,6 +45,9 @@ def kernel_path(s, m, dtype):
         if os.environ.get("HOP_LFT_VARIANT", "40") in ("40", "41"):
             return "lft_cond_kernel<SchedCondL,13,4>", "mfma"
         return "lft_sweep_v2_kernel<SchedLdlDma,13,4>", "mfma"
+    if dtype == "f32" and (s, m) == (13, 4) and os.environ.get("HOP_LFT_VARIANT", "40") in ("40", "41") \
+            and not os.environ.get("HOP_FORCE_GENERIC"):
+        return "lft_cond_kernel<SchedCond,13,4,float>", "mfma"  # fp32 blocks, fp64 arithmetic
     if (s, m) in SMALL_SHAPES[dtype]:
         return f"lft_small_kernel<{'float' if dtype == 'f32' else 'double'},{s},{m}>", "hbm"
     return "lft_sweep_kernel", "mfma"
@@ -195,7 +198,8 @@ def main():
             peak, unit = PEAK_HBM_GBS, "GB/s"
         else:
             achieved = lft_flops(N, s, m) * (hi - lo) / (kern_ms * 1e-3) / 1e12
-            peak = PEAK_F64_TFLOPS if args.dtype == "f64" else PEAK_F32_TFLOPS
+            peak = (PEAK_F64_TFLOPS if args.dtype == "f64" or kname.startswith("lft_cond")
+                    else PEAK_F32_TFLOPS)
             unit = "TFLOP/s"
         traffic = None
         try:
@@ -237,6 +241,8 @@ def main():
                              "executed_frac": cond_flops(N, s, m) * (hi - lo)
                              / (kern_ms * 1e-3) / 1e12 / peak}
                             if kname.startswith("lft_cond") else {}),
+                         **({"arithmetic": "f64 (fp32 blocks in HBM/LDS)"}
+                            if kname.endswith("float>") else {}),
                          "alg_bytes_per_sweep": lft_bytes(N, s, m, 8 if dtype == torch.float64 else 4)},
             "cpu_baseline": cpu,
             "status_ok": status_ok,

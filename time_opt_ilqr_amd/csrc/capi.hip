@@ -91,6 +91,9 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
     if constexpr (sizeof(T) == 8) {
       const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
       if (e != hipErrorNotSupported) return hip_status(e);
+    } else {
+      const hipError_t e = hop::dispatch_lft_v2_f32(a, (hipStream_t)stream);
+      if (e != hipErrorNotSupported) return hip_status(e);
     }
     const char* sv = getenv("HOP_SMALL_VARIANT");  // same-process A/B of the s <= 5 build
     const hipError_t e = (sv && atoi(sv) == 1)

@@ -95,6 +95,7 @@ struct RiccatiArgs {
 template <class T>
 hipError_t dispatch_lft(const LftArgs<T>& a, hipStream_t stream);
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream);
+hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream);
 template <class T>

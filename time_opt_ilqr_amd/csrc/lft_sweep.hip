@@ -64,8 +64,13 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_kernel(LftArgs<T> a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4, w = tid >> 6;
   const long long prob = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave + g;
-  const bool valid = prob < a.batch;
+  bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
+  if (a.cond & 1) {  // rerun launch after the conditioned-prefix kernel (fp32 blocks)
+    const bool need = valid && (a.status[prob] & (int)ST_RERUN);
+    if (!__any(need)) return;  // wave-uniform; no workgroup barrier in this kernel
+    valid = need;
+  }
   T* tile = smem + (w * kProbPerWave + g) * kLdsTile;
 #pragma unroll 1
   for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = T(0);

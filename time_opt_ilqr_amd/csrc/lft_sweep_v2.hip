@@ -709,15 +709,15 @@ __device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsign
 }
 
 
-template <int S, int MM>
+template <int S, int MM, int ES = 8>  // ES: bytes per element of the streamed blocks
 struct Geo {
   static constexpr int SS = S * S;
-  static constexpr int CHM = (SS * 8 + 15) / 16;      // 16-B chunks per S x S block
+  static constexpr int CHM = (SS * ES + 15) / 16;     // 16-B chunks per S x S block
   static constexpr int IMGM = CHM * 16;               // bytes per problem image (16-aligned)
   static constexpr int NJM = (kProbPerWave * CHM + 63) / 64;  // DMA instrs per block type
   static constexpr int IMGM_W = NJM * 1024;           // bytes per wave image (DMA writes 1 KiB)
   static constexpr int SM = S * MM;
-  static constexpr int CHB = (SM * 8 + 15) / 16;
+  static constexpr int CHB = (SM * ES + 15) / 16;
   static constexpr int IMGB = CHB * 16;
   static constexpr int NJB = (kProbPerWave * CHB + 63) / 64;
   static constexpr int IMGB_W = NJB * 1024;
@@ -738,7 +738,8 @@ struct Geo {
   static constexpr int CHX = (NN * 8 + 15) / 16, NJX = (kProbPerWave * CHX + 63) / 64;
   static constexpr int CHV = (NN * 8 + 15) / 16, NJV = (kProbPerWave * CHV + 63) / 64;
   static constexpr int CHU = (MM * 8 + 15) / 16, NJU = (kProbPerWave * CHU + 63) / 64;
-  static_assert(NJA <= NJM && NJR <= NJB, "raw blocks must fit the augmented image areas");
+  static_assert(ES != 8 || (NJA <= NJM && NJR <= NJB),
+                "raw blocks must fit the augmented image areas");
   static constexpr int OFF_VX = OFF_T + TILE_W, OFF_VA = OFF_VX + 1024 * NJX,
                        OFF_VU = OFF_VA + 1024 * NJV;
   // raw Q of the wave's problems, transposed (lane c reads its row as a column)
@@ -1471,10 +1472,16 @@ struct CondTraj {
   }
 };
 
-template <class C, int S, int MM>
-__global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
-  using G = Geo<S, MM>;
+// T = float: fp32 blocks in HBM / LDS (half the bytes), converted on the LDS
+// reads; the arithmetic stays fp64 (fp32 DPP FMAs issue no faster at one wave
+// per SIMD) and J / J* are rounded to fp32 on the store.
+template <class C, int S, int MM, class T = double>
+__global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
+  constexpr int ES = (int)sizeof(T);
+  constexpr bool F32 = ES == 4;
+  using G = Geo<S, MM, ES>;
   constexpr bool TRAJ = has_traj<C>();
+  static_assert(!F32 || (!TRAJ && !has_ldspipe<C>()), "fp32 blocks: augmented form, plain reads");
   constexpr int NN = G::NN;
   static_assert(S < kRowLanes, "m rides on lane S");
   static_assert(G::TILE_W >= 8 * S * S + 64, "zero area in the tile slot");
@@ -1489,10 +1496,11 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
   const unsigned zaddr = wlds + G::OFF_T;
 #pragma unroll 1
   for (int i = lane; i < S * S + 8; i += 64) zarea[i] = 0.0;
-  const double* imQ = reinterpret_cast<const double*>(wbase + G::OFF_Q + g * G::IMGM);
-  const double* imA = reinterpret_cast<const double*>(wbase + G::OFF_A + g * G::IMGM);
-  const double* imT = reinterpret_cast<const double*>(wbase + G::OFF_QT + g * G::IMGM);
-  const double* imB = reinterpret_cast<const double*>(wbase + G::OFF_B + g * G::IMGB);
+  const T* imQ = reinterpret_cast<const T*>(wbase + G::OFF_Q + g * G::IMGM);
+  const T* imA = reinterpret_cast<const T*>(wbase + G::OFF_A + g * G::IMGM);
+  const T* imT = reinterpret_cast<const T*>(wbase + G::OFF_QT + g * G::IMGM);
+  const T* imB = reinterpret_cast<const T*>(wbase + G::OFF_B + g * G::IMGB);
+  const T* zareaT = reinterpret_cast<const T*>(zarea);
 
   const long long wave_prob0 = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave;
   const long long prob = wave_prob0 + g;
@@ -1500,13 +1508,13 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
   const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
   const int N = a.n;
   constexpr int SS = S * S, SM = S * MM;
-  const long long pstrM = (long long)a.nalloc * SS * 8;
-  const long long pstrB = (long long)a.nalloc * SM * 8;
-  auto mk = [&](const double* base, long long pstr) {
+  const long long pstrM = (long long)a.nalloc * SS * ES;
+  const long long pstrB = (long long)a.nalloc * SM * ES;
+  auto mk = [&](const T* base, long long pstr) {
     const long long left = (a.batch - pb0) * pstr;
     const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
     return __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<double*>(base) + pb0 * (pstr / 8), (short)0, (int)nrec, 0x00020000);
+        const_cast<T*>(base) + pb0 * (pstr / ES), (short)0, (int)nrec, 0x00020000);
   };
   const long long pstA = (long long)a.nalloc * NN * NN * 8, pstR = (long long)a.nalloc * NN * MM * 8;
   const long long pstX = (long long)(a.nalloc + 1) * NN * 8, pstV = (long long)a.nalloc * NN * 8;
@@ -1546,34 +1554,44 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
           voTA, voTR, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR,
           soV + NN * 8, soV, soU);
-    } else {
-      static_assert(TRAJ || (G::NJM == 6 && G::NJB == 2), "augmented pieces of s = 13, m = 4");
-      const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
+    } else if constexpr (G::NJM == 6 && G::NJB == 2) {
+      const unsigned soM = (unsigned)(k * SS * ES), soB = (unsigned)(k * SM * ES);
       dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
                                                          soB);
+    } else {
+      const unsigned soM = (unsigned)(k * SS * ES), soB = (unsigned)(k * SM * ES);
+#pragma unroll
+      for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rQ, wlds + G::OFF_Q + 1024 * j, soM);
+#pragma unroll
+      for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rA, wlds + G::OFF_A + 1024 * j, soM);
+#pragma unroll
+      for (int j = 0; j < G::NJB; ++j) dma16(voB[j], rB, wlds + G::OFF_B + 1024 * j, soB);
+#pragma unroll
+      for (int j = 0; j < G::NJM; ++j) dma16(voM[j], rT, wlds + G::OFF_QT + 1024 * j, soM);
     }
   };
 
   const long long pb = valid ? prob : a.batch - 1;
   double rinv[MM];
   {
-    const double* Rp = a.R + pb * a.r_bstride;
+    const T* Rp = a.R + pb * a.r_bstride;
 #pragma unroll
-    for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
+    for (int i = 0; i < MM; ++i)
+      rinv[i] = (c < MM) ? (double)Rp[i * MM + (c < MM ? c : 0)] : 0.0;
   }
   double* cq = reinterpret_cast<double*>(wbase + G::OFF_CQ) + g * NN * NN;
   CondTraj<S, MM> tb;
-  if constexpr (TRAJ) {
+  if constexpr (TRAJ && !F32) {
     tb.init(a, pb, c, cq, const_cast<double*>(imQ), const_cast<double*>(imT));
     wave_sync();
     tb.load_rows(cq, imT, c);
   }
   // X = [Sigma_0 + eps I | z0], gamma_0 = 0 (Sigma_0 = 0: z0 known exactly);
   // the trajectory form's z0 is e_s (augmented.py:57)
-  const double* zp = a.z0 + pb * a.z_bstride;
+  const T* zp = a.z0 + pb * a.z_bstride;
   double X[S + 1];
   static_for<S>([&](auto I) {
-    const double z = TRAJ ? (I == NN ? 1.0 : 0.0) : zp[I];
+    const double z = TRAJ ? (I == NN ? 1.0 : 0.0) : (double)zp[I];
     X[I] = (c == S) ? z : sel_lane<I>(0.0, 1e-9);
   });
   X[S] = 0.0;
@@ -1601,9 +1619,10 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     dma_wait();
     wave_sync();
     stamp(0);
-    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
+    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = (T)jprev;
     double atil = 0.0;
-    if constexpr (TRAJ) {
+    if constexpr (F32) {
+    } else if constexpr (TRAJ) {
       const double* sX = reinterpret_cast<const double*>(wbase + G::OFF_VX) + g * 2 * G::CHX;
       const double* sV = reinterpret_cast<const double*>(wbase + G::OFF_VA) + g * 2 * G::CHV;
       const double* sU = reinterpret_cast<const double*>(wbase + G::OFF_VU) + g * 2 * G::CHU;
@@ -1644,8 +1663,25 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       for (int q = 0; q < MM; ++q) brow[q] = o2[2 * S + q];
       stamp(3);
     } else {
-    sym_from_z<C, S>(imQ, zaddr, c, NE);
-    sym_from_z<C, S>(imT, zaddr, c, NX);
+    if constexpr (F32) {  // fp32 images: converting reads, offset form applied in fp64
+      const bool in = c < S;
+      const T* qc = in ? imQ + c : zareaT;
+      const T* qr = in ? imQ + S * c : zareaT;
+      const T* tc = in ? imT + c : zareaT;
+      const T* tr = in ? imT + S * c : zareaT;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        NE[i] = 0.5 * ((double)qc[S * i] + (double)qr[i]);
+        NX[i] = 0.5 * ((double)tc[S * i] + (double)tr[i]);
+      }
+      static_for<S>([&](auto I) {
+        NE[I] += sel_lane<I>(0.0, 1e-9 - 1.0);
+        NX[I] += sel_lane<I>(0.0, 1e-9 - 1.0);
+      });
+    } else {
+      sym_from_z<C, S>(imQ, zaddr, c, NE);
+      sym_from_z<C, S>(imT, zaddr, c, NX);
+    }
     stamp(2);
     {
       double d1 = 1.0, d2 = 1.0;
@@ -1655,11 +1691,11 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     }
     stamp(3);
     if constexpr (has_arow<C>()) {
-      const double* pr = imA + c;  // lanes > S-1 read the next row: unused (bcast_j, j < S)
+      const T* pr = imA + c;  // lanes > S-1 read the next row: unused (bcast_j, j < S)
 #pragma unroll
-      for (int i = 0; i < S; ++i) ar[i] = pr[i * S];
+      for (int i = 0; i < S; ++i) ar[i] = (double)pr[i * S];
     }
-    if constexpr (TRAJ) {  // row c of A_aug = [[A_k, a~],[0, 1]], B_aug = [[B_k],[0]]
+    if constexpr (TRAJ && !F32) {  // row c of A_aug = [[A_k, a~],[0, 1]], B_aug = [[B_k],[0]]
       const double* sA = reinterpret_cast<const double*>(wbase + G::OFF_A) + g * 2 * G::CHA;
       const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
       const int cc = c < NN ? c : 0;
@@ -1670,12 +1706,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       for (int j = 0; j < MM; ++j) brow[j] = c < NN ? sR[cc * MM + j] : 0.0;
     } else {
       const bool in = c < S;
-      const double* pa = in ? imA + S * c : zarea;  // branch-free: lanes > S-1 read zeros
-      const double* pbm = in ? imB + MM * c : zarea;
+      const T* pa = in ? imA + S * c : zareaT;  // branch-free: lanes > S-1 read zeros
+      const T* pbm = in ? imB + MM * c : zareaT;
 #pragma unroll
-      for (int j = 0; j < S; ++j) at[j] = pa[j];
+      for (int j = 0; j < S; ++j) at[j] = (double)pa[j];
 #pragma unroll
-      for (int j = 0; j < MM; ++j) brow[j] = pbm[j];
+      for (int j = 0; j < MM; ++j) brow[j] = (double)pbm[j];
     }
     }
     at[S] = e_s;
@@ -1698,16 +1734,16 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     stamp(5);
     // ---- predict: Sigma_{k+1} = A Sigma' A^T + B R^-1 B^T + eps I, m_{k+1} = A m'
     {
-      double T[S];
-      zero(T);
+      double Tm[S];
+      zero(Tm);
       double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
-      gxy<C, false, S, S + 1>(T, Xs, at);  // T = [Sigma' | m'] A~^T
+      gxy<C, false, S, S + 1>(Tm, Xs, at);  // T = [Sigma' | m'] A~^T
       static_for<S>([&](auto I) { X[I] = sel_lane<I>(0.0, 1e-9); });
       if constexpr (has_arow<C>()) {
-        gxy<C, false, S, S>(Xs, ar, T);  // + A T, one chain per row
+        gxy<C, false, S, S>(Xs, ar, Tm);  // + A T, one chain per row
       } else {
         double (&at13)[S] = reinterpret_cast<double (&)[S]>(at);
-        gxty<C, false>(Xs, at13, T);  // + A T
+        gxty<C, false>(Xs, at13, Tm);  // + A T
       }
       double y[MM];
       zero(y);
@@ -1729,7 +1765,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
       jk = 0.5 * (q - gam);
     }
     stamp(7);
-    if constexpr (TRAJ) tb.load_rows(cq, imT, c);
+    if constexpr (TRAJ && !F32) tb.load_rows(cq, imT, c);
     bad = bad || !finite_val(jk);
     if (fuse_argmin) {
       const int t = k + 1;
@@ -1754,11 +1790,11 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<double> a) {
     }
   }
   if (valid && c == 0) {
-    if (N > 0) a.J[prob * N + N - 1] = jprev;
+    if (N > 0) a.J[prob * N + N - 1] = (T)jprev;
     a.status[prob] = bad ? (int)ST_RERUN : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
-      a.j_star[prob] = best;
+      a.j_star[prob] = (T)best;
     }
   }
 }
@@ -2156,6 +2192,30 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   return hipErrorNotSupported;
 }
 
+}  // namespace hop
+
+// fp32 blocks at s = 13, m = 4: the conditioned-prefix kernel on fp32 images
+// (fp64 arithmetic), then the generic fp32 kernel in rerun mode for the problems
+// it flagged.  HOP_LFT_VARIANT=30 (or any LFT schedule) keeps the generic path.
+namespace hop {
+hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
+  if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv || a.traj) return hipErrorNotSupported;
+  if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
+  const char* ev = getenv("HOP_LFT_VARIANT");
+  const int variant = ev ? atoi(ev) : 40;
+  if (variant != 40 && variant != 41) return hipErrorNotSupported;
+  using G = v2::Geo<13, 4, 4>;
+  const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+  LftArgs<float> c = a;
+  const char* fv = getenv("HOP_COND_FORCE");
+  c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
+  hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4, float>), dim3((unsigned)blocks),
+                     dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
+  if (variant == 41) return hipGetLastError();
+  LftArgs<float> r = a;
+  r.cond = 1;
+  return dispatch_lft<float>(r, stream);
+}
 }  // namespace hop
 
 // Diagnostic (not part of include/hop.h): read (and optionally reset) the
