@@ -1735,9 +1735,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     // ---- predict: Sigma_{k+1} = A Sigma' A^T + B R^-1 B^T + eps I, m_{k+1} = A m'
     {
       double Tm[S];
-      zero(Tm);
       double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
-      gxy<C, false, S, S + 1>(Tm, Xs, at);  // T = [Sigma' | m'] A~^T
+      // T = [Sigma' | m'] A~^T; A~^T's row S is e_S, so its term is X masked to lane S
+#pragma unroll
+      for (int i = 0; i < S; ++i) Tm[i] = X[i] * e_s;
+      double (&atS)[S] = reinterpret_cast<double (&)[S]>(at);
+      gxy<C, false, S, S>(Tm, Xs, atS);
       static_for<S>([&](auto I) { X[I] = sel_lane<I>(0.0, 1e-9); });
       if constexpr (has_arow<C>()) {
         gxy<C, false, S, S>(Xs, ar, Tm);  // + A T, one chain per row
