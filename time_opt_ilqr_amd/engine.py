@@ -103,7 +103,9 @@ def propagate(A, B, Q, R, z0, QT, *, n_use: Optional[int] = None, r_is_inverse: 
         z_bs = 0
     n_eff = max(n_use, 0)
     J = torch.empty((Bn, n_eff), dtype=dt, device=dev) if out is None else out
-    status = torch.zeros((Bn,), dtype=torch.int32, device=dev)
+    # every sweep kernel writes the status of each problem it runs; only the
+    # n_use <= 0 call launches nothing (and must report 0)
+    status = (torch.empty if n_eff > 0 else torch.zeros)((Bn,), dtype=torch.int32, device=dev)
     fuse = t_max is not None
     ts = torch.empty((Bn,), dtype=torch.int32, device=dev) if fuse else None
     js = torch.empty((Bn,), dtype=dt, device=dev) if fuse else None
