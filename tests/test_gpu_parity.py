@@ -494,3 +494,30 @@ def test_cond_fp32_blocks_config5_shape(dev, monkeypatch, golden_dir):
     gen = engine.propagate(*args, **kw)
     assert torch.equal(forced.J, gen.J) and torch.equal(forced.status, gen.status)
     assert _elem_rel(gen.J.cpu().numpy(), d["J"]) <= 2e-3
+
+
+def test_cond_nonfinite_short_horizons_and_tails(dev):
+    """Default s=13 path (conditioned kernel + rerun): a NaN block is handed over and
+    reported exactly as the reference association reports it (non-finite J at that
+    horizon, ST_NONFINITE); N = 1 and t_min = t_max; a batch of 17 (tail of 1)."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    Bn, s, m, N = 17, 13, 4, 12
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(6060, Bn, s, m, N)
+    QT = QT.copy()
+    QT[16, 5, 2, 3] = np.nan
+    args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
+    res = engine.propagate(*args, t_min=3, t_max=3)
+    st = res.status.cpu().numpy()
+    J = res.J.cpu().numpy()
+    assert st[16] & orc.ST_NONFINITE and (st[:16] == 0).all()
+    assert np.isnan(J[16, 5]) and np.isfinite(np.delete(J[16], 5)).all()
+    Jo, _ = orc.lft_sweep_batch(A[:16], Bm[:16], Q[:16], Ri[:16], z0[0], QT[:16])
+    assert _elem_rel(J[:16], Jo) <= 1e-10
+    assert (res.t_star.cpu().numpy()[:16] == 3).all()
+    one = engine.propagate(*args, n_use=1)
+    Jo1, _ = orc.lft_sweep_batch(A, Bm, Q, Ri, z0[0], QT, N=1)
+    assert _elem_rel(one.J.cpu().numpy(), Jo1) <= 1e-10
+    assert int(one.status.abs().sum()) == 0
+    empty = engine.propagate(*args, n_use=0)
+    assert empty.J.shape == (Bn, 0) and int(empty.status.abs().sum()) == 0
