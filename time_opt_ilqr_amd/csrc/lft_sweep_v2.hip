@@ -21,6 +21,10 @@
 //    dependent chain of pivot p+1 (broadcast, v_rcp_f64, Newton-folded scale)
 //    is interleaved into the 13 broadcast-FMAs of pivot p.
 //
+// This file also holds the conditioned-prefix kernels (lft_cond_kernel,
+// lft_cond_cf_kernel), the default for s = 13, m = 4, which hand
+// the problems they cannot take to lft_sweep_v2_kernel in rerun mode.
+//
 // Schedules are runtime-selectable (HOP_LFT_VARIANT) for same-process A/B:
 //   2  Select : compiler-scheduled pivots with lane-p selects (first v2)
 //   8  Chain  : offset form, short C++ pivot chain, pad-free DPP blocks
@@ -28,8 +32,15 @@
 //   12 SchedRow: Sched + X*Y products as one dependent DPP chain per output
 //      row (accumulator forwarded: 4.0 vs 4.9 cycles per FMA)
 //   14 SchedLdl: SchedRow + the query's Wt = (QT^-1 + Gbar)^-1 and its two
-//      products replaced by one LDL^T elimination that streams X0 (default)
-//   20 SchedLdl + per-section s_memtime stamps (diagnostic, tools/stamps.py)
+//      products replaced by one LDL^T elimination that streams X0
+//   30 SchedLdlDma: SchedLdl with the step's LDS-DMA pieces from one asm block
+//      (the reference association; the rerun path of the conditioned kernels)
+//   20 / 32 stamped SchedLdl / SchedLdlDma (diagnostic, tools/stamps.py)
+//   40 (default) conditioned prefix SchedCondL + rerun; 41 without the rerun;
+//   42 its stamps (tools/stamps.py --cond); 43 SchedCond (no LDS reads inside
+//   the sweep blocks).  Trajectory form: 53 (default) closed-form stage
+//   inverses + rerun, 54 without; 40 / 41 Gauss-Jordan stage inverses; 24
+//   stamped SchedLdlTraj.
 #include <stdlib.h>
 
 #include "hop_device.hpp"
@@ -84,17 +95,6 @@ constexpr bool has_qldl() {
   if constexpr (requires { C::QLDL; }) return C::QLDL != 0;
   return false;
 }
-struct SchedLdl2 : SchedLdl {  // + compose by two-pass LDL^T (no W inverse, no products)
-  static constexpr int CLDL = 1;
-};
-template <class C>
-constexpr bool has_cldl() {
-  if constexpr (requires { C::CLDL; }) return C::CLDL != 0;
-  return false;
-}
-struct SchedLdl2Stamped : SchedLdl2 {
-  static constexpr int STAMP = 1;
-};
 struct SchedStamped : SchedLdl {
   static constexpr int STAMP = 1;
 };
@@ -104,15 +104,6 @@ struct SchedLdlTraj : SchedLdl {
   static constexpr int TRAJ = 1;
 };
 struct SchedLdlTrajStamped : SchedLdlTraj {
-  static constexpr int STAMP = 1;
-};
-// software pipeline across steps: the query of step k-1 runs at the top of step
-// k, and its bordered elimination is interleaved instruction by instruction
-// with the W_k sweep (SweepElimQ): two latency-bound chains hide each other
-struct SchedPipe : SchedLdl {
-  static constexpr int PIPE = 1;
-};
-struct SchedPipeStamped : SchedPipe {
   static constexpr int STAMP = 1;
 };
 // the step's 20 LDS-DMA pieces issued from one asm block (dma_step20)
@@ -145,17 +136,10 @@ constexpr bool has_arow() {
   if constexpr (requires { C::AROW; }) return C::AROW != 0;
   return false;
 }
-// conditioned-prefix kernel + per-section s_memtime stamps (diagnostic, tools/stamps.py --cond)
-
 // conditioned-prefix kernel on the trajectory form (lft_cond_kernel)
 struct SchedCondTraj : SchedLdlDma {
   static constexpr int TRAJ = 1;
 };
-template <class C>
-constexpr bool has_pipe() {
-  if constexpr (requires { C::PIPE; }) return C::PIPE != 0;
-  return false;
-}
 template <class C>
 constexpr bool has_traj() {
   if constexpr (requires { C::TRAJ; }) return C::TRAJ != 0;
@@ -410,28 +394,6 @@ __device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c
   return q;
 }
 
-// SchedPipe: W_k = -(sym(w) + eps I)^-1 (offset form, parked in tw) and the
-// bordered elimination of X0_{k-1} (parked in tile, row S = z0) in one asm block.
-template <class C, int S>
-__device__ __forceinline__ double neg_inverse_and_quad(double (&w)[S], double* tw, double* tile,
-                                                       int c, int mt, unsigned& st, double off) {
-  lds_put(tw, c, w);
-  diag_add<S, kLdsRow>(tw, c, 1e-9 - 1.0 - off);
-  wave_sync();
-  double x[S];
-  sym_from<C, S, kLdsRow>(tw, c, w);
-  sym_from<C, S, kLdsRow>(tile, c, x);
-  double dminw = 1.0, acc = 0.0, dminx = 1.0;
-  SweepElimQ<S>::run(w, dminw, x, acc, dminx, 1e-9);
-  bool okw = pivots_ok(w, dminw);
-  double q = bcast<S>(acc);
-  const bool okx = (dminx > 0.0) && (q == q);
-  if (__any(!okw)) retry_inverse<C, S, kLdsRow>(w, tw, c, okw, mt, st);
-  if (__any(!okx)) q = quad_retry<C, S>(x, tile, c, okx, q, mt, st);
-  wave_sync();
-  return q;
-}
-
 // Query without the Wt inverse (has_qldl): r = Xt + Gbar - I (offset form) is
 // parked, symmetrised and eliminated (QueryLdl); the same row operations turn a
 // copy of H = Fbar^T into L^-1 H and X0 = Ebar - sum_p Ht_p (x) Ht_p / d_p is
@@ -479,61 +441,6 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
   wave_sync();
 }
 
-
-// ---------------------------------------------------------------------------
-// Compose by two-pass LDL^T (has_cldl): M = E_k + Gbar_{k-1} = L D L^T.
-//   pass 1: eliminate M (offset form, in registers, retry ladder from the tile);
-//           afterwards row p of r holds U_p = D L^T row p at lanes > p and
-//           d_p - 1 at lane p (rows are never touched once they are pivots).
-//   pass 2: no dependent chains: Htil = L^-1 H and Ftil = L^-1 F by forward
-//           substitution (H_i += bcast_i(U_p) (-Htil_p / d_p), i > p), and the
-//           three products of the compose streamed as rank-1 updates:
-//             Ebar   -= sum_p Htil_p (x) Htil_p / d_p    (Fbar W Fbar^T)
-//             Fbar^T' = sum_p Ftil_p (x) Htil_p / d_p    (F^T W Fbar^T)
-//             Gbar    = G - sum_p Ftil_p (x) Ftil_p / d_p (G - F^T W F)
-// ---------------------------------------------------------------------------
-template <class C, int S, int p>
-__device__ __forceinline__ void elim_pivot_off(double (&r)[S], double& dmin) {
-  double d = 1.0;
-  // block p-1 wrote S-p rows, r[p] first: fewer than 3 leave < 2 wait states
-  fmac_bcast<p, p == 0 || (S - p) <= 2>(d, r[p], 1.0);
-  const double rd0 = __builtin_amdgcn_rcp(d);
-  const double e = __builtin_fma(-d, rd0, 1.0);
-  const double sc0 = -r[p] * rd0;
-  dmin = __builtin_fmin(dmin, d);
-  const double sc = __builtin_fma(sc0, e, sc0);
-  if constexpr (p == 0) TailB<S>::template elim<p>(r, sc);
-  else TailB<S>::template elimq<p>(r, sc);
-}
-
-// a NaN pivot turns every later row NaN, the last one included
-template <int S>
-__device__ __forceinline__ bool elim_ok(const double (&r)[S], double dmin) {
-  const double x = bcast<S - 1>(r[S - 1]);
-  return (dmin > 0.0) && (x == x);
-}
-
-template <class C, int S>
-__device__ __forceinline__ void compose_pass2(const double (&r)[S], double (&H)[S], double (&F)[S],
-                                              double (&Eb)[S], double (&Gb)[S]) {
-  double H2[S];
-  zero(H2);
-  static_for<S>([&](auto P) {
-    constexpr int p = P;
-    double d = 1.0;
-    fmac_bcast<p, p == 0>(d, r[p], 1.0);
-    const double rd0 = __builtin_amdgcn_rcp(d);
-    const double e = __builtin_fma(-d, rd0, 1.0);
-    const double r1 = __builtin_fma(rd0, e, rd0);
-    const double hs = -H[p] * r1, fs = -F[p] * r1;
-    LaneT<S>::template fmaq<p>(H, r[p], hs);  // Htil rows below p
-    LaneT<S>::template fmaq<p>(F, r[p], fs);  // Ftil rows below p
-    LaneB<S>::fmaq(Eb, H[p], hs);
-    LaneB<S>::fma_negq(H2, F[p], hs);
-    LaneB<S>::fmaq(Gb, F[p], fs);
-  });
-  copy(H, H2);
-}
 
 // Negated inverse of sym(img): r <- -(sym(M) + eps I)^-1  (+ I in offset form)
 template <class C, int S, int LD>
@@ -726,9 +633,6 @@ struct Geo {
   static constexpr int OFF_Q = 0, OFF_A = IMGM_W, OFF_QT = 2 * IMGM_W, OFF_B = 3 * IMGM_W;
   static constexpr int OFF_T = 3 * IMGM_W + IMGB_W;
   static constexpr int WAVE_BYTES = OFF_T + TILE_W;
-  // has_cldl: a second tile set parks QT^-1 (NX) across the compose
-  static constexpr int OFF_X = OFF_T + TILE_W;
-  static constexpr int WAVE_BYTES_X = OFF_X + TILE_W;
   // trajectory form (n = S-1): raw A_k staged in the A image area, raw B_k in
   // the B area, then x_{k+1}, a_k and u_k after the tiles.  Per problem the
   // staged block of a piece type is CH 16-B chunks at 16 CH g.
@@ -763,20 +667,16 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   using G = Geo<S, MM>;
   constexpr bool OFF = offset_form<C>();
   constexpr bool TRAJ = has_traj<C>();
-  static_assert(!TRAJ || (OFF && C::ELIM && !has_cldl<C>()), "trajectory form: SchedLdl family");
-  constexpr bool PIPE = has_pipe<C>();
-  static_assert(!PIPE || (has_qldl<C>() && !has_cldl<C>() && !TRAJ), "pipelined query: SchedLdl");
+  static_assert(!TRAJ || (OFF && C::ELIM), "trajectory form: SchedLdl family");
   constexpr int NN = G::NN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  constexpr int WB =
-      (has_cldl<C>() || PIPE) ? G::WAVE_BYTES_X : (TRAJ ? G::WAVE_BYTES_T : G::WAVE_BYTES);
+  constexpr int WB = TRAJ ? G::WAVE_BYTES_T : G::WAVE_BYTES;
   unsigned char* wbase = smem_raw + w * WB;
   const unsigned wlds = (unsigned)(uintptr_t)wbase;  // LDS byte address (wave-uniform)
   double* tile = reinterpret_cast<double*>(wbase + G::OFF_T) + g * kLdsTile;
-  double* tileX = reinterpret_cast<double*>(wbase + G::OFF_X) + g * kLdsTile;
   const double* imQ = reinterpret_cast<const double*>(wbase + G::OFF_Q + g * G::IMGM);
   const double* imA = reinterpret_cast<const double*>(wbase + G::OFF_A + g * G::IMGM);
   const double* imT = reinterpret_cast<const double*>(wbase + G::OFF_QT + g * G::IMGM);
@@ -972,7 +872,6 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 
   dma_step(0);
   double Eb[S], H[S], Gb[S];
-  double NXp[S];  // SchedPipe: -QT_{k-1}^-1 + I, queried at the top of step k
   double best = 0.0;
   int tbest = 0;
   const bool fuse_argmin = a.t_max > 0;
@@ -995,15 +894,6 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       }
     }
   };
-  // SchedPipe: query of step k-1 (horizon k), X0 parked in the tile for the
-  // bordered elimination that runs inside the W_k sweep
-  auto pipe_query = [&]() {
-    double Mq[S], X0[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) Mq[i] = Gb[i] - NXp[i];  // QT^-1 + Gbar
-    query_x0_ldl<C, S>(Mq, H, Eb, X0, tile, c, mt, st);
-    lds_put(tile, c, X0);
-  };
   unsigned long long sec[15] = {};
   unsigned long long tprev = 0;
   auto stamp = [&](int j) {
@@ -1018,19 +908,11 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
     stamp(-1);
-    if constexpr (PIPE) {
-      if (k > 0) pipe_query();  // needs no new input: runs before the DMA wait
-      stamp(9);
-    }
     dma_wait();
     wave_sync();
     // J of the previous step is stored only now, so that the vmcnt(0) above
     // never waits on a store issued at the end of the previous step
-    if constexpr (PIPE) {
-      if (k > 1 && valid && c == 0) a.J[prob * N + k - 2] = jprev;  // horizon k-1
-    } else {
-      if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
-    }
+    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = jprev;
     double atil = 0.0;  // trajectory form: a~_k = a_k - B_k du_k (augmented.py:50)
     if constexpr (TRAJ) {
       // build the last row / column and the diagonal of Q_aug[k] (augmented.py:31-47)
@@ -1114,7 +996,6 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     stamp(0);
     neg_inverse2<C, S, S, S>(NE, imQ, NX, imT, c, mt, st);
     stamp(1);
-    if constexpr (has_cldl<C>()) lds_put(tileX, c, NX);  // own column, read back at the query
     double at[S], brow[MM];
     if constexpr (TRAJ) {  // row c of A_aug = [[A_k, a~],[0, 1]], B_aug = [[B_k],[0]]
       const double* sA = reinterpret_cast<const double*>(wbase + G::OFF_A) + g * 2 * G::CHA;
@@ -1137,24 +1018,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     // offset form: NE, NX, NW carry +I; a product -(N + I) Y = (-N) Y - Y starts from Y
     double F[S];
     if constexpr (OFF) copy(F, at); else zero(F);
-    double Mr[S];  // has_cldl: M = E_k + Gbar_{k-1}, eliminated in pass 1
-    double dminM = 1.0;
-    if (has_cldl<C>() && k > 0) {
-#pragma unroll
-      for (int i = 0; i < S; ++i) Mr[i] = Gb[i] - NE[i];  // E_k + Gbar - I (offset form)
-      lds_put(tile, c, Mr);
-      diag_add<S, kLdsRow>(tile, c, 1e-9);
-      wave_sync();
-      sym_from<C, S, kLdsRow>(tile, c, Mr);
-      // pass 1 pivots interleaved with the rows of F = E A^T (independent work)
-      static_for<S>([&](auto P) {
-        elim_pivot_off<C, S, P>(Mr, dminM);
-        if constexpr (P == 0) LaneDot<S>::fma_neg(F[P], NE[P], at);
-        else LaneDot<S>::fma_negq(F[P], NE[P], at);
-      });
-    } else {
-      gxy<C, true>(F, NE, at);    // F = E A^T
-    }
+    gxy<C, true>(F, NE, at);    // F = E A^T
     double Gk[S];
     zero(Gk);
     gxty<C, false>(Gk, at, F);  // A F
@@ -1180,46 +1044,11 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
         }
       }
       copy(Gb, Gk);
-    } else if constexpr (has_cldl<C>()) {
-      const bool ok0 = elim_ok(Mr, dminM);
-      if (__any(!ok0)) {  // chol_inv ladder on M alone (utils.py:69-93)
-        double eps = ok0 ? 1e-9 : 1e-8, cur = 1e-9;
-        int tries = ok0 ? 0 : 1;
-        bool done = ok0;
-        if (!ok0) st |= ST_JITTER;
-#pragma unroll 1
-        while (true) {
-          diag_add<S, kLdsRow>(tile, c, eps - cur);
-          cur = eps;
-          sym_from<C, S, kLdsRow>(tile, c, Mr);
-          double dm = 1.0;
-          static_for<S>([&](auto P) { elim_pivot_off<C, S, P>(Mr, dm); });
-          const bool ok = elim_ok(Mr, dm);
-          const bool last = tries >= mt;
-          if (!done && !ok && last) st |= ST_LU;
-          done = done || ok || last;
-          if (!__any(!done)) break;
-          if (!done) {
-            eps *= 10.0;
-            ++tries;
-          }
-        }
-      }
-      wave_sync();
-      stamp(4);
-      copy(Gb, Gk);
-      compose_pass2<C, S>(Mr, H, F, Eb, Gb);
     } else {
       double NW[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) NW[i] = Gb[i] - NE[i];  // E_k + Gbar
-      if constexpr (PIPE) {  // NW = -W, and J(k) = 1/2 z0^T X0_{k-1}^-1 z0 alongside
-        const double jk = 0.5 * neg_inverse_and_quad<C, S>(NW, tileX, tile, c, mt, st, -1.0);
-        take_j(k, jk);
-        jprev = jk;
-      } else {
-        neg_inverse_reg<C, S>(NW, tile, c, mt, st, -1.0);     // NW = -W
-      }
+      neg_inverse_reg<C, S>(NW, tile, c, mt, st, -1.0);     // NW = -W
       stamp(4);
       double Z[S];
       if constexpr (OFF) copy(Z, H); else zero(Z);
@@ -1235,15 +1064,6 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     stamp(5);
 
     // ---- query horizon t = k + 1
-    if constexpr (PIPE) {  // deferred to the top of step k + 1 (or after the loop)
-      copy(NXp, NX);
-      load_rows();
-      continue;
-    }
-    if constexpr (has_cldl<C>()) {
-#pragma unroll
-      for (int i = 0; i < S; ++i) NX[i] = tileX[i * kLdsRow + c];
-    }
 #pragma unroll
     for (int i = 0; i < S; ++i) NX[i] = Gb[i] - NX[i];   // QT^-1 + Gbar
     if constexpr (has_qldl<C>()) {
@@ -1276,19 +1096,6 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
     jprev = jk;
   }
   dma_wait();
-  if constexpr (PIPE) {  // the last query (horizon N) has no W sweep to ride in
-    if (N > 0) {
-      if (N > 1 && valid && c == 0) a.J[prob * N + N - 2] = jprev;
-      pipe_query();
-      double X0[S];
-      wave_sync();
-#pragma unroll
-      for (int i = 0; i < S; ++i) X0[i] = tile[i * kLdsRow + c];
-      const double jk = 0.5 * quad_inverse<C, S>(X0, tile, c, mt, st);
-      take_j(N, jk);
-      jprev = jk;
-    }
-  }
   if constexpr (C::STAMP) {
     if (lane == 0) {
       for (int j = 0; j < 15; ++j) atomicAdd(&g_hop_stamp[j], sec[j]);
@@ -2174,21 +1981,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     if (variant == 8) return go(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes);
     if (variant == 10) return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
     if (variant == 12) return go(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes);
-    if (variant == 16)
-      return go(v2::lft_sweep_v2_kernel<v2::SchedLdl2, 13, 4>,
-                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
-    if (variant == 22)
-      return go(v2::lft_sweep_v2_kernel<v2::SchedLdl2Stamped, 13, 4>,
-                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
     if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
-    if (variant == 26)
-      return go(v2::lft_sweep_v2_kernel<v2::SchedPipe, 13, 4>,
-                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
     if (variant == 30) return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes);
     if (variant == 32) return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDmaStamped, 13, 4>, bytes);
-    if (variant == 28)
-      return go(v2::lft_sweep_v2_kernel<v2::SchedPipeStamped, 13, 4>,
-                v2::Geo<13, 4>::WAVE_BYTES_X * kWavesPerBlock);
     if (variant == 14) return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
     return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes);
   }
