@@ -230,6 +230,53 @@ int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float
                     int64_t batch, int32_t n_alloc, int32_t n, int32_t m, float* K, float* k,
                     float* Vxx, float* Vx, float* V0, int32_t* status, void* stream);
 
+/*
+ * Batched dynamics and finite-difference linearisation.
+ * System ids (the reference's systems.py makers, F discretised with the given dt):
+ *   0 double integrator  make_double_integrator     systems.py:28-50    n=2,  m=1
+ *   1 cart-pole          make_cartpole_swingup      systems.py:57-112   n=4,  m=1
+ *   2 quadrotor          make_quadrotor             systems.py:119-230  n=12, m=4
+ *   3 point mass         make_pointmass_navigation  systems.py:237-296  n=4,  m=2
+ *   4 segway             make_segway_balance        systems.py:303-349  n=4,  m=1
+ * hop_system_dims writes n and m of a system id (either pointer may be NULL).
+ */
+#define HOP_SYS_DOUBLE_INTEGRATOR 0
+#define HOP_SYS_CARTPOLE 1
+#define HOP_SYS_QUADROTOR 2
+#define HOP_SYS_POINTMASS 3
+#define HOP_SYS_SEGWAY 4
+int hop_system_dims(int32_t system, int32_t* n, int32_t* m);
+
+/*
+ * hop_linearize_f64
+ * Replaces linearize_forward_diff_traj(F, X, U, epsx, epsu, relx, relu)
+ *            /root/reference/linearization.py:216-262   (central = 0)
+ *      and linearize_central_diff_traj(F, X, U, epsx, epsu, relx, relu)
+ *            /root/reference/linearization.py:177-211   (central = 1)
+ *      plus compute_affine_residuals(F, X, U)  linearization.py:269-270
+ * for a batch of trajectories, steps k < n_use (len(U) in the reference).
+ *   X [batch][n_alloc+1][n]   U [batch][n_alloc][m]
+ *   A [batch][n_alloc][n][n]  Bm [batch][n_alloc][n][m]  (the layout hop_augment_*,
+ *      hop_lft_sweep_traj_* and hop_riccati_* read)
+ *   a_res [batch][n_alloc][n] = F(x_k, u_k) - x_{k+1} (nullable)
+ *   Fx    [batch][n_alloc][n] = F(x_k, u_k)          (nullable)
+ *   h = max(eps, rel * max(1, |v|)) per entry (reference defaults 1e-5 / 1e-6);
+ *   forward differences give an all-NaN (A_k, B_k) when F(x_k, u_k) is not finite.
+ */
+int hop_linearize_f64(int32_t system, double dt, const double* X, const double* U,
+                      int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                      double epsx, double epsu, double relx, double relu, double* A,
+                      double* Bm, double* a_res, double* Fx, void* stream);
+
+/*
+ * hop_dynamics_f64
+ * Replaces F(x, u) of the systems above (one discrete step) for `count`
+ * independent pairs: Xn[q] = F(X[q], U[q]), rows `*_stride` elements apart.
+ */
+int hop_dynamics_f64(int32_t system, double dt, const double* X, int64_t x_stride,
+                     const double* U, int64_t u_stride, int64_t count, double* Xn,
+                     int64_t xn_stride, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -293,6 +293,51 @@ def traj_real(tag, maker_kwargs, maker, T_min=None, T_max=None, S_window=20):
     print(f"traj_real_{tag}: N={N} T*={int(np.argmin(props[0][T_min - 1:T_max]) + T_min)}")
 
 
+LIN_SYSTEMS = {  # system id of hop_linearize_f64 -> reference maker (systems.py)
+    "di": (0, "make_double_integrator"),
+    "cartpole": (1, "make_cartpole_swingup"),
+    "quadrotor": (2, "make_quadrotor"),
+    "pointmass": (3, "make_pointmass_navigation"),
+    "segway": (4, "make_segway_balance"),
+}
+
+
+def lin_golden(name, N, seed, scale):
+    """Dynamics F and both finite-difference linearisations of the reference
+    (linearization.py:177-270) plus compute_affine_residuals on a seeded random
+    trajectory around the system's x0 / u_ref.  The quadrotor capture also holds
+    states that trip each NaN guard of its F (systems.py:170-195)."""
+    _, maker = LIN_SYSTEMS[name]
+    F, x0, xg, u_ref, *_ = getattr(ref_systems, maker)()
+    rng = np.random.default_rng(seed)
+    n, m = len(x0), len(u_ref)
+    X = x0 + scale * rng.standard_normal((N + 1, n))
+    U = u_ref + scale * rng.standard_normal((N, m))
+    if name == "quadrotor":
+        X[3, 7] = np.pi / 2 - 5e-4      # |cos(pitch)| < 1e-3
+        X[5, 10] = 2e3                  # |omega| > 1e3
+        X[7, 0] = 2e6                   # ||x|| > 1e6
+        X[9, 2] = np.nan                # non-finite state
+        U[11, 1] = np.inf               # non-finite control
+    Fx = np.array([F(X[k], U[k]) for k in range(N)])
+    Af, Bf = ref_lin.linearize_forward_diff_traj(F, X, U)
+    Ac, Bc = ref_lin.linearize_central_diff_traj(F, X, U)
+    a_res = np.array([r.ravel() for r in ref_lin.compute_affine_residuals(F, X, U)])
+    np.savez_compressed(os.path.join(HERE, f"lin_{name}.npz"), X=X, U=U, dt=float(F.dt),
+                        Fx=Fx, A_fwd=np.array(Af), B_fwd=np.array(Bf), A_cen=np.array(Ac),
+                        B_cen=np.array(Bc), a_res=a_res)
+    print(f"lin_{name}: n={n} m={m} N={N}")
+
+
+def main_lin():
+    np.seterr(all="ignore")
+    lin_golden("di", 20, 9000, 0.5)
+    lin_golden("cartpole", 20, 9001, 1.5)
+    lin_golden("quadrotor", 24, 9002, 0.4)
+    lin_golden("pointmass", 20, 9003, 0.7)
+    lin_golden("segway", 20, 9004, 0.8)
+
+
 def main_traj():
     np.seterr(all="ignore")
     traj_synth("n12_m4_N100", 12, 4, 100, [8000, 8001, 8002, 8003], [1.0, 1.0, 1e-12, 1e-12])
@@ -321,6 +366,9 @@ def main():
 if __name__ == "__main__":
     if "--traj" in sys.argv:  # only the trajectory-form fixtures
         main_traj()
+    elif "--lin" in sys.argv:  # only the dynamics / linearisation fixtures
+        main_lin()
     else:
         main()
         main_traj()
+        main_lin()

@@ -56,6 +56,11 @@ SIGNATURES = {
     "hop_lft_sweep_traj_f32": (C.c_int, _TRJ32 + _TRAJ_TAIL),
     "hop_riccati_f64": (C.c_int, _RIC64),
     "hop_riccati_f32": (C.c_int, _RIC32),
+    "hop_system_dims": (C.c_int, [_I32, _P, _P]),
+    "hop_linearize_f64": (C.c_int, [_I32, C.c_double, _P, _P, _I64, _I32, _I32, _I32,
+                                    C.c_double, C.c_double, C.c_double, C.c_double, _P, _P, _P,
+                                    _P, _P]),
+    "hop_dynamics_f64": (C.c_int, [_I32, C.c_double, _P, _I64, _P, _I64, _I64, _P, _I64, _P]),
 }
 
 _lock = threading.Lock()

@@ -16,9 +16,9 @@ CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
 SOURCES = ["capi.hip", "augment.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "lft_small_noslp.hip",
-           "riccati.hip"]
+           "riccati.hip", "linearize.hip"]
 EXTRA = {"lft_small_noslp.hip": ["-fno-slp-vectorize"]}
-HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp", "wrap.hpp"]
+HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp", "wrap.hpp", "dynamics.hpp"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",
          "-Wno-unused-but-set-variable"]

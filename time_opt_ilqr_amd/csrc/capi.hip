@@ -7,6 +7,7 @@
 #include "../../include/hop.h"
 #include "hop_device.hpp"
 #include "hop_kernels.hpp"
+#include "dynamics.hpp"
 
 namespace {
 
@@ -378,6 +379,49 @@ int hop_lft_sweep_traj_f32(const float* A, const float* Bm, const float* a_res, 
                        qxx_extra, qx_extra, c_extra, wrap_mask, q_reg, rho_reg, n, m),
       R_inv, r_bs, batch, n_alloc, n_use, max_tries, t_min, t_max, J, status, t_star, j_star,
       workspace, workspace_bytes, stream);
+}
+
+int hop_system_dims(int32_t system, int32_t* n, int32_t* m) {
+  if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
+  if (n) *n = hop::dyn::state_dim(system);
+  if (m) *m = hop::dyn::control_dim(system);
+  return HOP_OK;
+}
+
+int hop_linearize_f64(int32_t system, double dt, const double* X, const double* U,
+                      int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                      double epsx, double epsu, double relx, double relu, double* A,
+                      double* Bm, double* a_res, double* Fx, void* stream) {
+  if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (n_use > n_alloc) return fail(HOP_E_ARG, "n_use > n_alloc");
+  if (central != 0 && central != 1) return fail(HOP_E_ARG, "central must be 0 or 1");
+  if (batch == 0 || n_use <= 0) return HOP_OK;
+  if (!X || !U || !A || !Bm) return fail(HOP_E_ARG, "null input/output pointer");
+  if (batch * (int64_t)n_use > (int64_t)0xffffffffLL * 64)
+    return fail(HOP_E_SIZE, "batch * n_use too large for one launch");
+  hop::LinArgs a{};
+  a.sys = system; a.central = central; a.dt = dt;
+  a.epsx = epsx; a.epsu = epsu; a.relx = relx; a.relu = relu;
+  a.X = X; a.U = U; a.batch = batch; a.nalloc = n_alloc; a.nuse = n_use;
+  a.A = A; a.B = Bm; a.a_res = a_res; a.Fx = Fx;
+  return hip_status(hop::dispatch_linearize(a, (hipStream_t)stream));
+}
+
+int hop_dynamics_f64(int32_t system, double dt, const double* X, int64_t x_stride,
+                     const double* U, int64_t u_stride, int64_t count, double* Xn,
+                     int64_t xn_stride, void* stream) {
+  if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
+  if (count < 0) return fail(HOP_E_ARG, "count < 0");
+  if (count == 0) return HOP_OK;
+  if (!X || !U || !Xn) return fail(HOP_E_ARG, "null input/output pointer");
+  const int n = hop::dyn::state_dim(system), m = hop::dyn::control_dim(system);
+  if (x_stride < n || u_stride < m || xn_stride < n) return fail(HOP_E_ARG, "row stride too small");
+  if (count > (int64_t)0xffffffffLL * 256) return fail(HOP_E_SIZE, "count too large for one launch");
+  hop::DynArgs a{};
+  a.sys = system; a.dt = dt; a.X = X; a.U = U; a.Xn = Xn;
+  a.count = count; a.x_stride = x_stride; a.u_stride = u_stride; a.xn_stride = xn_stride;
+  return hip_status(hop::dispatch_dynamics(a, (hipStream_t)stream));
 }
 
 }  // extern "C"

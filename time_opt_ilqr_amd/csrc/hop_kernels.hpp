@@ -92,6 +92,34 @@ struct RiccatiArgs {
   int* status;  // [B]
 };
 
+// batched finite-difference linearisation (linearize.hip, dynamics.hpp)
+struct LinArgs {
+  int sys;              // hop::dyn::System
+  int central;          // 0 forward differences, 1 central
+  double dt, epsx, epsu, relx, relu;
+  const double* X;      // [B][nalloc+1][n]
+  const double* U;      // [B][nalloc][m]
+  long long batch;
+  int nalloc, nuse;
+  double* A;            // [B][nalloc][n][n]
+  double* B;            // [B][nalloc][n][m]
+  double* a_res;        // [B][nalloc][n] or null
+  double* Fx;           // [B][nalloc][n] or null
+};
+
+// batched dynamics step x' = F(x, u) (row strides in elements)
+struct DynArgs {
+  int sys;
+  double dt;
+  const double* X;
+  const double* U;
+  double* Xn;
+  long long count, x_stride, u_stride, xn_stride;
+};
+
+hipError_t dispatch_linearize(const LinArgs& a, hipStream_t stream);
+hipError_t dispatch_dynamics(const DynArgs& a, hipStream_t stream);
+
 template <class T>
 hipError_t dispatch_lft(const LftArgs<T>& a, hipStream_t stream);
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream);

@@ -351,3 +351,88 @@ def propagate_traj(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, *, wrap_idx=No
         ws.record_stream(torch.cuda.current_stream(dev))
     del keep
     return SweepResult(J, status, ts, js)
+
+
+# ---- batched dynamics + finite-difference linearisation
+
+SYSTEM_IDS = {"double_integrator": 0, "di": 0, "cartpole": 1, "quadrotor": 2, "pointmass": 3,
+              "segway": 4}
+
+
+def system_dims(system) -> tuple:
+    """(n, m) of a system id or name (hop_system_dims)."""
+    sid = system_id(system)
+    n, m = _lib.C.c_int32(), _lib.C.c_int32()
+    _lib.check(_lib.load().hop_system_dims(sid, _lib.C.byref(n), _lib.C.byref(m)))
+    return n.value, m.value
+
+
+def system_id(system) -> int:
+    if isinstance(system, str):
+        if system not in SYSTEM_IDS:
+            raise ValueError(f"unknown system {system!r} (one of {sorted(SYSTEM_IDS)})")
+        return SYSTEM_IDS[system]
+    sid = getattr(system, "system_id", system)
+    if not isinstance(sid, int) or not 0 <= sid < 5:
+        raise ValueError(f"unknown system id {system!r}")
+    return sid
+
+
+@dataclass
+class Linearization:
+    A: "object"       # [B, N, n, n]
+    B: "object"       # [B, N, n, m]
+    a_res: "object"   # [B, N, n]  F(x_k, u_k) - x_{k+1}
+    Fx: "object" = None  # [B, N, n] F(x_k, u_k) (want_fx=True)
+
+
+def linearize(system, X, U, dt: float, *, central: bool = False, n_use: Optional[int] = None,
+              epsx: float = 1e-5, epsu: float = 1e-5, relx: float = 1e-6, relu: float = 1e-6,
+              want_fx: bool = False) -> Linearization:
+    """Batched linearize_{forward,central}_diff_traj + compute_affine_residuals
+    (linearization.py:177-270) for X [B, N+1, n], U [B, N, m] (fp64, on the
+    device).  Steps k < n_use (default N) are written; A / B / a_res come out in
+    the layout augment / propagate_traj / riccati read."""
+    torch = _torch()
+    sid = system_id(system)
+    n, m = system_dims(sid)
+    X = _dev(X, "X", torch.float64)
+    U = _dev(U, "U", torch.float64, X.device)
+    if X.dim() == 2:
+        X, U = X[None], U[None]
+    if X.dim() != 3 or U.dim() != 3 or X.shape[-1] != n or U.shape[-1] != m:
+        raise ValueError(f"X must be [B, N+1, {n}] and U [B, N, {m}] for system {sid}")
+    Bn, N = U.shape[0], U.shape[1]
+    if X.shape[0] != Bn or X.shape[1] != N + 1:
+        raise ValueError("X must hold N+1 states per problem (len(U) + 1)")
+    n_use = N if n_use is None else int(n_use)
+    if n_use > N:
+        raise IndexError(f"n_use={n_use} exceeds the {N} steps supplied")
+    dev = X.device
+    A = torch.empty((Bn, N, n, n), dtype=torch.float64, device=dev)
+    Bm = torch.empty((Bn, N, n, m), dtype=torch.float64, device=dev)
+    a_res = torch.empty((Bn, N, n), dtype=torch.float64, device=dev)
+    Fx = torch.empty((Bn, N, n), dtype=torch.float64, device=dev) if want_fx else None
+    rc = _lib.load().hop_linearize_f64(sid, float(dt), _lib.ptr(X), _lib.ptr(U), Bn, N, n_use,
+                                       int(bool(central)), float(epsx), float(epsu), float(relx),
+                                       float(relu), _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(a_res),
+                                       _lib.ptr(Fx), _lib.stream_handle(dev))
+    _lib.check(rc)
+    return Linearization(A, Bm, a_res, Fx)
+
+
+def dynamics(system, X, U, dt: float):
+    """x' = F(x, u) for X [..., n], U [..., m] (fp64, on the device)."""
+    torch = _torch()
+    sid = system_id(system)
+    n, m = system_dims(sid)
+    X = _dev(X, "X", torch.float64)
+    U = _dev(U, "U", torch.float64, X.device)
+    if X.shape[-1] != n or U.shape[-1] != m or X.shape[:-1] != U.shape[:-1]:
+        raise ValueError(f"X [..., {n}] and U [..., {m}] with the same leading shape expected")
+    cnt = X.numel() // n
+    out = torch.empty_like(X)
+    rc = _lib.load().hop_dynamics_f64(sid, float(dt), _lib.ptr(X), n, _lib.ptr(U), m, cnt,
+                                      _lib.ptr(out), n, _lib.stream_handle(X.device))
+    _lib.check(rc)
+    return out
