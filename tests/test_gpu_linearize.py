@@ -41,7 +41,9 @@ def _close(got, ref, f_tol=2e-15, ab_tol=1e-8, kind="ab"):
     got, ref = np.asarray(got), np.asarray(ref)
     assert got.shape == ref.shape
     assert np.array_equal(np.isnan(got), np.isnan(ref)), "NaN pattern differs"
-    ok = ~np.isnan(ref)
+    # +-inf (e.g. a_res = F(x_k) - x_{k+1} with x_{k+1} = inf) must match exactly
+    assert np.array_equal(got[np.isinf(ref)], ref[np.isinf(ref)]), "inf entries differ"
+    ok = np.isfinite(ref)
     tol = ab_tol if kind == "ab" else f_tol * np.maximum(1.0, np.abs(ref[ok]))
     err = np.abs(got[ok] - ref[ok])
     assert (err <= tol).all(), float(err.max())
