@@ -346,6 +346,76 @@ def main_traj():
     traj_real("Quad_N160", {}, ref_systems.make_quadrotor)
 
 
+ILQR_CASES = [  # (tag, maker, maker kwargs, T_min, T_max, max_iter, central)
+    ("di", "make_double_integrator", dict(N=50), 10, 50, 12, False),
+    ("cartpole", "make_cartpole_swingup", dict(N=120), 20, 110, 4, False),
+    ("quadrotor", "make_quadrotor", dict(N=100), 30, 90, 3, False),
+    ("pointmass", "make_pointmass_navigation", dict(N=120), 30, 110, 4, True),
+    ("segway", "make_segway_balance", dict(N=120), 20, 110, 4, False),
+]
+
+
+def ilqr_capture(tag, maker, maker_kwargs, T_min, T_max, max_iter, central, keep=3):
+    """ilqr_timeopt(method="propagator") end to end (solver.py:449-765), with
+    the first `keep` forward_linesearch_fixedT calls (solver.py:233-286) captured
+    (inputs X, U, T*, k, K and outputs X', U', J, accepted), plus rollout
+    (solver.py:42-62) and cost_timeopt_true (solver.py:65-102) on the final
+    trajectory.  extra_stage_cost (point mass obstacles) is passed through."""
+    F, x0, xg, u_ref, Q, R, alpha, w, N, _, _, wrap_idx, extra = \
+        getattr(ref_systems, maker)(**maker_kwargs)
+    esc = extra["extra_stage_cost"] if extra else None
+    calls = []
+    real_fwd = ref_solver.forward_linesearch_fixedT
+
+    def fwd_spy(F_, X, U, xg_, u_ref_, Q_, R_, alpha_, w_, T_star, k_list, K_list, **kw):
+        out = real_fwd(F_, X, U, xg_, u_ref_, Q_, R_, alpha_, w_, T_star, k_list, K_list, **kw)
+        if len(calls) < keep:
+            calls.append(dict(X=np.array(X), U=np.array(U), T_star=int(T_star),
+                              k=np.array(k_list).reshape(len(k_list), -1),
+                              K=np.array(K_list), X_new=np.array(out[0]),
+                              U_new=np.array(out[1]), J=float(out[2]), acc=bool(out[3])))
+        return out
+
+    ref_solver.forward_linesearch_fixedT = fwd_spy
+    try:
+        sol = ref_solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max,
+                                      method="propagator", max_iter=max_iter,
+                                      wrap_idx=wrap_idx, use_central_diff=central,
+                                      extra_stage_cost=esc)
+    finally:
+        ref_solver.forward_linesearch_fixedT = real_fwd
+    U0 = np.tile(np.asarray(u_ref, dtype=float).reshape(1, -1), (N, 1))
+    d = dict(N=N, T_min=T_min, T_max=T_max, max_iter=max_iter, central=int(central),
+             dt=float(F.dt), x0=x0, xg=xg, u_ref=u_ref, Q=Q, R=R,
+             Qf=ref_utils.as_terminal_weight(alpha, len(x0)), w=w,
+             wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64),
+             X0=ref_solver.rollout(F, x0, U0), X=sol["X"], U=sol["U"],
+             J_hist=np.array(sol["J_hist"]), T_hist=np.array(sol["T_hist"]),
+             T_star=int(sol["T_star"]), n_fwd=len(calls))
+    for i, c in enumerate(calls):
+        for key, v in c.items():
+            d[f"f{i}_{key}"] = v
+    # cost_timeopt_true on the final trajectory at a few horizons
+    Ts = np.array([1, T_min, int(sol["T_star"]), T_max])
+    d["cost_T"] = Ts
+    d["cost_J"] = np.array([ref_solver.cost_timeopt_true(sol["X"], sol["U"], xg, u_ref, Q, R,
+                                                         alpha, w, int(T), wrap_idx, esc)
+                            for T in Ts])
+    # rollout with a blow-up: controls scaled until the state norm guard trips
+    Ubig = sol["U"] * 1e4
+    d["U_big"] = Ubig
+    d["X_big"] = ref_solver.rollout(F, x0, Ubig, max_state_norm=1e3)
+    np.savez_compressed(os.path.join(HERE, f"ilqr_{tag}.npz"), **d)
+    print(f"ilqr_{tag}: T*={sol['T_star']} J_hist={sol['J_hist']} T_hist={sol['T_hist']} "
+          f"fwd captured={len(calls)}")
+
+
+def main_ilqr():
+    np.seterr(all="ignore")
+    for case in ILQR_CASES:
+        ilqr_capture(*case)
+
+
 def main():
     np.seterr(all="ignore")
     synthetic_lft("s13_m4_N100", 13, 4, 100, 1000, 4, 40, 100)
@@ -368,7 +438,10 @@ if __name__ == "__main__":
         main_traj()
     elif "--lin" in sys.argv:  # only the dynamics / linearisation fixtures
         main_lin()
+    elif "--ilqr" in sys.argv:  # only the forward line search / outer loop fixtures
+        main_ilqr()
     else:
         main()
         main_traj()
         main_lin()
+        main_ilqr()
