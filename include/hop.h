@@ -277,6 +277,92 @@ int hop_dynamics_f64(int32_t system, double dt, const double* X, int64_t x_strid
                      const double* U, int64_t u_stride, int64_t count, double* Xn,
                      int64_t xn_stride, void* stream);
 
+/*
+ * Forward pass and outer-loop bookkeeping of ilqr_timeopt.
+ * Cost parameters shared by the entry points below (device pointers, each with a
+ * batch stride in elements: 0 = one block shared by the whole batch):
+ *   xg [n], u_ref [m], Q [n][n], R [m][m], Qf [n][n] = as_terminal_weight(alpha)
+ *   (utils.py:49-62), w [1] (the time weight), obstacles [n_obs][4] =
+ *   (cx, cy, radius, weight) of the point-mass extra_stage_cost
+ *   (systems.py:271-293; NULL / 0 for none), wrap_mask = bit i for wrap_idx i.
+ */
+
+/*
+ * hop_rollout_f64
+ * Replaces rollout(F, x0, U, max_state_norm)  /root/reference/solver.py:42-62
+ *   x0 [batch or 1][n] (x0_batch_stride 0 or n), U [batch][N][m] -> X [batch][N+1][n];
+ *   the first step whose state is not finite or has ||x|| > max_state_norm sets
+ *   X[k+1:] = NaN.
+ */
+int hop_rollout_f64(int32_t system, double dt, const double* x0, int64_t x0_batch_stride,
+                    const double* U, int64_t batch, int32_t N, double max_state_norm, double* X,
+                    void* stream);
+
+/*
+ * hop_cost_true_f64
+ * Replaces cost_timeopt_true(X, U, xg, u_ref, Q, R, alpha, w, T_star, wrap_idx,
+ *          extra_stage_cost)  /root/reference/solver.py:65-102
+ *   X [batch][N+1][n], U [batch][N][m], T_star [batch] -> J [batch]
+ *   (+inf for T* <= 0 or non-finite data, NaN for T* > N where the reference
+ *   would raise IndexError).
+ */
+int hop_cost_true_f64(int32_t system, const double* X, const double* U, const int32_t* T_star,
+                      const double* xg, int64_t xg_bs, const double* u_ref, int64_t ur_bs,
+                      const double* Q, int64_t q_bs, const double* R, int64_t r_bs,
+                      const double* Qf, int64_t qf_bs, const double* w, int64_t w_bs,
+                      const double* obstacles, int32_t n_obs, uint32_t wrap_mask, int64_t batch,
+                      int32_t N, double* J, void* stream);
+
+/*
+ * hop_forward_linesearch_f64
+ * Replaces forward_linesearch_fixedT(F, X, U, xg, u_ref, Q, R, alpha, w, T_star,
+ *          k_list, K_list, alphas, wrap_idx, extra_stage_cost)
+ *          /root/reference/solver.py:233-286
+ *   K [batch][N][m][n], k [batch][N][m] (hop_riccati_f64 mode 0 output),
+ *   alphas: HOST array of n_alpha <= 8 step sizes (reference (1, .5, .25, .1, .05)),
+ *   active [batch] nullable (0 = skip: X' = X, U' = U, accepted = -2).
+ *   Out: X_new [batch][N+1][n], U_new [batch][N][m], J [batch] (the accepted J'
+ *   or J_old), J_old [batch], accepted [batch] = index of the accepted alpha or -1.
+ *   workspace: hop_forward_workspace_bytes(system, batch, N, n_alpha) bytes.
+ */
+size_t hop_forward_workspace_bytes(int32_t system, int64_t batch, int32_t N, int32_t n_alpha);
+int hop_forward_linesearch_f64(int32_t system, double dt, const double* X, const double* U,
+                               const double* xg, int64_t xg_bs, const double* u_ref,
+                               int64_t ur_bs, const double* Q, int64_t q_bs, const double* R,
+                               int64_t r_bs, const double* Qf, int64_t qf_bs, const double* w,
+                               int64_t w_bs, const double* obstacles, int32_t n_obs,
+                               uint32_t wrap_mask, const int32_t* T_star, const int32_t* active,
+                               const double* K, const double* k, const double* alphas,
+                               int32_t n_alpha, int64_t batch, int32_t N, void* workspace,
+                               size_t workspace_bytes, double* X_new, double* U_new, double* J,
+                               double* J_old, int32_t* accepted, void* stream);
+
+/*
+ * hop_obstacle_cost_f64
+ * Replaces the point-mass extra_stage_cost(x, u) -> (c, cx, cxx)
+ *          /root/reference/systems.py:271-293
+ * for `count` states X[r * x_stride + 0..n-1]: c [count], cx [count][n],
+ * cxx [count][n][n] (each nullable).  Feeds qxx_extra / qx_extra / c_extra of
+ * hop_augment_* / hop_lft_sweep_traj_* / hop_riccati_*.
+ */
+int hop_obstacle_cost_f64(const double* X, int64_t x_stride, int64_t count, int32_t n,
+                          const double* obstacles, int32_t n_obs, double* c, double* cx,
+                          double* cxx, void* stream);
+
+/*
+ * hop_ilqr_accept_f64
+ * The accept / LM / stop-rule step of ilqr_timeopt  /root/reference/solver.py:737-752
+ * (warm = 1: the warm-start record of solver.py:548-553) per problem:
+ *   accepted (hop_forward_linesearch_f64) >= 0 and J finite -> T_bar = T_star,
+ *   append (J, T_star) to J_hist/T_hist [batch][hist_cap], lm = max(lm/10, 1e-12);
+ *   else lm *= 10.  done = 1 once |dJ|/(|J|+1e-12) < 1e-4 over the last two records
+ *   and the last three T are equal.  Problems with done = 1 are left untouched.
+ */
+int hop_ilqr_accept_f64(int64_t batch, int32_t warm, const double* J, const int32_t* accepted,
+                        const int32_t* T_star, double* lm, int32_t* T_bar, double* J_hist,
+                        int32_t* T_hist, int32_t* n_hist, int32_t hist_cap, int32_t* done,
+                        void* stream);
+
 #ifdef __cplusplus
 }
 #endif

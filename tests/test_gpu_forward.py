@@ -1,0 +1,242 @@
+"""GPU parity of the forward pass and the device outer loop (forward.hip,
+solver.py) against the reference's own captures (tests/golden/ilqr_*.npz,
+make_golden.py --ilqr) and the oracle (oracle/ilqr_oracle.py, pinned by them).
+
+Tolerances (written where they are used):
+  * J (true cost): 1e-12 relative -- the kernel's dot products run as fma
+    chains where NumPy hands them to BLAS, so the last bits differ;
+  * X', U' of an accepted step: 1e-12 relative to the trajectory's scale
+    (bit-exact dynamics for DI / point mass / segway, ocml trig for the others);
+  * whole outer loop: the same T_hist and accepted iterations, J_hist to 1e-9
+    relative (each iteration re-linearises, so 1e-16 differences compound).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import dyn_oracle as dyn
+from oracle import ilqr_oracle as io
+
+pytestmark = pytest.mark.gpu
+
+TAGS = ["di", "cartpole", "quadrotor", "pointmass", "segway"]
+
+
+def _t(x, dev):
+    import torch
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _rel(got, ref):
+    got, ref = np.asarray(got, float), np.asarray(ref, float)
+    return float(np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-300))
+
+
+def _case(golden_dir, tag):
+    d = np.load(os.path.join(golden_dir, f"ilqr_{tag}.npz"))
+    obs = None
+    if tag == "pointmass":
+        from time_opt_ilqr_amd.systems import OBSTACLES
+        obs = np.array([[o[0], o[1], r, wt] for o, r, wt in OBSTACLES])
+    return d, dyn.SYSTEMS[tag], [int(i) for i in d["wrap_idx"]], obs
+
+
+def _cost(d, wrap, obs, dev):
+    from time_opt_ilqr_amd import engine
+    return engine.CostParams(_t(d["xg"], dev), _t(d["u_ref"], dev), _t(d["Q"], dev),
+                             _t(d["R"], dev), _t(d["Qf"], dev), float(d["w"]),
+                             None if obs is None else _t(obs, dev), wrap)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_forward_linesearch_vs_reference_captures(dev, golden_dir, tag):
+    """every captured forward_linesearch_fixedT call, batched into one launch"""
+    from time_opt_ilqr_amd import engine
+    d, sid, wrap, obs = _case(golden_dir, tag)
+    nf = int(d["n_fwd"])
+    N = int(d["N"])
+    n, m = dyn.DIMS[sid]
+    g = lambda i, k: d[f"f{i}_{k}"]  # noqa: E731
+    X = np.stack([g(i, "X") for i in range(nf)])
+    U = np.stack([g(i, "U") for i in range(nf)])
+    T = [int(g(i, "T_star")) for i in range(nf)]
+    K = np.zeros((nf, N, m, n))
+    k = np.zeros((nf, N, m))
+    for i in range(nf):
+        K[i, :T[i]] = g(i, "K")
+        k[i, :T[i]] = g(i, "k")
+    r = engine.forward_linesearch(sid, _t(X, dev), _t(U, dev), T, _t(K, dev), _t(k, dev),
+                                  _cost(d, wrap, obs, dev), float(d["dt"]))
+    acc = _np(r.accepted)
+    for i in range(nf):
+        assert (acc[i] >= 0) == bool(g(i, "acc")), (i, acc[i])
+        Jr = float(g(i, "J"))
+        assert abs(float(r.J[i]) - Jr) <= 1e-12 * max(1.0, abs(Jr))
+        assert _rel(_np(r.X[i]), g(i, "X_new")) <= 1e-12
+        assert _rel(_np(r.U[i]), g(i, "U_new")) <= 1e-12
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_rollout_and_cost_vs_reference(dev, golden_dir, tag):
+    from time_opt_ilqr_amd import engine
+    d, sid, wrap, obs = _case(golden_dir, tag)
+    N, dt = int(d["N"]), float(d["dt"])
+    U0 = np.tile(d["u_ref"].reshape(1, -1), (N, 1))
+    X0 = _np(engine.rollout(sid, _t(d["x0"], dev), _t(U0, dev)[None], dt))[0]
+    assert np.array_equal(np.isnan(X0), np.isnan(d["X0"]))
+    assert _rel(np.nan_to_num(X0), np.nan_to_num(d["X0"])) <= 1e-13
+    Xb = _np(engine.rollout(sid, _t(d["x0"], dev), _t(d["U_big"], dev)[None], dt,
+                            max_state_norm=1e3))[0]
+    assert np.array_equal(np.isnan(Xb), np.isnan(d["X_big"]))
+    Ts = [int(t) for t in d["cost_T"]]
+    B = len(Ts)
+    J = _np(engine.cost_true(sid, _t(np.stack([d["X"]] * B), dev),
+                             _t(np.stack([d["U"]] * B), dev), Ts, _cost(d, wrap, obs, dev)))
+    assert np.all(np.abs(J - d["cost_J"]) <= 1e-12 * np.maximum(1.0, np.abs(d["cost_J"])))
+
+
+def test_cost_edge_cases(dev, golden_dir):
+    """T* <= 0 -> inf, non-finite data -> inf, T* > N -> NaN (reference: IndexError)"""
+    from time_opt_ilqr_amd import engine
+    d, sid, wrap, obs = _case(golden_dir, "di")
+    N = int(d["N"])
+    X = np.stack([d["X"]] * 4)
+    U = np.stack([d["U"]] * 4)
+    X[2, 3, 0] = np.nan
+    J = _np(engine.cost_true(sid, _t(X, dev), _t(U, dev), [0, -3, 10, N + 1],
+                             _cost(d, wrap, obs, dev)))
+    assert np.isposinf(J[0]) and np.isposinf(J[1]) and np.isposinf(J[2]) and np.isnan(J[3])
+    J = _np(engine.cost_true(sid, _t(X, dev), _t(U, dev), [2, 3, 2, N], _cost(d, wrap, obs, dev)))
+    assert np.isfinite(J[2])  # the NaN in X[3] is not read at T* = 2
+    ref = io.cost_true(d["X"], d["U"], d["xg"], d["u_ref"], d["Q"], d["R"], d["Qf"],
+                       float(d["w"]), N, wrap)
+    assert abs(J[3] - ref) <= 1e-12 * abs(ref)
+
+
+def test_linesearch_mixed_batch_vs_oracle(dev, golden_dir):
+    """quadrotor, 37 problems (ragged) built from a captured line search with the
+    feed-forward k scaled per problem (x1 .. x300, negated): every step-size index
+    is accepted somewhere, large steps trip the dynamics' NaN guards, negated
+    steps accept nothing; one problem is inactive, one has T* = 0, several have
+    shorter horizons"""
+    import torch
+    from time_opt_ilqr_amd import engine
+    d, sid, wrap, obs = _case(golden_dir, "quadrotor")
+    g = lambda k: d[f"f1_{k}"]  # noqa: E731
+    N, T0 = int(d["N"]), int(g("T_star"))
+    Bn = 37
+    scales = np.array([1, 3, 10, 30, 100, 300, -1, -10, 0.3])
+    sc = scales[np.arange(Bn) % len(scales)]
+    X = np.stack([g("X")] * Bn)
+    U = np.stack([g("U")] * Bn)
+    K = np.zeros((Bn, N, 4, 12))
+    k = np.zeros((Bn, N, 4))
+    K[:, :T0] = g("K")
+    k[:, :T0] = g("k")[None] * sc[:, None, None]
+    T = np.full(Bn, T0)
+    T[3] = 0
+    T[10:14] = [1, 5, T0 // 2, N]
+    active = np.ones(Bn, dtype=np.int32)
+    active[7] = 0
+    r = engine.forward_linesearch(2, _t(X, dev), _t(U, dev), torch.as_tensor(T), _t(K, dev),
+                                  _t(k, dev), _cost(d, wrap, obs, dev), float(d["dt"]),
+                                  active=torch.as_tensor(active))
+    acc = _np(r.accepted)
+    seen = set()
+    for b in range(Bn):
+        if not active[b]:
+            assert acc[b] == -2 and np.array_equal(_np(r.X[b]), X[b], equal_nan=True)
+            continue
+        Xo, Uo, Jo, ok, ai = io.forward_linesearch(2, float(d["dt"]), X[b], U[b], d["xg"],
+                                                   d["u_ref"], d["Q"], d["R"], d["Qf"],
+                                                   float(d["w"]), int(T[b]), k[b], K[b],
+                                                   wrap_idx=wrap)
+        seen.add(ai)
+        assert acc[b] == ai, (b, acc[b], ai)
+        Jg = float(r.J[b])
+        assert abs(Jg - Jo) <= 1e-12 * max(1.0, abs(Jo)) or (np.isinf(Jo) and np.isinf(Jg))
+        assert _rel(_np(r.X[b]), Xo) <= 1e-11
+        assert _rel(_np(r.U[b]), Uo) <= 1e-11
+    assert -1 in seen and 0 in seen and len(seen) >= 4, seen
+
+
+def test_obstacle_cost_kernel(dev):
+    from time_opt_ilqr_amd import engine, systems
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-2.5, 2.5, (3, 17, 4))
+    obs = np.array([[o[0], o[1], r, wt] for o, r, wt in systems.OBSTACLES])
+    c, cx, cxx = engine.obstacle_cost(_t(X, dev), _t(obs, dev))
+    for idx in np.ndindex(3, 17):
+        rc, rcx, rcxx = systems.obstacle_stage_cost(X[idx])
+        assert abs(float(c[idx]) - rc) <= 1e-14 * max(1.0, abs(rc))
+        assert np.allclose(_np(cx[idx]), rcx, rtol=1e-13, atol=1e-15)
+        assert np.allclose(_np(cxx[idx]), rcxx, rtol=1e-13, atol=1e-15)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_ilqr_outer_loop_vs_reference(dev, golden_dir, tag):
+    """solver.ilqr_timeopt (device end to end) against the reference's run"""
+    from time_opt_ilqr_amd import solver, systems
+    d, sid, wrap, obs = _case(golden_dir, tag)
+    mk = list(systems.MAKERS.values())[sid]
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap_idx, extra = mk(N=int(d["N"]))
+    sol = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, int(d["N"]), int(d["T_min"]),
+                              int(d["T_max"]), max_iter=int(d["max_iter"]), wrap_idx=wrap_idx,
+                              use_central_diff=bool(d["central"]),
+                              extra_stage_cost=extra["extra_stage_cost"] if extra else None)
+    # cart-pole: the zero angle weight makes E_k = (Q_k + 1e-9 I)^-1 reach 5e8, so the
+    # compose inverse W has cond ~1e9 and the J curve / gains carry ~1e-9 relative
+    # rounding differences from the reference's LAPACK path (same T* everywhere)
+    tol = 1e-8 if tag == "cartpole" else 1e-9
+    assert sol["T_hist"] == [int(t) for t in d["T_hist"]]
+    assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= tol
+    assert sol["T_star"] == int(d["T_star"])
+    assert _rel(np.nan_to_num(sol["X"]), np.nan_to_num(d["X"])) <= 100 * tol
+
+
+def test_ilqr_batch_mixed_problems_vs_oracle(dev):
+    """a batch of DI problems with different x0: per-problem T_hist / J_hist /
+    stop iteration equal the oracle's scalar runs"""
+    import torch
+    from time_opt_ilqr_amd import solver, systems
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, _ = \
+        systems.make_double_integrator(N=50)
+    rng = np.random.default_rng(2)
+    Bn = 6
+    X0 = x0 + rng.uniform(-1.5, 1.5, (Bn, 2))
+    Qf = np.asarray(io.orc.terminal_weight(alpha, 2))
+    res = solver.ilqr_timeopt_batch(0, X0, xg, u_ref, Q, R, Qf, w, 50, 10, 50, dt=F.dt,
+                                    max_iter=12, use_central_diff=False)
+    nh = _np(res["n_hist"])
+    for b in range(Bn):
+        o = io.ilqr_timeopt(0, F.dt, X0[b], xg, u_ref, Q, R, Qf, w, 50, 10, 50, max_iter=12,
+                            central=False)
+        assert _np(res["T_hist"][b, :nh[b]]).tolist() == o["T_hist"]
+        assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9
+        assert int(res["T_star"][b]) == o["T_star"]
+    assert not bool(torch.as_tensor(res["crashed"]).any())
+
+
+def test_reference_shaped_forward_dropins(dev, golden_dir):
+    from time_opt_ilqr_amd import solver, systems
+    d, sid, wrap, obs = _case(golden_dir, "segway")
+    F = systems.make_segway_balance(N=int(d["N"]))[0]
+    g = lambda k: d[f"f0_{k}"]  # noqa: E731
+    T = int(g("T_star"))
+    Xn, Un, J, acc = solver.forward_linesearch_fixedT(
+        F, g("X"), g("U"), d["xg"], d["u_ref"], d["Q"], d["R"], d["Qf"], float(d["w"]), T,
+        list(g("k")), list(g("K")), wrap_idx=wrap)
+    assert acc == bool(g("acc")) and abs(J - float(g("J"))) <= 1e-12 * abs(float(g("J")))
+    assert _rel(Xn, g("X_new")) <= 1e-12
+    X0 = solver.rollout(F, d["x0"], np.tile(d["u_ref"], (int(d["N"]), 1)))
+    assert _rel(X0, d["X0"]) <= 1e-13
+    Jc = solver.cost_timeopt_true(d["X"], d["U"], d["xg"], d["u_ref"], d["Q"], d["R"], d["Qf"],
+                                  float(d["w"]), int(d["cost_T"][2]), wrap)
+    assert abs(Jc - float(d["cost_J"][2])) <= 1e-12 * abs(float(d["cost_J"][2]))
+    assert solver.cost_timeopt_true(d["X"], d["U"], d["xg"], d["u_ref"], d["Q"], d["R"],
+                                    d["Qf"], float(d["w"]), 0) == float("inf")

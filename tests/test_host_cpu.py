@@ -24,13 +24,13 @@ def lib():
 def _header_functions():
     src = open(os.path.join(REPO, "include", "hop.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(hop_\w+)\s*\(", src,
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t|const char\*)\s+(hop_\w+)\s*\(", src,
                                  flags=re.M)))
 
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 16
+    assert len(names) == 22
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:

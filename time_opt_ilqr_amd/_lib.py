@@ -41,6 +41,8 @@ _TRJ32 = _TRJ64[:19] + [C.c_float, C.c_float]
 _AUG_TAIL = [_I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]
 _TRAJ_TAIL = [_P, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64,
               _P]
+# cost parameters of the forward-pass entries: xg bs u_ref bs Q bs R bs Qf bs w bs obs n_obs wrap
+_COST = [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _U32]
 
 SIGNATURES = {
     "hop_abi_version": (C.c_int, []),
@@ -61,6 +63,16 @@ SIGNATURES = {
                                     C.c_double, C.c_double, C.c_double, C.c_double, _P, _P, _P,
                                     _P, _P]),
     "hop_dynamics_f64": (C.c_int, [_I32, C.c_double, _P, _I64, _P, _I64, _I64, _P, _I64, _P]),
+    "hop_rollout_f64": (C.c_int, [_I32, C.c_double, _P, _I64, _P, _I64, _I32, C.c_double, _P,
+                                  _P]),
+    "hop_cost_true_f64": (C.c_int, [_I32, _P, _P, _P] + _COST + [_I64, _I32, _P, _P]),
+    "hop_forward_workspace_bytes": (C.c_size_t, [_I32, _I64, _I32, _I32]),
+    "hop_forward_linesearch_f64": (C.c_int, [_I32, C.c_double, _P, _P] + _COST +
+                                   [_P, _P, _P, _P, _P, _I32, _I64, _I32, _P, C.c_size_t, _P, _P,
+                                    _P, _P, _P, _P]),
+    "hop_obstacle_cost_f64": (C.c_int, [_P, _I64, _I64, _I32, _P, _I32, _P, _P, _P, _P]),
+    "hop_ilqr_accept_f64": (C.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P,
+                                      _P]),
 }
 
 _lock = threading.Lock()

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
 SOURCES = ["capi.hip", "augment.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "lft_small_noslp.hip",
-           "riccati.hip", "linearize.hip"]
+           "riccati.hip", "linearize.hip", "forward.hip"]
 EXTRA = {"lft_small_noslp.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp", "wrap.hpp", "dynamics.hpp"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")

@@ -424,4 +424,116 @@ int hop_dynamics_f64(int32_t system, double dt, const double* X, int64_t x_strid
   return hip_status(hop::dispatch_dynamics(a, (hipStream_t)stream));
 }
 
+static int cost_args(int32_t system, const double* xg, int64_t xg_bs, const double* u_ref,
+                     int64_t ur_bs, const double* Q, int64_t q_bs, const double* R, int64_t r_bs,
+                     const double* Qf, int64_t qf_bs, const double* w, int64_t w_bs,
+                     const double* obstacles, int32_t n_obs, uint32_t wrap_mask,
+                     hop::CostArgs* c) {
+  if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
+  if (!xg || !u_ref || !Q || !R || !Qf || !w) return fail(HOP_E_ARG, "null cost parameter");
+  if (xg_bs < 0 || ur_bs < 0 || q_bs < 0 || r_bs < 0 || qf_bs < 0 || w_bs < 0)
+    return fail(HOP_E_ARG, "negative batch stride");
+  if (n_obs < 0 || n_obs > 64 || (n_obs > 0 && !obstacles))
+    return fail(HOP_E_ARG, "obstacles: 0 <= n_obs <= 64 rows of (cx, cy, radius, weight)");
+  const int n = hop::dyn::state_dim(system);
+  if (n_obs > 0 && n < 2) return fail(HOP_E_ARG, "obstacles need a planar position (n >= 2)");
+  if (wrap_mask >> n) return fail(HOP_E_ARG, "wrap index out of range");
+  *c = hop::CostArgs{xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs, w, w_bs,
+                     n_obs > 0 ? obstacles : nullptr, n_obs, wrap_mask};
+  return HOP_OK;
+}
+
+int hop_rollout_f64(int32_t system, double dt, const double* x0, int64_t x0_batch_stride,
+                    const double* U, int64_t batch, int32_t N, double max_state_norm, double* X,
+                    void* stream) {
+  if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
+  if (batch < 0 || N < 0 || x0_batch_stride < 0) return fail(HOP_E_ARG, "negative size/stride");
+  if (batch == 0) return HOP_OK;
+  if (!x0 || !X || (N > 0 && !U)) return fail(HOP_E_ARG, "null pointer");
+  hop::RolloutArgs a{dt, x0, x0_batch_stride, U, batch, N, max_state_norm, X};
+  return hip_status(hop::dispatch_forward(system, 0, &a, (hipStream_t)stream));
+}
+
+int hop_cost_true_f64(int32_t system, const double* X, const double* U, const int32_t* T_star,
+                      const double* xg, int64_t xg_bs, const double* u_ref, int64_t ur_bs,
+                      const double* Q, int64_t q_bs, const double* R, int64_t r_bs,
+                      const double* Qf, int64_t qf_bs, const double* w, int64_t w_bs,
+                      const double* obstacles, int32_t n_obs, uint32_t wrap_mask, int64_t batch,
+                      int32_t N, double* J, void* stream) {
+  hop::CostCall a{};
+  int rc = cost_args(system, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs, w, w_bs,
+                     obstacles, n_obs, wrap_mask, &a.c);
+  if (rc) return rc;
+  if (batch < 0 || N < 0) return fail(HOP_E_ARG, "negative size");
+  if (batch == 0) return HOP_OK;
+  if (!X || !T_star || !J || (N > 0 && !U)) return fail(HOP_E_ARG, "null pointer");
+  a.X = X; a.U = U; a.T = T_star; a.batch = batch; a.N = N; a.J = J;
+  return hip_status(hop::dispatch_forward(system, 1, &a, (hipStream_t)stream));
+}
+
+size_t hop_forward_workspace_bytes(int32_t system, int64_t batch, int32_t N, int32_t n_alpha) {
+  if (system < 0 || system >= hop::dyn::kNumSystems || batch < 0 || N < 0 || n_alpha < 0)
+    return 0;
+  const int64_t n = hop::dyn::state_dim(system), m = hop::dyn::control_dim(system);
+  const int64_t row = (int64_t)(N + 1) * n + (int64_t)N * m;
+  return (size_t)(batch * n_alpha * (1 + row) * (int64_t)sizeof(double));
+}
+
+int hop_forward_linesearch_f64(int32_t system, double dt, const double* X, const double* U,
+                               const double* xg, int64_t xg_bs, const double* u_ref,
+                               int64_t ur_bs, const double* Q, int64_t q_bs, const double* R,
+                               int64_t r_bs, const double* Qf, int64_t qf_bs, const double* w,
+                               int64_t w_bs, const double* obstacles, int32_t n_obs,
+                               uint32_t wrap_mask, const int32_t* T_star, const int32_t* active,
+                               const double* K, const double* k, const double* alphas,
+                               int32_t n_alpha, int64_t batch, int32_t N, void* workspace,
+                               size_t workspace_bytes, double* X_new, double* U_new, double* J,
+                               double* J_old, int32_t* accepted, void* stream) {
+  hop::FwdArgs a{};
+  int rc = cost_args(system, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs, w, w_bs,
+                     obstacles, n_obs, wrap_mask, &a.c);
+  if (rc) return rc;
+  if (batch < 0 || N < 0) return fail(HOP_E_ARG, "negative size");
+  if (n_alpha < 1 || n_alpha > 8 || !alphas) return fail(HOP_E_ARG, "1 <= n_alpha <= 8 host alphas");
+  if (batch == 0) return HOP_OK;
+  if (!X || !T_star || !K || !k || !X_new || !U_new || !J || !J_old || !accepted ||
+      (N > 0 && !U))
+    return fail(HOP_E_ARG, "null pointer");
+  const size_t need = hop_forward_workspace_bytes(system, batch, N, n_alpha);
+  if (!workspace || workspace_bytes < need) return fail(HOP_E_ARG, "workspace too small");
+  if (batch * (n_alpha + 1) > (int64_t)0xffffffffLL * 64 || batch > 0x7fffffffLL)
+    return fail(HOP_E_SIZE, "batch too large for one launch");
+  a.dt = dt; a.X = X; a.U = U; a.T_star = T_star; a.active = active; a.K = K; a.kff = k;
+  for (int i = 0; i < n_alpha; ++i) a.alphas[i] = alphas[i];
+  a.n_alpha = n_alpha; a.batch = batch; a.N = N;
+  a.Jc = (double*)workspace;
+  a.ws = a.Jc + batch * n_alpha;
+  a.J_old = J_old; a.X_new = X_new; a.U_new = U_new; a.J = J; a.accepted = accepted;
+  return hip_status(hop::dispatch_forward(system, 2, &a, (hipStream_t)stream));
+}
+
+int hop_obstacle_cost_f64(const double* X, int64_t x_stride, int64_t count, int32_t n,
+                          const double* obstacles, int32_t n_obs, double* c, double* cx,
+                          double* cxx, void* stream) {
+  if (count < 0 || n < 2 || n > 16 || x_stride < n || n_obs < 0)
+    return fail(HOP_E_ARG, "bad size/stride");
+  if (count == 0) return HOP_OK;
+  if (!X || (n_obs > 0 && !obstacles)) return fail(HOP_E_ARG, "null pointer");
+  hop::ObstacleArgs a{X, x_stride, count, n, obstacles, n_obs, c, cx, cxx};
+  return hip_status(hop::dispatch_obstacle(a, (hipStream_t)stream));
+}
+
+int hop_ilqr_accept_f64(int64_t batch, int32_t warm, const double* J, const int32_t* accepted,
+                        const int32_t* T_star, double* lm, int32_t* T_bar, double* J_hist,
+                        int32_t* T_hist, int32_t* n_hist, int32_t hist_cap, int32_t* done,
+                        void* stream) {
+  if (batch < 0 || hist_cap < 1) return fail(HOP_E_ARG, "bad size");
+  if (batch == 0) return HOP_OK;
+  if (!J || !accepted || !T_star || !lm || !T_bar || !J_hist || !T_hist || !n_hist || !done)
+    return fail(HOP_E_ARG, "null pointer");
+  hop::AcceptArgs a{batch, warm ? 1 : 0, hist_cap, J, accepted, T_star, lm, T_bar, J_hist,
+                    T_hist, n_hist, done};
+  return hip_status(hop::dispatch_accept(a, (hipStream_t)stream));
+}
+
 }  // extern "C"

@@ -1,0 +1,409 @@
+// Forward pass of the time-optimal iLQR on the device:
+//   rollout                    solver.py:42-62    hop_rollout_f64
+//   cost_timeopt_true          solver.py:65-102   hop_cost_true_f64
+//   forward_linesearch_fixedT  solver.py:233-286  hop_forward_linesearch_f64
+//   extra_stage_cost of the point-mass maker (systems.py:271-293)
+//                                                 hop_obstacle_cost_f64
+// plus the accept / Levenberg-Marquardt / stop-rule bookkeeping of the outer
+// loop (solver.py:737-752), hop_ilqr_accept_f64.
+//
+// The rollouts are sequential in k, so the parallelism is across problems and
+// across the line-search step sizes: pass 1 gives one lane to every
+// (problem, alpha) pair -- the reference tries the alphas in order and keeps the
+// first whose true cost beats J_old; running them side by side and taking the
+// smallest accepted index is the same choice -- plus one lane per problem for
+// J_old.  Each lane keeps its candidate trajectory in a workspace row
+// [problem][alpha][X' | U'] that it writes sequentially, so the writes fill L2
+// lines while the lane walks the horizon.  Pass 2 (one workgroup per problem)
+// picks the winner and copies its row (or X, U when nothing was accepted) into
+// X', U' with coalesced loads and stores.
+//
+// The dynamics are dynamics.hpp's (bit-exact with NumPy for the libm-free
+// systems); the cost follows the reference's evaluation order per step,
+// c += (0.5 e.Qe + 0.5 du.Rdu) + w, then + c_extra.
+#include <math.h>
+
+#include "hop_device.hpp"
+#include "hop_kernels.hpp"
+#include "dynamics.hpp"
+
+namespace hop {
+namespace fwd {
+
+using namespace hop::dyn;
+
+constexpr int TPB = 64;
+
+__device__ inline bool fin(double v) { return v - v == 0.0; }
+
+// 0.5 v.(M v) for a row-major k x k matrix M (reference: 0.5 * float(v @ (M @ v)))
+template <int K>
+__device__ inline double half_quad(const double* __restrict__ M, const double* v) {
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    double r = 0.0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) r = fma(M[i * K + j], v[j], r);
+    acc = fma(v[i], r, acc);
+  }
+  return 0.5 * acc;
+}
+
+// sum of the Gaussian obstacle penalties at position (px, py) (systems.py:271-293, c only)
+__device__ inline double obstacle_c(const double* __restrict__ obs, int n_obs, double px,
+                                    double py) {
+  double c = 0.0;
+  for (int o = 0; o < n_obs; ++o) {
+    const double dx = px - obs[4 * o], dy = py - obs[4 * o + 1], r = obs[4 * o + 2];
+    const double s = dx * dx + dy * dy;
+    c += obs[4 * o + 3] * exp(-s / (2.0 * r * r));
+  }
+  return c;
+}
+
+template <int n>
+__device__ inline void wrap_err(const double* a, const double* b, unsigned mask, double* e) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    const double d = a[i] - b[i];
+    e[i] = (mask >> i) & 1u ? wrap_angle(d) : d;
+  }
+}
+
+// running-cost increment of step k (solver.py:87-95); false if e or du is not finite
+template <int n, int m>
+__device__ inline bool stage_inc(const CostArgs& c, long long b, const double* x,
+                                 const double* u, double& acc) {
+  double e[n], du[m];
+  wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
+  const double* ur = c.u_ref + b * c.ur_bs;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < n; ++i) ok = ok && fin(e[i]);
+#pragma unroll
+  for (int i = 0; i < m; ++i) {
+    du[i] = u[i] - ur[i];
+    ok = ok && fin(du[i]);
+  }
+  const double q = half_quad<n>(c.Q + b * c.q_bs, e);
+  const double r = half_quad<m>(c.R + b * c.r_bs, du);
+  acc += (q + r) + c.w[b * c.w_bs];
+  if (c.obs) acc += obstacle_c(c.obs, c.n_obs, x[0], x[1]);
+  return ok;
+}
+
+template <int n>
+__device__ inline double terminal_cost(const CostArgs& c, long long b, const double* x,
+                                       bool& ok) {
+  double e[n];
+  wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
+#pragma unroll
+  for (int i = 0; i < n; ++i) ok = ok && fin(e[i]);
+  return half_quad<n>(c.Qf + b * c.qf_bs, e);
+}
+
+// cost_timeopt_true over X [N+1][n], U [N][m] of problem b at horizon T
+template <int n, int m>
+__device__ double cost_true(const CostArgs& c, long long b, const double* X, const double* U,
+                            int T) {
+  if (T <= 0) return INFINITY;
+  double acc = 0.0;
+  bool ok = true;
+  for (int k = 0; k < T; ++k) {
+    double x[n], u[m];
+#pragma unroll
+    for (int i = 0; i < n; ++i) x[i] = X[k * n + i];
+#pragma unroll
+    for (int i = 0; i < m; ++i) u[i] = U[k * m + i];
+    ok = stage_inc<n, m>(c, b, x, u, acc) && ok;
+  }
+  double xT[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) xT[i] = X[T * n + i];
+  const double t = terminal_cost<n>(c, b, xT, ok);
+  return ok ? acc + t : INFINITY;
+}
+
+// ---------------------------------------------------------------- rollout
+template <int SYS>
+__global__ __launch_bounds__(TPB) void rollout_kernel(RolloutArgs a) {
+  constexpr int n = state_dim(SYS), m = control_dim(SYS);
+  const long long b = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (b >= a.batch) return;
+  const double* U = a.U + b * a.N * m;
+  double* X = a.X + b * (long long)(a.N + 1) * n;
+  double x[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) X[i] = x[i] = a.x0[b * a.x0_bs + i];
+  int k = 0;
+  for (; k < a.N; ++k) {
+    double u[m], xn[n];
+#pragma unroll
+    for (int i = 0; i < m; ++i) u[i] = U[k * m + i];
+    eval<SYS>(x, u, a.dt, xn);
+    bool ok = true;
+    double ss = 0.0;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      ok = ok && fin(xn[i]);
+      ss = fma(xn[i], xn[i], ss);
+    }
+    // reference: not finite or np.linalg.norm(xn) > max_state_norm -> X[k+1:] = NaN
+    if (!ok || sqrt(ss) > a.max_state_norm) break;
+#pragma unroll
+    for (int i = 0; i < n; ++i) X[(k + 1) * n + i] = x[i] = xn[i];
+  }
+  for (int r = k + 1; r <= a.N; ++r)
+#pragma unroll
+    for (int i = 0; i < n; ++i) X[r * n + i] = NAN;
+}
+
+// ---------------------------------------------------------------- cost
+template <int SYS>
+__global__ __launch_bounds__(TPB) void cost_kernel(CostArgs c, const double* X, const double* U,
+                                                   const int* T, long long batch, int N,
+                                                   double* J) {
+  constexpr int n = state_dim(SYS), m = control_dim(SYS);
+  const long long b = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (b >= batch) return;
+  const int t = T[b];
+  J[b] = t > N ? NAN
+               : cost_true<n, m>(c, b, X + b * (long long)(N + 1) * n, U + b * (long long)N * m,
+                                 t);
+}
+
+// ---------------------------------------------------------------- line search
+// pass 1: lane q = b * S + slot, S = n_alpha + 1; slot n_alpha computes J_old
+template <int SYS>
+__global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
+  constexpr int n = state_dim(SYS), m = control_dim(SYS);
+  const int S = a.n_alpha + 1;
+  const long long q = (long long)blockIdx.x * TPB + threadIdx.x;
+  if (q >= a.batch * S) return;
+  const long long b = q / S;
+  const int slot = (int)(q - b * S);
+  const int N = a.N;
+  const double* X = a.X + b * (long long)(N + 1) * n;
+  const double* U = a.U + b * (long long)N * m;
+  const int T = a.T_star[b];
+  const bool active = (a.active == nullptr || a.active[b] != 0) && T >= 0 && T <= N;
+  if (slot == a.n_alpha) {
+    a.J_old[b] = T > N ? NAN : cost_true<n, m>(a.c, b, X, U, T);
+    return;
+  }
+  double* J = a.Jc + b * a.n_alpha + slot;
+  if (!active) {
+    *J = NAN;
+    return;
+  }
+  const double alpha = a.alphas[slot];
+  const double* K = a.K + b * (long long)N * m * n;
+  const double* kf = a.kff + b * (long long)N * m;
+  const long long row = (long long)(N + 1) * n + (long long)N * m;
+  double* Xc = a.ws + (b * a.n_alpha + slot) * row;
+  double* Uc = Xc + (long long)(N + 1) * n;
+  double x[n];
+#pragma unroll
+  for (int i = 0; i < n; ++i) Xc[i] = x[i] = X[i];
+  double acc = 0.0;
+  bool ok = true;  // finite e / du along the horizon
+  for (int k = 0; k < N; ++k) {
+    double u[m], xn[n];
+#pragma unroll
+    for (int i = 0; i < m; ++i) u[i] = U[k * m + i];
+    if (k < T) {
+      double dx[n];
+      wrap_err<n>(x, X + k * n, a.c.wrap_mask, dx);
+      // U'[k] = U[k] + (K_k dx + alpha k_k)   (solver.py:262-263)
+#pragma unroll
+      for (int i = 0; i < m; ++i) {
+        double r = 0.0;
+#pragma unroll
+        for (int j = 0; j < n; ++j) r = fma(K[(k * m + i) * n + j], dx[j], r);
+        u[i] = u[i] + (r + alpha * kf[k * m + i]);
+      }
+      ok = stage_inc<n, m>(a.c, b, x, u, acc) && ok;
+    }
+#pragma unroll
+    for (int i = 0; i < m; ++i) Uc[k * m + i] = u[i];
+    eval<SYS>(x, u, a.dt, xn);
+    bool f = true;
+#pragma unroll
+    for (int i = 0; i < n; ++i) f = f && fin(xn[i]);
+    if (!f) {  // rejected step size (solver.py:265-267, 272-274)
+      *J = NAN;
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < n; ++i) Xc[(k + 1) * n + i] = x[i] = xn[i];
+    if (k + 1 == T) {
+      acc += terminal_cost<n>(a.c, b, x, ok);
+    }
+  }
+  if (T == 0) ok = false;  // cost_timeopt_true: T* <= 0 -> inf
+  *J = ok ? acc : INFINITY;
+}
+
+// pass 2: one workgroup per problem: the first alpha with J' < J_old, then the copy
+template <int SYS>
+__global__ __launch_bounds__(256) void linesearch_pick_kernel(FwdArgs a) {
+  constexpr int n = state_dim(SYS), m = control_dim(SYS);
+  const long long b = blockIdx.x;
+  __shared__ int s_win;
+  const int N = a.N;
+  if (threadIdx.x == 0) {
+    const double Jo = a.J_old[b];
+    int win = -1;
+    for (int s = 0; s < a.n_alpha; ++s) {
+      const double Jn = a.Jc[b * a.n_alpha + s];
+      if (Jn < Jo) {  // NaN (rejected / inactive) never wins
+        win = s;
+        break;
+      }
+    }
+    const bool active = (a.active == nullptr || a.active[b] != 0);
+    a.accepted[b] = active ? win : -2;
+    a.J[b] = win >= 0 ? a.Jc[b * a.n_alpha + win] : Jo;
+    s_win = win;
+  }
+  __syncthreads();
+  const int win = s_win;
+  const long long nx = (long long)(N + 1) * n, nu = (long long)N * m;
+  const double* srcX = win >= 0 ? a.ws + (b * a.n_alpha + win) * (nx + nu) : a.X + b * nx;
+  const double* srcU = win >= 0 ? srcX + nx : a.U + b * nu;
+  double* dX = a.X_new + b * nx;
+  double* dU = a.U_new + b * nu;
+  for (long long e = threadIdx.x; e < nx; e += 256) dX[e] = srcX[e];
+  for (long long e = threadIdx.x; e < nu; e += 256) dU[e] = srcU[e];
+}
+
+// ---------------------------------------------------------------- obstacles
+// c, cx, cxx of the point-mass obstacle penalties at `count` states (rows of n)
+__global__ __launch_bounds__(256) void obstacle_kernel(ObstacleArgs a) {
+  const long long r = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= a.count) return;
+  const int n = a.n;
+  const double px = a.X[r * a.x_stride], py = a.X[r * a.x_stride + 1];
+  double c = 0.0, g0 = 0.0, g1 = 0.0, h00 = 0.0, h01 = 0.0, h11 = 0.0;
+  for (int o = 0; o < a.n_obs; ++o) {
+    const double dx = px - a.obs[4 * o], dy = py - a.obs[4 * o + 1], rr = a.obs[4 * o + 2];
+    // the reference's groupings: 2.0 * r * r, r * r, r ** 4 (pow)
+    const double r2 = rr * rr, r4 = pow(rr, 4.0);
+    const double ci = a.obs[4 * o + 3] * exp(-(dx * dx + dy * dy) / (2.0 * rr * rr));
+    c += ci;
+    g0 += -(ci / r2) * dx;
+    g1 += -(ci / r2) * dy;
+    h00 += ci * (dx * dx / r4 - 1.0 / r2);
+    h01 += ci * (dx * dy / r4 - 0.0 / r2);
+    h11 += ci * (dy * dy / r4 - 1.0 / r2);
+  }
+  if (a.c) a.c[r] = c;
+  if (a.cx) {
+    double* g = a.cx + r * n;
+    for (int i = 0; i < n; ++i) g[i] = 0.0;
+    g[0] = g0;
+    g[1] = g1;
+  }
+  if (a.cxx) {
+    double* h = a.cxx + r * n * n;
+    for (int i = 0; i < n * n; ++i) h[i] = 0.0;
+    h[0] = h00;
+    h[1] = h01;
+    h[n] = h01;
+    h[n + 1] = h11;
+  }
+}
+
+// ---------------------------------------------------------------- accept / LM / stop
+// solver.py:737-752 per problem; warm = 1 for the warm-start update (solver.py:548-553:
+// J0 is recorded whenever the Riccati pass succeeded and J0 is finite, lm unchanged)
+__global__ __launch_bounds__(256) void accept_kernel(AcceptArgs a) {
+  const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.batch) return;
+  if (a.done[b]) return;
+  const int H = a.hist_cap;
+  int nh = a.n_hist[b];
+  const double J = a.J[b];
+  const int acc = a.accepted[b];
+  double* Jh = a.J_hist + b * H;
+  int* Th = a.T_hist + b * H;
+  if (a.warm) {
+    if (acc != -2 && fin(J) && nh < H) {
+      Jh[nh] = J;
+      Th[nh] = a.T_star[b];
+      a.n_hist[b] = ++nh;
+    }
+    return;
+  }
+  if (acc >= 0 && fin(J) && nh < H) {
+    a.T_bar[b] = a.T_star[b];
+    Jh[nh] = J;
+    Th[nh] = a.T_star[b];
+    a.n_hist[b] = ++nh;
+    const double l = a.lm[b] / 10.0;
+    a.lm[b] = l > 1e-12 ? l : 1e-12;
+  } else {
+    a.lm[b] = a.lm[b] * 10.0;
+  }
+  if (nh >= 2) {
+    const double rel = fabs(Jh[nh - 1] - Jh[nh - 2]) / (fabs(Jh[nh - 2]) + 1e-12);
+    if (rel < 1e-4 && nh >= 3 && Th[nh - 1] == Th[nh - 2] && Th[nh - 2] == Th[nh - 3])
+      a.done[b] = 1;
+  }
+}
+
+template <int SYS>
+hipError_t launch_all(int which, const void* args, hipStream_t st) {
+  switch (which) {
+    case 0: {
+      const RolloutArgs& a = *(const RolloutArgs*)args;
+      hipLaunchKernelGGL((rollout_kernel<SYS>), dim3((unsigned)((a.batch + TPB - 1) / TPB)),
+                         dim3(TPB), 0, st, a);
+      break;
+    }
+    case 1: {
+      const CostCall& a = *(const CostCall*)args;
+      hipLaunchKernelGGL((cost_kernel<SYS>), dim3((unsigned)((a.batch + TPB - 1) / TPB)),
+                         dim3(TPB), 0, st, a.c, a.X, a.U, a.T, a.batch, a.N, a.J);
+      break;
+    }
+    default: {
+      const FwdArgs& a = *(const FwdArgs*)args;
+      const long long lanes = a.batch * (a.n_alpha + 1);
+      hipLaunchKernelGGL((linesearch_kernel<SYS>), dim3((unsigned)((lanes + TPB - 1) / TPB)),
+                         dim3(TPB), 0, st, a);
+      hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL((linesearch_pick_kernel<SYS>), dim3((unsigned)a.batch), dim3(256), 0,
+                         st, a);
+    }
+  }
+  return hipGetLastError();
+}
+
+}  // namespace fwd
+
+hipError_t dispatch_forward(int sys, int which, const void* args, hipStream_t stream) {
+  switch (sys) {
+    case dyn::kDI: return fwd::launch_all<dyn::kDI>(which, args, stream);
+    case dyn::kCartpole: return fwd::launch_all<dyn::kCartpole>(which, args, stream);
+    case dyn::kQuadrotor: return fwd::launch_all<dyn::kQuadrotor>(which, args, stream);
+    case dyn::kPointmass: return fwd::launch_all<dyn::kPointmass>(which, args, stream);
+    default: return fwd::launch_all<dyn::kSegway>(which, args, stream);
+  }
+}
+
+hipError_t dispatch_obstacle(const ObstacleArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(fwd::obstacle_kernel, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+hipError_t dispatch_accept(const AcceptArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(fwd::accept_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256), 0,
+                     stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace hop

@@ -166,18 +166,33 @@ __device__ __forceinline__ float recip_nr(float d) {
   return __builtin_fmaf(r, __builtin_fmaf(-d, r, 1.0f), r);
 }
 
+// One pivot of the symmetric sweep operator on (M + eps I) (Goodnight):
+//   a_pp <- -1/d,  a_pc <- a_pc/d,  a_ip <- a_ip/d,  a_ic <- a_ic - a_ip a_pc/d,
+// d = a_pp + eps.  Row p and column p are scaled by their own multiply instead of
+// riding in the rank-1 update with a -e_p offset: the offset form computes
+// a_ip/d as a_ip (1 - (d-1)/d), which cancels to ~1e-16 d relative accuracy and
+// broke problems whose blocks reach 1e8 (cart-pole's zero angle weight gives
+// E_k = (Q_k + 1e-9 I)^-1 entries of 5e8).
+template <int p, class T, int S>
+__device__ __forceinline__ void sweep_pivot(T (&r)[S], T eps, int c, bool& ok) {
+  const T d = bcast<p>(r[p]) + eps;
+  ok = ok && (d > T(0));
+  const T rd = recip_nr(d);
+  const bool piv = (c == p);
+  const T sc = piv ? T(0) : -r[p] * rd;  // -a_pc/d off the pivot lane
+  const T rowp = piv ? -rd : r[p] * rd;
+  RowB<S>::template sweep<p>(r, sc);     // a_ic -= a_ip a_pc/d (lane p untouched)
+  const T f = piv ? rd : T(1);
+#pragma unroll
+  for (int i = 0; i < S; ++i) r[i] *= f;  // column p: a_ip/d
+  r[p] = rowp;
+}
+
 template <class T, int S>
 __device__ __forceinline__ void sweep_neg_inverse(T (&r)[S], T eps, int c, bool& ok) {
   static_for<S>([&](auto P) {
     constexpr int p = P;
-    const T d = bcast<p>(r[p]) + eps;
-    ok = ok && (d > T(0));
-    const T rd = recip_nr(d);
-    const T t = r[p] + ((c == p) ? (eps - T(1)) : T(0));  // column p minus e_p
-    const T sc = -t * rd;
-    r[p] = t;
-    RowB<S>::template sweep<p>(r, sc);                     // r += t' (-(t'_c)/d)
-    r[p] = r[p] - ((c == p) ? T(1) : T(0));                // pivot -> -1/d
+    sweep_pivot<p>(r, eps, c, ok);
   });
 }
 
@@ -261,20 +276,8 @@ __device__ __forceinline__ void sweep_neg_inverse2(T (&r1)[S], T eps1, bool& ok1
                                                    T eps2, bool& ok2, int c) {
   static_for<S>([&](auto P) {
     constexpr int p = P;
-    const T d1 = bcast<p>(r1[p]) + eps1;
-    const T d2 = bcast<p>(r2[p]) + eps2;
-    ok1 = ok1 && (d1 > T(0));
-    ok2 = ok2 && (d2 > T(0));
-    const T rd1 = recip_nr(d1), rd2 = recip_nr(d2);
-    const T t1 = r1[p] + ((c == p) ? (eps1 - T(1)) : T(0));
-    const T t2 = r2[p] + ((c == p) ? (eps2 - T(1)) : T(0));
-    const T sc1 = -t1 * rd1, sc2 = -t2 * rd2;
-    r1[p] = t1;
-    r2[p] = t2;
-    RowB<S>::template sweep<p>(r1, sc1);
-    RowB<S>::template sweep<p>(r2, sc2);
-    r1[p] = r1[p] - ((c == p) ? T(1) : T(0));
-    r2[p] = r2[p] - ((c == p) ? T(1) : T(0));
+    sweep_pivot<p>(r1, eps1, c, ok1);
+    sweep_pivot<p>(r2, eps2, c, ok2);
   });
 }
 

@@ -117,6 +117,57 @@ struct DynArgs {
   long long count, x_stride, u_stride, xn_stride;
 };
 
+// forward pass (forward.hip): rollout / true cost / line search / obstacles / accept
+struct CostArgs {
+  const double* xg; long long xg_bs;      // [B or 1][n]
+  const double* u_ref; long long ur_bs;   // [B or 1][m]
+  const double* Q; long long q_bs;        // [B or 1][n][n]
+  const double* R; long long r_bs;        // [B or 1][m][m]
+  const double* Qf; long long qf_bs;      // [B or 1][n][n]  (as_terminal_weight(alpha))
+  const double* w; long long w_bs;        // [B or 1]
+  const double* obs; int n_obs;           // [n_obs][4] = (cx, cy, radius, weight) or null
+  unsigned wrap_mask;
+};
+struct RolloutArgs {
+  double dt;
+  const double* x0; long long x0_bs;      // [B or 1][n]
+  const double* U;                        // [B][N][m]
+  long long batch; int N;
+  double max_state_norm;
+  double* X;                              // [B][N+1][n]
+};
+struct CostCall {
+  CostArgs c;
+  const double* X; const double* U; const int* T;
+  long long batch; int N;
+  double* J;
+};
+struct FwdArgs {
+  CostArgs c;
+  double dt;
+  const double* X; const double* U;       // [B][N+1][n], [B][N][m]
+  const int* T_star; const int* active;   // [B]; active nullable
+  const double* K; const double* kff;     // [B][N][m][n], [B][N][m]
+  double alphas[8]; int n_alpha;
+  long long batch; int N;
+  double* Jc;                             // workspace [B][n_alpha]
+  double* ws;                             // workspace [B][n_alpha][(N+1)n + Nm]
+  double* J_old;                          // [B]
+  double* X_new; double* U_new; double* J; int* accepted;
+};
+struct ObstacleArgs {
+  const double* X; long long x_stride, count; int n;
+  const double* obs; int n_obs;
+  double* c; double* cx; double* cxx;     // [count], [count][n], [count][n][n] (nullable)
+};
+struct AcceptArgs {
+  long long batch; int warm, hist_cap;
+  const double* J; const int* accepted; const int* T_star;
+  double* lm; int* T_bar; double* J_hist; int* T_hist; int* n_hist; int* done;
+};
+hipError_t dispatch_forward(int sys, int which, const void* args, hipStream_t stream);
+hipError_t dispatch_obstacle(const ObstacleArgs& a, hipStream_t stream);
+hipError_t dispatch_accept(const AcceptArgs& a, hipStream_t stream);
 hipError_t dispatch_linearize(const LinArgs& a, hipStream_t stream);
 hipError_t dispatch_dynamics(const DynArgs& a, hipStream_t stream);
 

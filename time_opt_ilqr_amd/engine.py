@@ -436,3 +436,186 @@ def dynamics(system, X, U, dt: float):
                                       _lib.ptr(out), n, _lib.stream_handle(X.device))
     _lib.check(rc)
     return out
+
+
+# ---- forward pass / outer-loop bookkeeping (forward.hip)
+
+ALPHAS = (1.0, 0.5, 0.25, 0.1, 0.05)  # solver.py:247
+
+
+@dataclass
+class CostParams:
+    """Device-resident cost data of cost_timeopt_true (solver.py:65-102): xg [n] or
+    [B, n], u_ref [m] or [B, m], Q, R, Qf (= as_terminal_weight(alpha)) shared or per
+    problem, w scalar or [B], obstacles [n_obs, 4] = (cx, cy, radius, weight) or None,
+    wrap_idx as in the reference."""
+    xg: "object"
+    u_ref: "object"
+    Q: "object"
+    R: "object"
+    Qf: "object"
+    w: "object"
+    obstacles: "object" = None
+    wrap_idx: Optional[Sequence[int]] = None
+
+    def args(self, Bn, n, m, dev):
+        torch = _torch()
+        dt = torch.float64
+        xg = _dev(self.xg, "xg", dt, dev)
+        u_ref = _dev(self.u_ref, "u_ref", dt, dev)
+        Q = _dev(self.Q, "Q", dt, dev)
+        R = _dev(self.R, "R", dt, dev)
+        Qf = _dev(self.Qf, "Qf", dt, dev)
+        w = _dev(torch.as_tensor(self.w, dtype=dt, device=dev).reshape(-1), "w", dt, dev)
+        for t, nm, shp in ((xg, "xg", (n,)), (u_ref, "u_ref", (m,)), (Q, "Q", (n, n)),
+                           (R, "R", (m, m)), (Qf, "Qf", (n, n))):
+            if tuple(t.shape[-len(shp):]) != shp:
+                raise ValueError(f"{nm} must end in {shp}, got {tuple(t.shape)}")
+        if w.numel() not in (1, Bn):
+            raise ValueError("w must be a scalar or [B]")
+        obs = None
+        if self.obstacles is not None and len(self.obstacles):
+            obs = _dev(torch.as_tensor(self.obstacles, dtype=dt, device=dev), "obstacles", dt, dev)
+            if obs.dim() != 2 or obs.shape[1] != 4:
+                raise ValueError("obstacles must be [n_obs, 4]")
+        n_obs = 0 if obs is None else obs.shape[0]
+        args = [_lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref),
+                _bstride(u_ref, 1, "u_ref", Bn), _lib.ptr(Q), _bstride(Q, 2, "Q", Bn),
+                _lib.ptr(R), _bstride(R, 2, "R", Bn), _lib.ptr(Qf), _bstride(Qf, 2, "Qf", Bn),
+                _lib.ptr(w), 0 if w.numel() == 1 else 1, _lib.ptr(obs), n_obs,
+                wrap_mask(self.wrap_idx, n)]
+        return args, (xg, u_ref, Q, R, Qf, w, obs)
+
+
+def _traj_xu(system, X, U):
+    sid = system_id(system)
+    n, m = system_dims(sid)
+    torch = _torch()
+    X = _dev(X, "X", torch.float64)
+    dev = X.device
+    U = _dev(U, "U", torch.float64, dev)
+    if X.dim() != 3 or U.dim() != 3 or X.shape[-1] != n or U.shape[-1] != m \
+            or X.shape[0] != U.shape[0] or X.shape[1] != U.shape[1] + 1:
+        raise ValueError(f"X must be [B, N+1, {n}] and U [B, N, {m}]")
+    return sid, n, m, X, U, dev
+
+
+def rollout(system, x0, U, dt: float, *, max_state_norm: float = 1e6):
+    """Batched rollout (solver.py:42-62): x0 [n] or [B, n], U [B, N, m] -> X [B, N+1, n]."""
+    torch = _torch()
+    sid = system_id(system)
+    n, m = system_dims(sid)
+    U = _dev(U, "U", torch.float64)
+    dev = U.device
+    x0 = _dev(x0, "x0", torch.float64, dev)
+    if U.dim() != 3 or U.shape[-1] != m:
+        raise ValueError(f"U must be [B, N, {m}]")
+    Bn, N = U.shape[0], U.shape[1]
+    if x0.shape[-1] != n or (x0.dim() == 2 and x0.shape[0] not in (1, Bn)) or x0.dim() > 2:
+        raise ValueError(f"x0 must be [{n}] or [B, {n}]")
+    X = torch.empty((Bn, N + 1, n), dtype=torch.float64, device=dev)
+    x_bs = n if (x0.dim() == 2 and x0.shape[0] == Bn and Bn > 1) else 0
+    rc = _lib.load().hop_rollout_f64(sid, float(dt), _lib.ptr(x0), x_bs, _lib.ptr(U), Bn, N,
+                                     float(max_state_norm), _lib.ptr(X), _lib.stream_handle(dev))
+    _lib.check(rc)
+    return X
+
+
+def cost_true(system, X, U, T_star, cost: CostParams):
+    """Batched cost_timeopt_true (solver.py:65-102) at per-problem horizons T_star [B]."""
+    torch = _torch()
+    sid, n, m, X, U, dev = _traj_xu(system, X, U)
+    Bn, N = U.shape[0], U.shape[1]
+    T = _dev(torch.as_tensor(T_star, device=dev).to(torch.int32).reshape(-1).expand(Bn),
+             "T_star")
+    cargs, keep = cost.args(Bn, n, m, dev)
+    J = torch.empty((Bn,), dtype=torch.float64, device=dev)
+    rc = _lib.load().hop_cost_true_f64(sid, _lib.ptr(X), _lib.ptr(U), _lib.ptr(T), *cargs, Bn, N,
+                                       _lib.ptr(J), _lib.stream_handle(dev))
+    _lib.check(rc)
+    del keep
+    return J
+
+
+@dataclass
+class LineSearchResult:
+    X: "object"         # [B, N+1, n]  X' (X where nothing was accepted)
+    U: "object"         # [B, N, m]
+    J: "object"         # [B]  accepted J' or J_old
+    J_old: "object"     # [B]
+    accepted: "object"  # [B] int32: alpha index, -1 none, -2 inactive
+
+
+def forward_linesearch(system, X, U, T_star, K, k, cost: CostParams, dt: float, *,
+                       alphas=ALPHAS, active=None) -> LineSearchResult:
+    """Batched forward_linesearch_fixedT (solver.py:233-286).  K [B, N, m, n] and
+    k [B, N, m] as hop_riccati mode 0 returns them; T_star [B]; active [B] bool/int
+    (None = all)."""
+    torch = _torch()
+    sid, n, m, X, U, dev = _traj_xu(system, X, U)
+    Bn, N = U.shape[0], U.shape[1]
+    K = _dev(K, "K", torch.float64, dev)
+    k = _dev(k, "k", torch.float64, dev)
+    if tuple(K.shape) != (Bn, N, m, n) or tuple(k.shape) != (Bn, N, m):
+        raise ValueError(f"K must be [B, N, {m}, {n}] and k [B, N, {m}]")
+    T = _dev(torch.as_tensor(T_star, device=dev).to(torch.int32).reshape(-1).expand(Bn),
+             "T_star")
+    act = None if active is None else _dev(torch.as_tensor(active, device=dev).to(torch.int32)
+                                           .reshape(-1).expand(Bn), "active")
+    al = [float(a) for a in alphas]
+    if not 1 <= len(al) <= 8:
+        raise ValueError("1..8 step sizes")
+    cargs, keep = cost.args(Bn, n, m, dev)
+    lib = _lib.load()
+    ws_bytes = int(lib.hop_forward_workspace_bytes(sid, Bn, N, len(al)))
+    ws = torch.empty((max(ws_bytes, 8),), dtype=torch.uint8, device=dev)
+    out = LineSearchResult(torch.empty_like(X), torch.empty_like(U),
+                           torch.empty((Bn,), dtype=torch.float64, device=dev),
+                           torch.empty((Bn,), dtype=torch.float64, device=dev),
+                           torch.empty((Bn,), dtype=torch.int32, device=dev))
+    c_al = (_lib.C.c_double * len(al))(*al)
+    rc = lib.hop_forward_linesearch_f64(
+        sid, float(dt), _lib.ptr(X), _lib.ptr(U), *cargs, _lib.ptr(T), _lib.ptr(act),
+        _lib.ptr(K), _lib.ptr(k), c_al, len(al), Bn, N, _lib.C.c_void_p(ws.data_ptr()),
+        ws_bytes, _lib.ptr(out.X), _lib.ptr(out.U), _lib.ptr(out.J), _lib.ptr(out.J_old),
+        _lib.ptr(out.accepted), _lib.stream_handle(dev))
+    _lib.check(rc)
+    ws.record_stream(torch.cuda.current_stream(dev))
+    del keep
+    return out
+
+
+def obstacle_cost(X, obstacles, *, want=("c", "cx", "cxx")):
+    """Point-mass extra_stage_cost (systems.py:271-293) at every state row of X [..., n]:
+    returns (c [...], cx [..., n], cxx [..., n, n]) (entries not in `want` are None)."""
+    torch = _torch()
+    X = _dev(X, "X", torch.float64)
+    dev = X.device
+    n = X.shape[-1]
+    rows = X.reshape(-1, n)
+    lead = tuple(X.shape[:-1])
+    obs = _dev(torch.as_tensor(obstacles, dtype=torch.float64, device=dev), "obstacles")
+    c = torch.empty(lead, dtype=torch.float64, device=dev) if "c" in want else None
+    cx = torch.empty(lead + (n,), dtype=torch.float64, device=dev) if "cx" in want else None
+    cxx = torch.empty(lead + (n, n), dtype=torch.float64, device=dev) if "cxx" in want else None
+    rc = _lib.load().hop_obstacle_cost_f64(_lib.ptr(rows), n, rows.shape[0], n, _lib.ptr(obs),
+                                           obs.shape[0], _lib.ptr(c), _lib.ptr(cx),
+                                           _lib.ptr(cxx), _lib.stream_handle(dev))
+    _lib.check(rc)
+    return c, cx, cxx
+
+
+def ilqr_accept(state, J, accepted, T_star, *, warm: bool = False):
+    """Accept / LM / stop-rule update of solver.py:737-752 on the per-problem state
+    tensors (lm, T_bar, J_hist, T_hist, n_hist, done) -- see solver.IlqrState."""
+    torch = _torch()
+    dev = J.device
+    Bn = J.shape[0]
+    T = _dev(torch.as_tensor(T_star, device=dev).to(torch.int32).reshape(-1).expand(Bn),
+             "T_star")
+    rc = _lib.load().hop_ilqr_accept_f64(
+        Bn, 1 if warm else 0, _lib.ptr(J), _lib.ptr(accepted), _lib.ptr(T), _lib.ptr(state.lm),
+        _lib.ptr(state.T_bar), _lib.ptr(state.J_hist), _lib.ptr(state.T_hist),
+        _lib.ptr(state.n_hist), state.J_hist.shape[1], _lib.ptr(state.done),
+        _lib.stream_handle(dev))
+    _lib.check(rc)

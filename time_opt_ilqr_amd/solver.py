@@ -1,0 +1,310 @@
+"""The time-optimal iLQR outer loop on the device.
+
+``ilqr_timeopt_batch`` runs ``ilqr_timeopt(method="propagator")``
+(/root/reference/solver.py:449-765) for a batch of independent problems of one
+system: every stage is a batched HIP launch of libhop_amd.so --
+linearisation (hop_linearize_f64), the select block (hop_lft_sweep_traj_f64:
+augmented builders + propagator + argmin), the truncated Riccati pass at T*
+(hop_riccati_f64 mode 0), the forward line search (hop_forward_linesearch_f64)
+and the accept / LM / stop-rule bookkeeping (hop_ilqr_accept_f64).  The host
+only sequences launches; it reads one flag per iteration (all problems done)
+to stop early.
+
+The reference-shaped single-problem drop-ins (same names and arguments as
+solver.py) are ``rollout``, ``cost_timeopt_true``, ``forward_linesearch_fixedT``
+and ``ilqr_timeopt`` / ``ilqr_timeopt_ourmethod``.  F must be a
+:class:`time_opt_ilqr_amd.systems.DeviceDynamics` (the make_* makers of
+:mod:`time_opt_ilqr_amd.systems` return one), and ``extra_stage_cost`` may be
+None or the point-mass obstacle cost of those makers: arbitrary Python callables
+cannot run on the device.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib, engine
+from .utils import _sym, as_terminal_weight, chol_inv
+
+ALPHAS = engine.ALPHAS
+
+
+def _torch():
+    import torch
+    return torch
+
+
+@dataclass
+class IlqrState:
+    """Per-problem outer-loop state (device tensors)."""
+    X: "object"        # [B, N+1, n]
+    U: "object"        # [B, N, m]
+    lm: "object"       # [B] f64
+    T_bar: "object"    # [B] i32
+    J_hist: "object"   # [B, H] f64
+    T_hist: "object"   # [B, H] i32
+    n_hist: "object"   # [B] i32
+    done: "object"     # [B] i32 (stop rule met, or the select block raised)
+    crashed: "object"  # [B] i32 (the reference would have raised in the select block)
+
+
+def _obstacle_rows(extra_stage_cost):
+    """The obstacle table of the point-mass extra_stage_cost, or None."""
+    if extra_stage_cost is None:
+        return None
+    from . import systems
+    if extra_stage_cost is systems.obstacle_stage_cost:
+        return np.array([[o[0], o[1], r, wt] for o, r, wt in systems.OBSTACLES])
+    obs = getattr(extra_stage_cost, "obstacles", None)
+    if obs is not None:
+        return np.asarray(obs, dtype=float).reshape(-1, 4)
+    raise NotImplementedError("extra_stage_cost must be None or the point-mass obstacle cost "
+                              "(systems.obstacle_stage_cost): arbitrary Python callables "
+                              "cannot run on the device")
+
+
+def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T_max: int, *,
+                       dt: float, U_init=None, max_iter: int = 15, lm_init: float = 1e-3,
+                       wrap_idx: Optional[Sequence[int]] = None, use_central_diff: bool = True,
+                       obstacles=None, alphas=ALPHAS, device=None) -> Dict[str, Any]:
+    """Batched ilqr_timeopt(method="propagator") (solver.py:449-765).
+
+    x0 [n] or [B, n] (torch or NumPy); U_init [B, N, m] or None (u_ref tiled);
+    xg/u_ref/Q/R shared or per problem; Qf = as_terminal_weight(alpha) [n, n];
+    w scalar.  Returns device tensors X, U, J_hist [B, H], T_hist, n_hist, T_star,
+    crashed, plus per-stage wall times (synchronised) in ``timers``.
+    """
+    torch = _torch()
+    sid = engine.system_id(system)
+    n, m = engine.system_dims(sid)
+    dev = device or torch.device("cuda", torch.cuda.current_device())
+    f64 = torch.float64
+    tt = lambda a: torch.as_tensor(np.asarray(a, dtype=float) if not isinstance(  # noqa: E731
+        a, torch.Tensor) else a, dtype=f64, device=dev).contiguous()
+    N, T_min, T_max = int(N), int(T_min), int(T_max)
+    if not 1 <= T_min <= T_max <= N:
+        raise IndexError("need 1 <= T_min <= T_max <= N (the reference indexes lists of N)")
+    x0 = tt(x0)
+    Bn = x0.shape[0] if x0.dim() == 2 else 1
+    xg_t, ur_t, Q_t, R_t, Qf_t = tt(xg), tt(np.atleast_1d(u_ref) if not isinstance(
+        u_ref, torch.Tensor) else u_ref), tt(Q), tt(R), tt(Qf)
+    R_np = R_t.cpu().numpy() if R_t.dim() == 2 else None
+    if R_np is None:
+        raise ValueError("R must be one [m, m] matrix shared by the batch")
+    R_inv = tt(chol_inv(_sym(R_np)))
+    P = tt(_sym(Qf_t.cpu().numpy()))
+    obs = None if obstacles is None or len(obstacles) == 0 else tt(obstacles)
+    cost = engine.CostParams(xg_t, ur_t, Q_t, R_t, Qf_t, float(w), obs, wrap_idx)
+    if U_init is None:
+        U = ur_t.reshape(-1, m).expand(Bn, m)[:, None, :].expand(Bn, N, m).contiguous()
+    else:
+        U = tt(U_init)
+        if U.dim() == 2:
+            U = U[None].expand(Bn, -1, -1)
+        if U.shape[1] < N:  # pad with the last control, as the reference does
+            U = torch.cat([U, U[:, -1:].expand(Bn, N - U.shape[1], m)], 1)
+        U = U[:, :N].contiguous()
+    timers = {"rollout": 0.0, "linearize": 0.0, "select": 0.0, "backward": 0.0, "forward": 0.0}
+
+    def clock(key, t0):
+        torch.cuda.synchronize(dev)
+        timers[key] += time.perf_counter() - t0
+
+    t0 = time.perf_counter()
+    X = engine.rollout(sid, x0, U, dt)
+    clock("rollout", t0)
+    H = int(max_iter) + 1
+    st = IlqrState(X, U, torch.full((Bn,), float(lm_init), dtype=f64, device=dev),
+                   torch.zeros((Bn,), dtype=torch.int32, device=dev),
+                   torch.zeros((Bn, H), dtype=f64, device=dev),
+                   torch.zeros((Bn, H), dtype=torch.int32, device=dev),
+                   torch.zeros((Bn,), dtype=torch.int32, device=dev),
+                   torch.zeros((Bn,), dtype=torch.int32, device=dev),
+                   torch.zeros((Bn,), dtype=torch.int32, device=dev))
+    bad = _lib.ST_FAIL | _lib.ST_NONFINITE
+
+    def iterate(warm):
+        t0 = time.perf_counter()
+        lin = engine.linearize(sid, st.X, st.U, dt, central=use_central_diff)
+        clock("linearize", t0)
+        t0 = time.perf_counter()
+        ex = {}
+        if obs is not None:
+            c, cx, cxx = engine.obstacle_cost(st.X[:, :N], obs)
+            ex = dict(qxx_extra=cxx, qx_extra=cx, c_extra=c)
+        sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, st.X, st.U, xg_t, ur_t, Q_t, R_inv,
+                                    P, float(w), wrap_idx=wrap_idx, n_use=T_max, t_min=T_min,
+                                    t_max=T_max, **ex)
+        # the reference raises out of ilqr_timeopt here (FloatingPointError / LinAlgError)
+        status_log.append(sel.status)
+        crash = ((sel.status & bad) != 0) & (st.done == 0)
+        st.crashed |= crash.to(torch.int32)
+        st.done |= crash.to(torch.int32)
+        T_star = sel.t_star
+        clock("select", t0)
+        t0 = time.perf_counter()
+        ric = engine.riccati(lin.A, lin.B, st.X, st.U, xg_t, ur_t, Q_t, R_t, Qf_t, T_star, st.lm,
+                             mode=0, wrap_idx=wrap_idx, reg_max_tries=1,
+                             **({} if obs is None else dict(qxx_extra=ex["qxx_extra"],
+                                                            qx_extra=ex["qx_extra"],
+                                                            c_extra=ex["c_extra"])))
+        clock("backward", t0)
+        t0 = time.perf_counter()
+        active = ((ric.status & _lib.ST_FAIL) == 0) & (st.done == 0)
+        fw = engine.forward_linesearch(sid, st.X, st.U, T_star, ric.K, ric.k, cost, dt,
+                                       alphas=alphas, active=active)
+        engine.ilqr_accept(st, fw.J, fw.accepted, T_star, warm=warm)
+        if warm:
+            # solver.py:548-553: X, U <- the line search's output, T_bar from the select
+            st.T_bar.copy_(T_star)
+        st.X, st.U = fw.X, fw.U
+        clock("forward", t0)
+
+    status_log = []
+    iterate(True)
+    iters = 0
+    for _ in range(int(max_iter)):
+        if bool((st.done != 0).all().item()):
+            break
+        iterate(False)
+        iters += 1
+    nh = st.n_hist
+    last = (nh - 1).clamp(min=0).long()
+    T_out = torch.where(nh > 0, st.T_hist.gather(1, last[:, None])[:, 0], st.T_bar)
+    return dict(X=st.X, U=st.U, J_hist=st.J_hist, T_hist=st.T_hist, n_hist=nh, T_star=T_out,
+                crashed=st.crashed, lm=st.lm, iterations=iters, timers=timers,
+                select_status=torch.stack(status_log, 1))
+
+
+# ---------------------------------------------------------------------------
+# reference-shaped single-problem drop-ins (solver.py names and arguments)
+# ---------------------------------------------------------------------------
+
+def _dyn(F):
+    from .systems import DeviceDynamics
+    if not isinstance(F, DeviceDynamics):
+        raise TypeError("F must be a time_opt_ilqr_amd.systems.DeviceDynamics "
+                        "(use the systems.make_* makers)")
+    return F
+
+
+def _dev():
+    from .horizon_selection import device
+    return device()
+
+
+def _t(a):
+    torch = _torch()
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(a, dtype=float)), dtype=torch.float64,
+                           device=_dev())
+
+
+def _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost):
+    n = X.shape[1]
+    obs = _obstacle_rows(extra_stage_cost)
+    return engine.CostParams(_t(np.asarray(xg, dtype=float).reshape(-1)),
+                             _t(np.atleast_1d(np.asarray(u_ref, dtype=float)).reshape(-1)),
+                             _t(Q), _t(np.atleast_2d(R)), _t(as_terminal_weight(alpha, n)),
+                             float(w), None if obs is None else _t(obs), wrap_idx)
+
+
+def rollout(F, x0: np.ndarray, U: np.ndarray, *, max_state_norm: float = 1e6) -> np.ndarray:
+    """solver.py:42-62 (GPU)."""
+    F = _dyn(F)
+    U = np.asarray(U, dtype=float)
+    if U.ndim == 1:
+        U = U.reshape(-1, 1)
+    X = engine.rollout(F.system_id, _t(np.asarray(x0, dtype=float).reshape(-1)), _t(U)[None],
+                       F.dt, max_state_norm=max_state_norm)
+    return X[0].cpu().numpy()
+
+
+def cost_timeopt_true(X, U, xg, u_ref, Q, R, alpha, w, T_star, wrap_idx=None,
+                      extra_stage_cost=None, *, system=None) -> float:
+    """solver.py:65-102 (GPU).  ``system`` (id, name or DeviceDynamics) selects the
+    kernel instantiation; by default it is inferred from (n, m)."""
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float)
+    if U.ndim == 1:
+        U = U.reshape(-1, 1)
+    T = int(T_star)
+    if T <= 0:
+        return float("inf")
+    if T > len(U) or T + 1 > len(X):
+        raise IndexError("index out of range")
+    sid = _system_for(system, X.shape[1], U.shape[1])
+    cost = _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost)
+    N = len(U)
+    J = engine.cost_true(sid, _t(X[:N + 1])[None], _t(U)[None], [T], cost)
+    return float(J[0].item())
+
+
+def _system_for(system, n, m):
+    if system is not None:
+        return engine.system_id(getattr(system, "system_id", system))
+    cands = [s for s in range(5) if engine.system_dims(s) == (n, m)]
+    if not cands:
+        raise ValueError(f"no device system with n={n}, m={m}")
+    return cands[0]  # the cost does not depend on the dynamics
+
+
+def forward_linesearch_fixedT(F, X, U, xg, u_ref, Q, R, alpha, w, T_star, k_list, K_list, *,
+                              alphas=ALPHAS, wrap_idx=None, extra_stage_cost=None):
+    """solver.py:233-286 (GPU) -> (X_new, U_new, J, accepted)."""
+    F = _dyn(F)
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float)
+    if U.ndim == 1:
+        U = U.reshape(-1, 1)
+    N, n, m = len(U), X.shape[1], U.shape[1]
+    T = int(T_star)
+    if T > N or len(K_list) < T or len(k_list) < T:
+        raise IndexError("list index out of range")
+    K = np.zeros((N, m, n))
+    k = np.zeros((N, m))
+    for i in range(max(T, 0)):
+        K[i] = np.asarray(K_list[i], dtype=float).reshape(m, n)
+        k[i] = np.asarray(k_list[i], dtype=float).reshape(-1)
+    cost = _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost)
+    r = engine.forward_linesearch(F.system_id, _t(X[:N + 1])[None], _t(U)[None], [T],
+                                  _t(K)[None], _t(k)[None], cost, F.dt, alphas=alphas)
+    acc = int(r.accepted[0].item()) >= 0
+    if not acc:
+        return X, U, float(r.J[0].item()), False
+    return r.X[0].cpu().numpy(), r.U[0].cpu().numpy(), float(r.J[0].item()), True
+
+
+def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: int, *,
+                 U_init=None, method: str = "propagator", max_iter: int = 15,
+                 lm_init: float = 1e-3, S_window: int = 20, wrap_idx: Optional[List[int]] = None,
+                 use_central_diff: bool = True, extra_stage_cost=None,
+                 onepass_preimage: str = "fixedpoint") -> Dict[str, Any]:
+    """solver.py:449-765 for one problem, method="propagator" (GPU end to end).
+    S_window / onepass_preimage only matter for method="onepass" (not on the device)."""
+    if method != "propagator":
+        raise NotImplementedError("the device outer loop implements method='propagator' "
+                                  "(the reference's 'ourmethod')")
+    F = _dyn(F)
+    obs = _obstacle_rows(extra_stage_cost)
+    n = F.n
+    res = ilqr_timeopt_batch(F.system_id, np.asarray(x0, dtype=float).reshape(1, -1), xg, u_ref,
+                             np.asarray(Q, dtype=float), np.atleast_2d(np.asarray(R, dtype=float)),
+                             as_terminal_weight(alpha, n), float(w), N, T_min, T_max, dt=F.dt,
+                             U_init=U_init, max_iter=max_iter, lm_init=lm_init,
+                             wrap_idx=wrap_idx, use_central_diff=use_central_diff,
+                             obstacles=obs, device=_dev())
+    if int(res["crashed"][0].item()):
+        raise np.linalg.LinAlgError("propagator_all_Jt_aug failed (non-finite or not PD)")
+    nh = int(res["n_hist"][0].item())
+    return {"X": res["X"][0].cpu().numpy(), "U": res["U"][0].cpu().numpy(),
+            "J_hist": [float(v) for v in res["J_hist"][0, :nh].cpu().numpy()],
+            "T_hist": [int(v) for v in res["T_hist"][0, :nh].cpu().numpy()],
+            "timers": res["timers"], "J_curve": None, "T_star": int(res["T_star"][0].item()),
+            "onepass_error": None}
+
+
+def ilqr_timeopt_ourmethod(*args, **kwargs):
+    return ilqr_timeopt(*args, method="propagator", **kwargs)
