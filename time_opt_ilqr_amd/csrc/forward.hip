@@ -72,9 +72,12 @@ __device__ inline void wrap_err(const double* a, const double* b, unsigned mask,
 }
 
 // running-cost increment of step k (solver.py:87-95); false if e or du is not finite
-template <int n, int m>
-__device__ inline bool stage_inc(const CostArgs& c, long long b, const double* x,
+// SH: every cost block is shared by the batch (all batch strides 0), so the block
+// addresses are wave-uniform and the compiler reads them through the scalar cache
+template <int n, int m, bool SH = false>
+__device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* x,
                                  const double* u, double& acc) {
+  const long long b = SH ? 0 : b_;
   double e[n], du[m];
   wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
   const double* ur = c.u_ref + b * c.ur_bs;
@@ -93,9 +96,10 @@ __device__ inline bool stage_inc(const CostArgs& c, long long b, const double* x
   return ok;
 }
 
-template <int n>
-__device__ inline double terminal_cost(const CostArgs& c, long long b, const double* x,
+template <int n, bool SH = false>
+__device__ inline double terminal_cost(const CostArgs& c, long long b_, const double* x,
                                        bool& ok) {
+  const long long b = SH ? 0 : b_;
   double e[n];
   wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
 #pragma unroll
@@ -174,10 +178,37 @@ __global__ __launch_bounds__(TPB) void cost_kernel(CostArgs c, const double* X, 
 }
 
 // ---------------------------------------------------------------- line search
-// pass 1: lane q = b * S + slot, S = n_alpha + 1; slot n_alpha computes J_old
-template <int SYS>
+// pass 1: lane q = b * S + slot, S = n_alpha + 1; slot n_alpha computes J_old.
+// Step k+1's rows of X, U, K, k are loaded at the top of step k (register double
+// buffer), so their latency hides under step k's dynamics and cost.
+template <int SYS, bool SH>
 __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   constexpr int n = state_dim(SYS), m = control_dim(SYS);
+  // shared cost blocks staged in LDS once per workgroup (every lane reads the same
+  // address: a broadcast, no bank conflicts); per-problem blocks stay in HBM
+  constexpr int NQ = n * n, NR = m * m;
+  __shared__ double sc[2 * NQ + NR + n + m + 1];
+  CostArgs cl = a.c;
+  if constexpr (SH) {
+    const CostArgs& c = a.c;
+    for (int i = threadIdx.x; i < 2 * NQ + NR + n + m + 1; i += TPB) {
+      double v;
+      if (i < NQ) v = c.Q[i];
+      else if (i < 2 * NQ) v = c.Qf[i - NQ];
+      else if (i < 2 * NQ + NR) v = c.R[i - 2 * NQ];
+      else if (i < 2 * NQ + NR + n) v = c.xg[i - 2 * NQ - NR];
+      else if (i < 2 * NQ + NR + n + m) v = c.u_ref[i - 2 * NQ - NR - n];
+      else v = c.w[0];
+      sc[i] = v;
+    }
+    __syncthreads();
+    cl.Q = sc;
+    cl.Qf = sc + NQ;
+    cl.R = sc + 2 * NQ;
+    cl.xg = sc + 2 * NQ + NR;
+    cl.u_ref = sc + 2 * NQ + NR + n;
+    cl.w = sc + 2 * NQ + NR + n + m;
+  }
   const int S = a.n_alpha + 1;
   const long long q = (long long)blockIdx.x * TPB + threadIdx.x;
   if (q >= a.batch * S) return;
@@ -208,23 +239,39 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   for (int i = 0; i < n; ++i) Xc[i] = x[i] = X[i];
   double acc = 0.0;
   bool ok = true;  // finite e / du along the horizon
-  for (int k = 0; k < N; ++k) {
-    double u[m], xn[n];
+  double nu[m], nx[n], nk[m], nK[m * n];  // rows of the next step
+  auto load = [&](int k) {
 #pragma unroll
-    for (int i = 0; i < m; ++i) u[i] = U[k * m + i];
+    for (int i = 0; i < m; ++i) nu[i] = U[k * m + i], nk[i] = kf[k * m + i];
+#pragma unroll
+    for (int i = 0; i < n; ++i) nx[i] = X[k * n + i];
+#pragma unroll
+    for (int i = 0; i < m * n; ++i) nK[i] = K[(long long)k * m * n + i];
+  };
+  if (N > 0) load(0);
+  for (int k = 0; k < N; ++k) {
+    // the shared cost blocks are re-read from LDS every step rather than hoisted
+    // into (spilling) registers
+    if constexpr (SH) asm volatile("" ::: "memory");
+    double u[m], xn[n];
     if (k < T) {
       double dx[n];
-      wrap_err<n>(x, X + k * n, a.c.wrap_mask, dx);
+      wrap_err<n>(x, nx, a.c.wrap_mask, dx);
       // U'[k] = U[k] + (K_k dx + alpha k_k)   (solver.py:262-263)
 #pragma unroll
       for (int i = 0; i < m; ++i) {
         double r = 0.0;
 #pragma unroll
-        for (int j = 0; j < n; ++j) r = fma(K[(k * m + i) * n + j], dx[j], r);
-        u[i] = u[i] + (r + alpha * kf[k * m + i]);
+        for (int j = 0; j < n; ++j) r = fma(nK[i * n + j], dx[j], r);
+        u[i] = nu[i] + (r + alpha * nk[i]);
       }
-      ok = stage_inc<n, m>(a.c, b, x, u, acc) && ok;
+    } else {
+#pragma unroll
+      for (int i = 0; i < m; ++i) u[i] = nu[i];
     }
+    // step k's rows are dead: load step k+1's under this step's cost and dynamics
+    if (k + 1 < N) load(k + 1);
+    if (k < T) ok = stage_inc<n, m, SH>(cl, b, x, u, acc) && ok;
 #pragma unroll
     for (int i = 0; i < m; ++i) Uc[k * m + i] = u[i];
     eval<SYS>(x, u, a.dt, xn);
@@ -238,7 +285,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = 0; i < n; ++i) Xc[(k + 1) * n + i] = x[i] = xn[i];
     if (k + 1 == T) {
-      acc += terminal_cost<n>(a.c, b, x, ok);
+      acc += terminal_cost<n, SH>(cl, b, x, ok);
     }
   }
   if (T == 0) ok = false;  // cost_timeopt_true: T* <= 0 -> inf
@@ -371,8 +418,14 @@ hipError_t launch_all(int which, const void* args, hipStream_t st) {
     default: {
       const FwdArgs& a = *(const FwdArgs*)args;
       const long long lanes = a.batch * (a.n_alpha + 1);
-      hipLaunchKernelGGL((linesearch_kernel<SYS>), dim3((unsigned)((lanes + TPB - 1) / TPB)),
-                         dim3(TPB), 0, st, a);
+      const CostArgs& c = a.c;
+      const bool shared = !c.xg_bs && !c.ur_bs && !c.q_bs && !c.r_bs && !c.qf_bs && !c.w_bs;
+      if (shared)
+        hipLaunchKernelGGL((linesearch_kernel<SYS, true>),
+                           dim3((unsigned)((lanes + TPB - 1) / TPB)), dim3(TPB), 0, st, a);
+      else
+        hipLaunchKernelGGL((linesearch_kernel<SYS, false>),
+                           dim3((unsigned)((lanes + TPB - 1) / TPB)), dim3(TPB), 0, st, a);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL((linesearch_pick_kernel<SYS>), dim3((unsigned)a.batch), dim3(256), 0,
