@@ -126,50 +126,67 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
                    torch.zeros((Bn,), dtype=torch.int32, device=dev))
     bad = _lib.ST_FAIL | _lib.ST_NONFINITE
 
-    def iterate(warm):
+    def iterate(s, warm):
+        """one update (solver.py:541-553 when warm, else 578-752) of the problems in s"""
         t0 = time.perf_counter()
-        lin = engine.linearize(sid, st.X, st.U, dt, central=use_central_diff)
+        lin = engine.linearize(sid, s.X, s.U, dt, central=use_central_diff)
         clock("linearize", t0)
         t0 = time.perf_counter()
         ex = {}
         if obs is not None:
-            c, cx, cxx = engine.obstacle_cost(st.X[:, :N], obs)
+            c, cx, cxx = engine.obstacle_cost(s.X[:, :N], obs)
             ex = dict(qxx_extra=cxx, qx_extra=cx, c_extra=c)
-        sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, st.X, st.U, xg_t, ur_t, Q_t, R_inv,
+        sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, s.X, s.U, xg_t, ur_t, Q_t, R_inv,
                                     P, float(w), wrap_idx=wrap_idx, n_use=T_max, t_min=T_min,
                                     t_max=T_max, **ex)
         # the reference raises out of ilqr_timeopt here (FloatingPointError / LinAlgError)
-        status_log.append(sel.status)
-        crash = ((sel.status & bad) != 0) & (st.done == 0)
-        st.crashed |= crash.to(torch.int32)
-        st.done |= crash.to(torch.int32)
+        crash = ((sel.status & bad) != 0) & (s.done == 0)
+        s.crashed |= crash.to(torch.int32)
+        s.done |= crash.to(torch.int32)
         T_star = sel.t_star
         clock("select", t0)
         t0 = time.perf_counter()
-        ric = engine.riccati(lin.A, lin.B, st.X, st.U, xg_t, ur_t, Q_t, R_t, Qf_t, T_star, st.lm,
+        ric = engine.riccati(lin.A, lin.B, s.X, s.U, xg_t, ur_t, Q_t, R_t, Qf_t, T_star, s.lm,
                              mode=0, wrap_idx=wrap_idx, reg_max_tries=1,
                              **({} if obs is None else dict(qxx_extra=ex["qxx_extra"],
                                                             qx_extra=ex["qx_extra"],
                                                             c_extra=ex["c_extra"])))
         clock("backward", t0)
         t0 = time.perf_counter()
-        active = ((ric.status & _lib.ST_FAIL) == 0) & (st.done == 0)
-        fw = engine.forward_linesearch(sid, st.X, st.U, T_star, ric.K, ric.k, cost, dt,
+        active = ((ric.status & _lib.ST_FAIL) == 0) & (s.done == 0)
+        fw = engine.forward_linesearch(sid, s.X, s.U, T_star, ric.K, ric.k, cost, dt,
                                        alphas=alphas, active=active)
-        engine.ilqr_accept(st, fw.J, fw.accepted, T_star, warm=warm)
+        engine.ilqr_accept(s, fw.J, fw.accepted, T_star, warm=warm)
         if warm:
             # solver.py:548-553: X, U <- the line search's output, T_bar from the select
-            st.T_bar.copy_(T_star)
-        st.X, st.U = fw.X, fw.U
+            s.T_bar.copy_(T_star)
+        s.X, s.U = fw.X, fw.U
         clock("forward", t0)
+        return sel.status
 
-    status_log = []
-    iterate(True)
+    # Problems that met the stop rule (or whose select raised) leave the batch: the
+    # remaining ones are gathered into a compact batch, so finished problems cost
+    # nothing (a crashed problem would otherwise force the select block's rerun
+    # launch every iteration).  Needs the cost blocks shared by the batch.
+    compact = all(t.dim() == d for t, d in ((xg_t, 1), (ur_t, 1), (Q_t, 2), (Qf_t, 2)))
+    fields = ("X", "U", "lm", "T_bar", "J_hist", "T_hist", "n_hist", "done", "crashed")
+    status_log = [iterate(st, True)]
     iters = 0
     for _ in range(int(max_iter)):
-        if bool((st.done != 0).all().item()):
+        live = st.done == 0
+        n_live = int(live.sum().item())
+        if n_live == 0:
             break
-        iterate(False)
+        if n_live == Bn or not compact:
+            status_log.append(iterate(st, False))
+        else:
+            idx = live.nonzero()[:, 0]
+            sub = IlqrState(*[getattr(st, f).index_select(0, idx) for f in fields])
+            stat = iterate(sub, False)
+            for f in fields:
+                getattr(st, f).index_copy_(0, idx, getattr(sub, f))
+            status_log.append(torch.zeros((Bn,), dtype=stat.dtype, device=dev)
+                              .index_copy_(0, idx, stat))
         iters += 1
     nh = st.n_hist
     last = (nh - 1).clamp(min=0).long()
