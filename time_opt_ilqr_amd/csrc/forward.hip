@@ -50,6 +50,16 @@ __device__ inline double half_quad(const double* __restrict__ M, const double* v
   return 0.5 * acc;
 }
 
+// the same for a diagonal M (off-diagonal entries exactly 0): the dense chain's
+// fma(0, v_j, r) terms add exact zeros, so this is bitwise the same number
+template <int K>
+__device__ inline double half_quad_diag(const double* __restrict__ M, const double* v) {
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < K; ++i) acc = fma(v[i], M[i * K + i] * v[i], acc);
+  return 0.5 * acc;
+}
+
 // sum of the Gaussian obstacle penalties at position (px, py) (systems.py:271-293, c only)
 __device__ inline double obstacle_c(const double* __restrict__ obs, int n_obs, double px,
                                     double py) {
@@ -76,7 +86,7 @@ __device__ inline void wrap_err(const double* a, const double* b, unsigned mask,
 // addresses are wave-uniform and the compiler reads them through the scalar cache
 template <int n, int m, bool SH = false>
 __device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* x,
-                                 const double* u, double& acc) {
+                                 const double* u, double& acc, bool diag = false) {
   const long long b = SH ? 0 : b_;
   double e[n], du[m];
   wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
@@ -89,8 +99,9 @@ __device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* 
     du[i] = u[i] - ur[i];
     ok = ok && fin(du[i]);
   }
-  const double q = half_quad<n>(c.Q + b * c.q_bs, e);
-  const double r = half_quad<m>(c.R + b * c.r_bs, du);
+  const double q = diag ? half_quad_diag<n>(c.Q + b * c.q_bs, e) : half_quad<n>(c.Q + b * c.q_bs, e);
+  const double r =
+      diag ? half_quad_diag<m>(c.R + b * c.r_bs, du) : half_quad<m>(c.R + b * c.r_bs, du);
   acc += (q + r) + c.w[b * c.w_bs];
   if (c.obs) acc += obstacle_c(c.obs, c.n_obs, x[0], x[1]);
   return ok;
@@ -98,13 +109,13 @@ __device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* 
 
 template <int n, bool SH = false>
 __device__ inline double terminal_cost(const CostArgs& c, long long b_, const double* x,
-                                       bool& ok) {
+                                       bool& ok, bool diag = false) {
   const long long b = SH ? 0 : b_;
   double e[n];
   wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
 #pragma unroll
   for (int i = 0; i < n; ++i) ok = ok && fin(e[i]);
-  return half_quad<n>(c.Qf + b * c.qf_bs, e);
+  return diag ? half_quad_diag<n>(c.Qf + b * c.qf_bs, e) : half_quad<n>(c.Qf + b * c.qf_bs, e);
 }
 
 // cost_timeopt_true over X [N+1][n], U [N][m] of problem b at horizon T
@@ -189,6 +200,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   constexpr int NQ = n * n, NR = m * m;
   __shared__ double sc[2 * NQ + NR + n + m + 1];
   CostArgs cl = a.c;
+  bool diag = false;
   if constexpr (SH) {
     const CostArgs& c = a.c;
     for (int i = threadIdx.x; i < 2 * NQ + NR + n + m + 1; i += TPB) {
@@ -202,6 +214,16 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
       sc[i] = v;
     }
     __syncthreads();
+    // every reference system has diagonal Q, R and terminal weight: then the cost
+    // reads only the diagonals (wave-uniform branch, bitwise the same value)
+    bool dg = true;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j)
+        if (i != j) dg = dg && sc[i * n + j] == 0.0 && sc[NQ + i * n + j] == 0.0;
+    for (int i = 0; i < m; ++i)
+      for (int j = 0; j < m; ++j)
+        if (i != j) dg = dg && sc[2 * NQ + i * m + j] == 0.0;
+    diag = dg;
     cl.Q = sc;
     cl.Qf = sc + NQ;
     cl.R = sc + 2 * NQ;
@@ -271,7 +293,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
     }
     // step k's rows are dead: load step k+1's under this step's cost and dynamics
     if (k + 1 < N) load(k + 1);
-    if (k < T) ok = stage_inc<n, m, SH>(cl, b, x, u, acc) && ok;
+    if (k < T) ok = stage_inc<n, m, SH>(cl, b, x, u, acc, diag) && ok;
 #pragma unroll
     for (int i = 0; i < m; ++i) Uc[k * m + i] = u[i];
     eval<SYS>(x, u, a.dt, xn);
@@ -285,7 +307,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = 0; i < n; ++i) Xc[(k + 1) * n + i] = x[i] = xn[i];
     if (k + 1 == T) {
-      acc += terminal_cost<n, SH>(cl, b, x, ok);
+      acc += terminal_cost<n, SH>(cl, b, x, ok, diag);
     }
   }
   if (T == 0) ok = false;  // cost_timeopt_true: T* <= 0 -> inf
