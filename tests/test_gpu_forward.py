@@ -240,3 +240,28 @@ def test_reference_shaped_forward_dropins(dev, golden_dir):
     assert abs(Jc - float(d["cost_J"][2])) <= 1e-12 * abs(float(d["cost_J"][2]))
     assert solver.cost_timeopt_true(d["X"], d["U"], d["xg"], d["u_ref"], d["Q"], d["R"],
                                     d["Qf"], float(d["w"]), 0) == float("inf")
+
+
+@pytest.mark.parametrize("wrap", [[6, 7], [], [0, 6, 7, 8]])
+def test_linesearch_nondefault_wrap_vs_oracle(dev, golden_dir, wrap):
+    """a wrap_idx other than the system's default takes the runtime-mask kernel"""
+    from time_opt_ilqr_amd import engine
+    d, sid, _, obs = _case(golden_dir, "quadrotor")
+    g = lambda k: d[f"f0_{k}"]  # noqa: E731
+    N, T0 = int(d["N"]), int(g("T_star"))
+    K = np.zeros((1, N, 4, 12))
+    k = np.zeros((1, N, 4))
+    K[0, :T0] = g("K")
+    k[0, :T0] = g("k")
+    X = g("X").copy()
+    X[:, 7] += 2 * np.pi  # wrapped components differ by a full turn
+    r = engine.forward_linesearch(2, _t(X[None], dev), _t(g("U")[None], dev), [T0],
+                                  _t(K, dev), _t(k, dev), _cost(d, wrap, obs, dev),
+                                  float(d["dt"]))
+    Xo, Uo, Jo, ok, ai = io.forward_linesearch(2, float(d["dt"]), X, g("U"), d["xg"],
+                                               d["u_ref"], d["Q"], d["R"], d["Qf"],
+                                               float(d["w"]), T0, k[0], K[0], wrap_idx=wrap)
+    assert int(r.accepted[0]) == ai
+    Jg = float(r.J[0])
+    assert abs(Jg - Jo) <= 1e-12 * max(1.0, abs(Jo)) or (np.isinf(Jo) and np.isinf(Jg))
+    assert _rel(_np(r.U[0]), Uo) <= 1e-11

@@ -72,24 +72,28 @@ __device__ inline double obstacle_c(const double* __restrict__ obs, int n_obs, d
   return c;
 }
 
-template <int n>
+// WM >= 0: the wrap mask is a compile-time constant (the system's default
+// wrap_idx), so unwrapped components cost nothing; WM = -1: runtime mask (every
+// component's wrap is evaluated and selected)
+template <int n, int WM = -1>
 __device__ inline void wrap_err(const double* a, const double* b, unsigned mask, double* e) {
+  const unsigned mk = WM >= 0 ? (unsigned)WM : mask;
 #pragma unroll
   for (int i = 0; i < n; ++i) {
     const double d = a[i] - b[i];
-    e[i] = (mask >> i) & 1u ? wrap_angle(d) : d;
+    e[i] = (mk >> i) & 1u ? wrap_angle(d) : d;
   }
 }
 
 // running-cost increment of step k (solver.py:87-95); false if e or du is not finite
 // SH: every cost block is shared by the batch (all batch strides 0), so the block
 // addresses are wave-uniform and the compiler reads them through the scalar cache
-template <int n, int m, bool SH = false>
+template <int n, int m, bool SH = false, int WM = -1>
 __device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* x,
                                  const double* u, double& acc, bool diag = false) {
   const long long b = SH ? 0 : b_;
   double e[n], du[m];
-  wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
+  wrap_err<n, WM>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
   const double* ur = c.u_ref + b * c.ur_bs;
   bool ok = true;
 #pragma unroll
@@ -107,12 +111,12 @@ __device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* 
   return ok;
 }
 
-template <int n, bool SH = false>
+template <int n, bool SH = false, int WM = -1>
 __device__ inline double terminal_cost(const CostArgs& c, long long b_, const double* x,
                                        bool& ok, bool diag = false) {
   const long long b = SH ? 0 : b_;
   double e[n];
-  wrap_err<n>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
+  wrap_err<n, WM>(x, c.xg + b * c.xg_bs, c.wrap_mask, e);
 #pragma unroll
   for (int i = 0; i < n; ++i) ok = ok && fin(e[i]);
   return diag ? half_quad_diag<n>(c.Qf + b * c.qf_bs, e) : half_quad<n>(c.Qf + b * c.qf_bs, e);
@@ -192,7 +196,7 @@ __global__ __launch_bounds__(TPB) void cost_kernel(CostArgs c, const double* X, 
 // pass 1: lane q = b * S + slot, S = n_alpha + 1; slot n_alpha computes J_old.
 // Step k+1's rows of X, U, K, k are loaded at the top of step k (register double
 // buffer), so their latency hides under step k's dynamics and cost.
-template <int SYS, bool SH>
+template <int SYS, bool SH, int WM>
 __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   constexpr int n = state_dim(SYS), m = control_dim(SYS);
   // shared cost blocks staged in LDS once per workgroup (every lane reads the same
@@ -278,7 +282,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
     double u[m], xn[n];
     if (k < T) {
       double dx[n];
-      wrap_err<n>(x, nx, a.c.wrap_mask, dx);
+      wrap_err<n, WM>(x, nx, a.c.wrap_mask, dx);
       // U'[k] = U[k] + (K_k dx + alpha k_k)   (solver.py:262-263)
 #pragma unroll
       for (int i = 0; i < m; ++i) {
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
     }
     // step k's rows are dead: load step k+1's under this step's cost and dynamics
     if (k + 1 < N) load(k + 1);
-    if (k < T) ok = stage_inc<n, m, SH>(cl, b, x, u, acc, diag) && ok;
+    if (k < T) ok = stage_inc<n, m, SH, WM>(cl, b, x, u, acc, diag) && ok;
 #pragma unroll
     for (int i = 0; i < m; ++i) Uc[k * m + i] = u[i];
     eval<SYS>(x, u, a.dt, xn);
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
 #pragma unroll
     for (int i = 0; i < n; ++i) Xc[(k + 1) * n + i] = x[i] = xn[i];
     if (k + 1 == T) {
-      acc += terminal_cost<n, SH>(cl, b, x, ok, diag);
+      acc += terminal_cost<n, SH, WM>(cl, b, x, ok, diag);
     }
   }
   if (T == 0) ok = false;  // cost_timeopt_true: T* <= 0 -> inf
@@ -442,12 +446,17 @@ hipError_t launch_all(int which, const void* args, hipStream_t st) {
       const long long lanes = a.batch * (a.n_alpha + 1);
       const CostArgs& c = a.c;
       const bool shared = !c.xg_bs && !c.ur_bs && !c.q_bs && !c.r_bs && !c.qf_bs && !c.w_bs;
-      if (shared)
-        hipLaunchKernelGGL((linesearch_kernel<SYS, true>),
-                           dim3((unsigned)((lanes + TPB - 1) / TPB)), dim3(TPB), 0, st, a);
+      // the reference's wrap_idx of each system (systems.py:48, 110, 228, 263, 347)
+      constexpr int WD = SYS == kCartpole || SYS == kSegway ? (1 << 2)
+                         : SYS == kQuadrotor                ? (7 << 6)
+                                                            : 0;
+      const dim3 grid((unsigned)((lanes + TPB - 1) / TPB));
+      if (shared && c.wrap_mask == (unsigned)WD)
+        hipLaunchKernelGGL((linesearch_kernel<SYS, true, WD>), grid, dim3(TPB), 0, st, a);
+      else if (shared)
+        hipLaunchKernelGGL((linesearch_kernel<SYS, true, -1>), grid, dim3(TPB), 0, st, a);
       else
-        hipLaunchKernelGGL((linesearch_kernel<SYS, false>),
-                           dim3((unsigned)((lanes + TPB - 1) / TPB)), dim3(TPB), 0, st, a);
+        hipLaunchKernelGGL((linesearch_kernel<SYS, false, -1>), grid, dim3(TPB), 0, st, a);
       hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL((linesearch_pick_kernel<SYS>), dim3((unsigned)a.batch), dim3(256), 0,
