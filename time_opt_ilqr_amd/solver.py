@@ -69,13 +69,16 @@ def _obstacle_rows(extra_stage_cost):
 def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T_max: int, *,
                        dt: float, U_init=None, max_iter: int = 15, lm_init: float = 1e-3,
                        wrap_idx: Optional[Sequence[int]] = None, use_central_diff: bool = True,
-                       obstacles=None, alphas=ALPHAS, device=None) -> Dict[str, Any]:
+                       obstacles=None, alphas=ALPHAS, device=None,
+                       stage_timers: bool = True) -> Dict[str, Any]:
     """Batched ilqr_timeopt(method="propagator") (solver.py:449-765).
 
     x0 [n] or [B, n] (torch or NumPy); U_init [B, N, m] or None (u_ref tiled);
     xg/u_ref/Q/R shared or per problem; Qf = as_terminal_weight(alpha) [n, n];
     w scalar.  Returns device tensors X, U, J_hist [B, H], T_hist, n_hist, T_star,
-    crashed, plus per-stage wall times (synchronised) in ``timers``.
+    crashed, plus per-stage wall times in ``timers`` (the reference's timers dict;
+    each stage is synchronised for it -- stage_timers=False skips those syncs and
+    leaves the host waiting only on the once-per-iteration "all done" flag).
     """
     torch = _torch()
     sid = engine.system_id(system)
@@ -110,8 +113,9 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     timers = {"rollout": 0.0, "linearize": 0.0, "select": 0.0, "backward": 0.0, "forward": 0.0}
 
     def clock(key, t0):
-        torch.cuda.synchronize(dev)
-        timers[key] += time.perf_counter() - t0
+        if stage_timers:
+            torch.cuda.synchronize(dev)
+            timers[key] += time.perf_counter() - t0
 
     t0 = time.perf_counter()
     X = engine.rollout(sid, x0, U, dt)
