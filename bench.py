@@ -1,21 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: batched LFT backward sweeps/s (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lft|config3|config5|select_gains]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver form, N > 1)
 
 A "step" is one pass of the hot path over one batch: the fused LFT sweep
 (stage + prefix compose + all-horizon query) of every problem plus the fused
 horizon argmin, with the (T*, J*) all-gather over RCCL when N > 1.  Inputs are
-synthetic Quadrotor-shaped blocks (s = n+1 = 13, m = 4, N = 100, fp64) resident
-in HBM before timing (configs[1] of BASELINE.json; per-GPU work fixed as N
-grows -> weak scaling).  Rank 0 prints ONE JSON line.
+synthetic blocks resident in HBM before timing.  Rank 0 prints ONE JSON line.
+
+Workloads (BASELINE.json configs):
+  lft (default)  N=1: config 2 -- Quadrotor shape s=13, m=4, N=100, 4096 problems, fp64.
+                 N>1: config 4 -- the same shape, 32768 problems per GPU (262144 on 8
+                 GPUs), contiguous shards, weak scaling.
+  config3        Cartpole shape s=5, m=1, N=200, 65536 problems, fp32 (small-s kernel).
+  config5        mixed Segway / Cartpole / Quadrotor (i mod 3) padded to s=13, m=4,
+                 N=128, 16384 problems per GPU (131072 on 8), fp32 blocks.
+  select_gains   the select + backward of solver.py:581-597: trajectory-form select
+                 (in-kernel augmentation + LFT + argmin) followed by the truncated
+                 Riccati gains at each problem's T* (n=12, m=4, N=100, 4096, fp64).
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -28,6 +36,7 @@ PEAK_F32_TFLOPS = 157.3  # MI355X fp32 vector (packed)
 PEAK_HBM_GBS = 8000.0
 SMALL_SHAPES = {"f32": {(2, 1), (3, 1), (4, 1), (4, 2), (5, 1), (5, 2)},
                 "f64": {(2, 1), (3, 1), (4, 1), (4, 2)}}
+CONFIG5_ALG_FLOPS = 2472905  # mean over the true shapes (13/4 and 5/1 x2)
 
 
 def baseline_metric():
@@ -40,17 +49,16 @@ def baseline_metric():
 
 
 def kernel_path(s, m, dtype):
-    """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound."""
+    """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound.
+    The s=13 kernels are compute-bound on the fp64 pipe (MI355X: vector fp64 peak ==
+    matrix fp64 peak); they issue DPP-broadcast FMAs, not MFMA."""
     if dtype == "f64" and (s, m) == (13, 4):
-        if os.environ.get("HOP_LFT_VARIANT", "40") in ("40", "41"):
-            return "lft_cond_kernel<SchedCondL,13,4>", "mfma"
-        return "lft_sweep_v2_kernel<SchedLdlDma,13,4>", "mfma"
-    if dtype == "f32" and (s, m) == (13, 4) and os.environ.get("HOP_LFT_VARIANT", "40") in ("40", "41") \
-            and not os.environ.get("HOP_FORCE_GENERIC"):
-        return "lft_cond_kernel<SchedCond,13,4,float>", "mfma"  # fp32 blocks, fp64 arithmetic
+        return "lft_cond_kernel<SchedCondL,13,4>", "fp64"
+    if dtype == "f32" and (s, m) == (13, 4):
+        return "lft_cond_kernel<SchedCond,13,4,float>", "fp64"  # fp32 blocks, fp64 arithmetic
     if (s, m) in SMALL_SHAPES[dtype]:
         return f"lft_small_kernel<{'float' if dtype == 'f32' else 'double'},{s},{m}>", "hbm"
-    return "lft_sweep_kernel", "mfma"
+    return "lft_sweep_kernel", "fp64" if dtype == "f64" else "fp32"
 
 
 def lft_flops(N, s, m):
@@ -71,9 +79,44 @@ def lft_bytes(N, s, m, w=8):
     return w * (N * (3 * s * s + s * m) + m * m + s + N)
 
 
+def riccati_flops(n, m, T):
+    """SURVEY.md 8(d) Riccati add-on: (4n^3 + 10n^2 m) per step."""
+    return (4 * n ** 3 + 10 * n * n * m) * T
+
+
 # ---------------------------------------------------------------------------
 # CPU baseline: the oracle's NumPy restatement on the host cores (rank 0 only)
 # ---------------------------------------------------------------------------
+
+def host_cores():
+    """CPUs this process may actually use: the affinity mask, capped by a cgroup
+    v2 cpu.max quota when one is set (a GPU box shows the whole machine in
+    os.cpu_count() but grants a share of it)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
 
 def _cpu_worker(args):
     seed0, count, s, m, N = args
@@ -85,24 +128,112 @@ def _cpu_worker(args):
     return count, time.perf_counter() - t0
 
 
-def cpu_baseline(s, m, N, per_core=640, cores=None):
+def cpu_baseline(s, m, N, target_s=8.0):
+    """Sweeps/s of the NumPy restatement on every usable host core (one process
+    per core, one BLAS thread each); the per-process sample is sized from a
+    one-sweep probe to about target_s seconds of work."""
     import multiprocessing as mp
-    cores = cores or min(16, os.cpu_count() or 1)
+    cores = host_cores()
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     os.environ["OMP_NUM_THREADS"] = "1"
     ctx = mp.get_context("spawn")
-    jobs = [(10_000 + c * per_core, per_core, s, m, N) for c in range(cores)]
-    # warm the interpreters (imports) before the timed map
     with ctx.Pool(cores) as pool:
-        pool.map(_cpu_worker, [(0, 1, s, m, 2)] * cores)
+        probe = pool.map(_cpu_worker, [(0, 2, s, m, N)] * cores)  # imports + timing probe
+        per_sweep = max(t / c for c, t in probe)
+        per_core = max(4, int(target_s / max(per_sweep, 1e-6)))
+        jobs = [(10_000 + c * per_core, per_core, s, m, N) for c in range(cores)]
         t0 = time.perf_counter()
         res = pool.map(_cpu_worker, jobs)
         wall = time.perf_counter() - t0
     done = sum(r[0] for r in res)
     return {"value": done / wall, "unit": "sweeps/s", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": f"{done} synthetic sweeps (s={s}, m={m}, N={N}, fp64) of the NumPy "
                       f"restatement oracle/hop_oracle.py, {cores} processes x 1 BLAS thread, "
                       f"{wall:.1f} s wall"}
+
+
+# ---------------------------------------------------------------------------
+# workloads: each returns (launch(), problems per step, description dict)
+# ---------------------------------------------------------------------------
+
+def _lft_workload(args, world, lo, hi, dev):
+    import torch
+    from time_opt_ilqr_amd import engine, synth
+    s, m, N = args.s, args.m, args.N
+    dtype = torch.float64 if args.dtype == "f64" else torch.float32
+    A, Bm, Q, Ri, z0, QT = synth.device_batch(hi - lo, s, m, N, seed=1234 + lo, device=dev,
+                                              dtype=dtype)
+    t_min, t_max = min(args.t_min, N), N
+
+    def launch():
+        return engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
+
+    kname, bound = kernel_path(s, m, args.dtype)
+    w = 8 if args.dtype == "f64" else 4
+    info = dict(kernel=kname, bound=bound, flops=lft_flops(N, s, m), bytes=lft_bytes(N, s, m, w),
+                executed=cond_flops(N, s, m) if kname.startswith("lft_cond") else None,
+                t_min=t_min, t_max=t_max, s=s, m=m, N=N,
+                host=(A, Bm, Q, Ri, z0, QT))
+    return launch, info
+
+
+def _config5_workload(args, world, lo, hi, dev):
+    import torch
+    from time_opt_ilqr_amd import engine, synth
+    N = args.N
+    mb, _ = synth.config5_batch(hi - lo, N, seed=77 + lo, device=dev, dtype=torch.float32)
+    t_min = min(args.t_min, N)
+
+    def launch():
+        return engine.propagate(mb.A, mb.B, mb.Q, mb.R_inv, mb.z0, mb.QT, t_min=t_min, t_max=N)
+
+    info = dict(kernel="lft_cond_kernel<SchedCond,13,4,float>", bound="fp64",
+                flops=CONFIG5_ALG_FLOPS, bytes=lft_bytes(N, 13, 4, 4),
+                executed=cond_flops(N, 13, 4), t_min=t_min, t_max=N, s=13, m=4, N=N,
+                host=(mb.A, mb.B, mb.Q, mb.R_inv, mb.z0, mb.QT))
+    return launch, info
+
+
+def _select_gains_workload(args, world, lo, hi, dev):
+    import torch
+    from time_opt_ilqr_amd import engine
+    Bn, n, m, N = hi - lo, args.s - 1, args.m, args.N
+    g = torch.Generator(device=dev)
+    g.manual_seed(11 + lo)
+    kw = dict(device=dev, dtype=torch.float64, generator=g)
+    eye = torch.eye(n, device=dev, dtype=torch.float64)
+    A = eye + 0.05 * torch.randn((Bn, N, n, n), **kw)
+    Bm = 0.1 * torch.randn((Bn, N, n, m), **kw)
+    X = 0.5 * torch.randn((Bn, N + 1, n), **kw)
+    U = 0.3 * torch.randn((Bn, N, m), **kw)
+    a_res = 0.02 * torch.randn((Bn, N, n), **kw)
+    xg = 0.2 * torch.randn((n,), **kw)
+    ur = 0.1 * torch.randn((m,), **kw)
+    M = torch.randn((n, n), **kw)
+    Q = M @ M.T / n + 0.5 * eye
+    R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
+    Rinv = torch.linalg.inv(R)
+    P = torch.diag(1.0 + 9.0 * torch.rand((n,), **kw))
+    w = 0.5
+    t_min = min(args.t_min, N)
+
+    def launch():
+        sel = engine.propagate_traj(A, Bm, a_res, X, U, xg, ur, Q, Rinv, P, w, t_min=t_min,
+                                    t_max=N, rho_reg=1.0)
+        ric = engine.riccati(A, Bm, X, U, xg, ur, Q, R, P, sel.t_star, 1e-3, mode=0)
+        sel.riccati_status = ric.status
+        return sel
+
+    info = dict(kernel="lft_cond_cf_kernel<SchedCondTraj,13,4> + riccati_kernel<double,12,4>",
+                bound="fp64", flops=lft_flops(N, n + 1, m) + riccati_flops(n, m, N),
+                bytes=8 * (N * (n * n + n * m + 2 * n + m) + n), executed=None,
+                t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
+    return launch, info
+
+
+WORKLOADS = {"lft": _lft_workload, "config3": _lft_workload, "config5": _config5_workload,
+             "select_gains": _select_gains_workload}
 
 
 def main():
@@ -110,13 +241,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="problems per GPU")
-    ap.add_argument("--s", type=int, default=13)
-    ap.add_argument("--m", type=int, default=4)
-    ap.add_argument("--N", type=int, default=100)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lft")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="problems per GPU (default: the workload's config size)")
+    ap.add_argument("--s", type=int, default=None)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--t-min", type=int, default=40)
-    ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive side figure")
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="untimed launches before the warm-up steps (GPU clock ramp)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
@@ -126,9 +260,21 @@ def main():
     import torch.distributed as dist
     from time_opt_ilqr_amd import build as hop_build
     from time_opt_ilqr_amd import distributed as hd
-    from time_opt_ilqr_amd import engine, synth
 
     rank, world, local = hd.env_rank_world()
+    wl = args.workload
+    # workload defaults (BASELINE.json configs)
+    dflt = {"lft": (4096 if world == 1 else 32768, 13, 4, 100, "f64"),
+            "config3": (65536, 5, 1, 200, "f32"),
+            "config5": (16384, 13, 4, 128, "f32"),
+            "select_gains": (4096, 13, 4, 100, "f64")}[wl]
+    args.batch = args.batch or dflt[0]
+    args.s = args.s or dflt[1]
+    args.m = args.m or dflt[2]
+    args.N = args.N or dflt[3]
+    args.dtype = args.dtype or dflt[4]
+    if wl == "config3":
+        args.t_min = min(args.t_min, 20)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -137,15 +283,13 @@ def main():
         hop_build.build(verbose=False)
     if world > 1:
         dist.barrier()
-    dtype = torch.float64 if args.dtype == "f64" else torch.float32
-    Bn, s, m, N = args.batch, args.s, args.m, args.N
+    Bn = args.batch
     lo, hi = hd.shard_bounds(Bn * world, rank, world)
-    A, Bm, Q, Ri, z0, QT = synth.device_batch(hi - lo, s, m, N, seed=1234 + lo, device=dev,
-                                               dtype=dtype)
-    t_min, t_max = min(args.t_min, N), N
+    launch, info = WORKLOADS[wl](args, world, lo, hi, dev)
+    s, m, N = info["s"], info["m"], info["N"]
 
     def step():
-        r = engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
+        r = launch()
         if world > 1:
             hd.gather_selection(r.t_star, r.j_star, Bn * world)
         return r
@@ -158,13 +302,15 @@ def main():
     t_pw = time.perf_counter()
     while time.perf_counter() - t_pw < args.prewarm_s:
         for _ in range(8):  # local launches only: ranks may differ in count, no collective
-            engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
+            launch()
             prewarm += 1
         torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     K = args.steps
+    # HIP events on the stream the kernels are launched on (engine launches on
+    # torch's current stream)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K)]
     if world > 1:
@@ -173,7 +319,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(K):
         ev[i][0].record()
-        r = engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
+        r = launch()
         ev[i][1].record()
         if world > 1:
             hd.gather_selection(r.t_star, r.j_star, Bn * world)
@@ -187,25 +333,46 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     status_ok = int(r.status.abs().sum().item()) == 0 and bool(torch.isfinite(r.J).all())
+    if hasattr(r, "riccati_status"):
+        status_ok = status_ok and int(r.riccati_status.abs().sum().item()) == 0
+
+    # PCIe-inclusive side figure (never `value`): the step's inputs start in pinned
+    # host memory and are copied H2D inside the timed region
+    h2d = None
+    if rank == 0 and not args.no_h2d and info["host"] is not None:
+        dev_in = info["host"]
+        pinned = [t.cpu().pin_memory() for t in dev_in]
+        reps = 3
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            for d_, h_ in zip(dev_in, pinned):
+                d_.copy_(h_, non_blocking=True)
+            launch()
+        torch.cuda.synchronize()
+        h2d_s = (time.perf_counter() - t1) / reps
+        nbytes = sum(t.numel() * t.element_size() for t in pinned)
+        h2d = {"value": (hi - lo) / h2d_s, "unit": "sweeps/s", "ms_per_step": h2d_s * 1e3,
+               "h2d_bytes_per_step": nbytes, "note": "inputs copied from pinned host memory "
+               "each step (PCIe-inclusive); not the headline value"}
+        del pinned
 
     if rank == 0:
         total = Bn * world * K
         value = total / elapsed
-        kname, bound = kernel_path(s, m, args.dtype)
-        w = 8 if dtype == torch.float64 else 4
-        if bound == "hbm":
-            achieved = lft_bytes(N, s, m, w) * (hi - lo) / (kern_ms * 1e-3) / 1e9
+        per_launch = hi - lo
+        if info["bound"] == "hbm":
+            achieved = info["bytes"] * per_launch / (kern_ms * 1e-3) / 1e9
             peak, unit = PEAK_HBM_GBS, "GB/s"
         else:
-            achieved = lft_flops(N, s, m) * (hi - lo) / (kern_ms * 1e-3) / 1e12
-            peak = (PEAK_F64_TFLOPS if args.dtype == "f64" or kname.startswith("lft_cond")
-                    else PEAK_F32_TFLOPS)
+            achieved = info["flops"] * per_launch / (kern_ms * 1e-3) / 1e12
+            peak = PEAK_F64_TFLOPS if info["bound"] == "fp64" else PEAK_F32_TFLOPS
             unit = "TFLOP/s"
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            key = f"s{s}_m{m}_N{N}_B{hi - lo}_{args.dtype}"
+            key = f"{wl}_s{s}_m{m}_N{N}_B{per_launch}_{args.dtype}"
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
@@ -213,10 +380,31 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(s, m, N)
+            if wl == "select_gains":
+                cpu["note"] = "LFT sweep only (the Riccati gains are not in the CPU sample)"
+        roof = {"bound": info["bound"], "achieved": achieved, "peak": peak, "unit": unit,
+                "frac": achieved / peak, "traffic": traffic, "kernel": info["kernel"],
+                "kernel_ms": kern_ms, "flops_per_sweep": info["flops"],
+                "alg_bytes_per_sweep": info["bytes"]}
+        if info["executed"]:
+            ex = info["executed"] * per_launch / (kern_ms * 1e-3) / 1e12
+            roof.update(executed_flops_per_sweep=info["executed"], executed_tflops=ex,
+                        executed_frac=ex / peak)
+        if args.dtype == "f32" and info["bound"] == "fp64":
+            roof["arithmetic"] = "f64 (fp32 blocks in HBM/LDS)"
+        if info["bound"] != "hbm":
+            roof["hbm_gbs"] = info["bytes"] * per_launch / (kern_ms * 1e-3) / 1e9
+        names = {"lft": ("config 2: LFT sweep + fused argmin" if world == 1 else
+                         "config 4 shard: LFT sweep + fused argmin"),
+                 "config3": "config 3: LFT sweep + fused argmin (small-s kernel)",
+                 "config5": "config 5: mixed Segway/Cartpole/Quadrotor padded to s=13 m=4, "
+                            "LFT sweep + fused argmin",
+                 "select_gains": "select (in-kernel augmentation + LFT + argmin) + truncated "
+                                 "Riccati gains at each T* (solver.py:581-597)"}
         line = {
             "metric": baseline_metric(),
             "value": value,
-            "unit": "sweeps/s",
+            "unit": "sweeps/s" if wl != "select_gains" else "problems/s",
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
@@ -227,24 +415,13 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (device RNG, well-conditioned SPD blocks; SURVEY.md 8(d))",
-            "config": {"workload": f"LFT sweep + fused argmin, s={s} m={m} N={N}",
+            "config": {"workload": f"{names[wl]}, s={s} m={m} N={N}",
                        "batch_per_gpu": Bn, "global_batch": Bn * world, "s": s, "m": m,
-                       "N": N, "t_min": t_min, "t_max": t_max, "parallelism": f"dp{world}"},
-            "roofline": {"bound": bound, "achieved": achieved, "peak": peak,
-                         "unit": unit, "frac": achieved / peak,
-                         "traffic": traffic,
-                         "kernel": kname, "kernel_ms": kern_ms,
-                         "flops_per_sweep": lft_flops(N, s, m),
-                         **({"executed_flops_per_sweep": cond_flops(N, s, m),
-                             "executed_tflops": cond_flops(N, s, m) * (hi - lo)
-                             / (kern_ms * 1e-3) / 1e12,
-                             "executed_frac": cond_flops(N, s, m) * (hi - lo)
-                             / (kern_ms * 1e-3) / 1e12 / peak}
-                            if kname.startswith("lft_cond") else {}),
-                         **({"arithmetic": "f64 (fp32 blocks in HBM/LDS)"}
-                            if kname.endswith("float>") else {}),
-                         "alg_bytes_per_sweep": lft_bytes(N, s, m, 8 if dtype == torch.float64 else 4)},
+                       "N": N, "t_min": info["t_min"], "t_max": info["t_max"],
+                       "parallelism": f"dp{world}"},
+            "roofline": roof,
             "cpu_baseline": cpu,
+            "h2d_inclusive": h2d,
             "status_ok": status_ok,
         }
         print(json.dumps(line), flush=True)

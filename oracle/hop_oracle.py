@@ -511,3 +511,47 @@ def synth_traj_problem(seed, n, m, N):
     a_res = np.stack([(X[k + 1] + a_raw[k]) - X[k + 1] for k in range(N)])
     return dict(A=A, B=B, a_res=a_res, X=X, U=U, xg=xg, u_ref=u_ref, Q=Q, R=R, alpha=alpha,
                 w=w, wrap_idx=[0], a_raw=a_raw)
+
+
+# ---------------------------------------------------------------------------
+# Config 5: mixed Segway / Cartpole / Quadrotor shapes
+# ---------------------------------------------------------------------------
+
+CONFIG5_KINDS = (("segway", 5, 1), ("cartpole", 5, 1), ("quadrotor", 13, 4))
+
+
+def config5_kind(i):
+    """Member i of the config-5 batch: kind i mod 3 -> (name, s, m)."""
+    return CONFIG5_KINDS[int(i) % 3]
+
+
+def synth_config5_problem(base_seed, i, N):
+    """Problem i of the mixed batch at its TRUE shape (synth_lft_problem with
+    seed base_seed + i and the kind's (s, m))."""
+    _, s, m = config5_kind(i)
+    return synth_lft_problem(base_seed + int(i), s, m, N)
+
+
+def embed_block_decoupled(A, Bm, Q, R_inv, z0, QT, s_out, m_out):
+    """NumPy statement of the block-decoupled embedding:
+    real state dims keep their indices, pad dims sit between them and the
+    homogeneous coordinate (last); A_pad = 0, B_pad rows / extra columns 0,
+    Q_pad = QT_pad = I, R_inv_pad = I, z0_pad = 0.  One problem, (N, s, s) blocks."""
+    N, s = A.shape[0], A.shape[1]
+    m = Bm.shape[-1]
+    n = s - 1
+    idx = list(range(n)) + [s_out - 1]
+
+    def sq(M, fill):
+        out = np.zeros((N, s_out, s_out))
+        out[:, n:s_out - 1, n:s_out - 1] = fill * np.eye(s_out - 1 - n)
+        out[np.ix_(range(N), idx, idx)] = M
+        return out
+
+    Bp = np.zeros((N, s_out, m_out))
+    Bp[np.ix_(range(N), idx, range(m))] = Bm
+    Rp = np.eye(m_out)
+    Rp[:m, :m] = R_inv
+    zp = np.zeros(s_out)
+    zp[idx] = z0
+    return sq(A, 0.0), Bp, sq(Q, 1.0), Rp, zp, sq(QT, 1.0)

@@ -433,8 +433,159 @@ def main():
     chol_inv_cases()
 
 
+# ---------------------------------------------------------------------------
+# round 2: wider synthetic goldens, config 5, the legacy twin + plots/, LU slot
+# ---------------------------------------------------------------------------
+
+def synthetic_lft_wide(tag, s, m, N, base_seed, count, T_min, T_max):
+    """J(t) and T* of `count` synthetic problems (no E/F/G): the default-path goldens."""
+    J = np.array([ref_hs.propagator_all_Jt_aug(*_prop_args(orc.synth_lft_problem(base_seed + i,
+                                                                                 s, m, N), N))
+                  for i in range(count)])
+    Tstar = np.array([int(np.argmin(j[T_min - 1:T_max]) + T_min) for j in J])
+    np.savez_compressed(os.path.join(HERE, f"lft_wide_{tag}.npz"), s=s, m=m, N=N,
+                        base_seed=base_seed, count=count, T_min=T_min, T_max=T_max,
+                        J=J, T_star=Tstar)
+    print(f"lft_wide_{tag}: {count} problems, T*={Tstar}")
+
+
+def _prop_args(prob, N):
+    A, Bm, Q, R, R_inv, z0, QT = prob
+    return (list(A), list(Bm), list(Q), [R] * N, z0, list(QT))
+
+
+def _prop(prob, N, **kw):
+    A, Bm, Q, R, R_inv, z0, QT = prob
+    return ref_hs.propagator_all_Jt_aug(list(A), list(Bm), list(Q), [R] * N, z0, list(QT),
+                                        T_use=N, R_inv_cached=R_inv, **kw)
+
+
+def config5_golden(N=128, base_seed=9000, count=12, T_min=40, T_max=128):
+    """Mixed Segway / Cartpole / Quadrotor shapes (i mod 3) at their TRUE sizes."""
+    J = np.array([_prop(orc.synth_config5_problem(base_seed, i, N), N) for i in range(count)])
+    Tstar = np.array([int(np.argmin(j[T_min - 1:T_max]) + T_min) for j in J])
+    np.savez_compressed(os.path.join(HERE, "config5_mixed_N128.npz"), N=N, base_seed=base_seed,
+                        count=count, T_min=T_min, T_max=T_max, J=J, T_star=Tstar)
+    print(f"config5_mixed_N128: T*={Tstar}")
+
+
+def lu_slot_cases(seed=9500):
+    """chol_inv's LU fallback (utils.py:88-93, np.linalg.solve = gesv with partial
+    pivoting) on NON-diagonal indefinite blocks, alone and inside a propagator
+    sweep: Q_k of problem 0 at step 3 and QT of problem 1 at step 5 are replaced by
+    symmetric indefinite matrices whose eigenvalues lie in [-3, -0.5] u [0.5, 3]
+    (Cholesky fails for every jitter up to 1e-2)."""
+    rng = np.random.default_rng(seed)
+    d = {}
+
+    def indef(s):
+        Qm, _ = np.linalg.qr(rng.standard_normal((s, s)))
+        ev = rng.uniform(0.5, 3.0, s) * np.where(np.arange(s) % 2 == 0, 1.0, -1.0)
+        return Qm @ np.diag(ev) @ Qm.T
+
+    for s in (3, 5, 13):
+        M = indef(s)
+        d[f"inv_s{s}_in"] = M
+        d[f"inv_s{s}_out"] = ref_utils.chol_inv(M)
+    for tag, s, m, N in (("s13_m4_N20", 13, 4, 20), ("s5_m1_N20", 5, 1, 20)):
+        probs = [list(orc.synth_lft_problem(seed + 10 + i, s, m, N)) for i in range(3)]
+        probs[0][2] = probs[0][2].copy()
+        probs[0][2][3] = indef(s)
+        probs[1][6] = probs[1][6].copy()
+        probs[1][6][5] = indef(s)
+        d[f"lft_{tag}_Q03"] = probs[0][2][3]
+        d[f"lft_{tag}_QT15"] = probs[1][6][5]
+        d[f"lft_{tag}_J"] = np.array([_prop(tuple(p), N) for p in probs])
+        d[f"lft_{tag}_base_seed"] = seed + 10
+    np.savez_compressed(os.path.join(HERE, "lu_slot_cases.npz"), **d)
+    print("lu_slot_cases:", sorted(d))
+
+
+LEGACY_CASES = ("DoubleIntegrator", "Segway_Balance", "Ballbot_Balance", "Quadrotor_Hover")
+
+
+def legacy_plots(case):
+    """The legacy twin (ilqr_propagator.py) exactly as its main() runs it
+    (ilqr_propagator.py:759-781): capture the FINAL brute-force curve call of the
+    'bruteforce' run (ilqr_propagator.py:636, the J_bruteforce column of
+    plots/<case>_Jt.csv) and the final propagator call of the 'propagator' run
+    (ilqr_propagator.py:641, J_propagator), inputs and outputs, next to the CSV
+    columns the reference committed."""
+    import csv
+    import ilqr_propagator as leg
+    makers = {"DoubleIntegrator": leg.make_double_integrator, "Segway_Balance": leg.make_segway,
+              "Ballbot_Balance": leg.make_ballbot, "Quadrotor_Hover": leg.make_quadrotor}
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx = makers[case]()
+    d = dict(N=N, T_min=T_min, T_max=T_max, alpha=alpha, w=w, Q=Q, R=R, xg=xg, u_ref=u_ref,
+             wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64))
+    real_bf, real_prop = leg.bruteforce_all_Jt_backward_expansion, leg.propagator_all_Jt_aug
+    calls = []
+
+    def bf_spy(A_list, B_list, X, U, *a, **k):
+        J = real_bf(A_list, B_list, X, U, *a, **k)
+        calls.append(("bf", dict(A=np.array(A_list), B=np.array(B_list), X=np.array(X),
+                                 U=np.array(U), J=np.array(J))))
+        return J
+
+    def prop_spy(A_aug, B_aug, Q_aug, R_list, z0, QT, T_use=None, R_inv_cached=None):
+        J = real_prop(A_aug, B_aug, Q_aug, R_list, z0, QT, T_use=T_use, R_inv_cached=R_inv_cached)
+        calls.append(("prop", dict(A=np.array(A_aug[:T_use]), B=np.array(B_aug[:T_use]),
+                                   Q=np.array(Q_aug[:T_use]), QT=np.array(QT[:T_use]),
+                                   z0=np.array(z0), R_inv=np.array(R_inv_cached),
+                                   J=np.array(J))))
+        return J
+
+    leg.bruteforce_all_Jt_backward_expansion, leg.propagator_all_Jt_aug = bf_spy, prop_spy
+    try:
+        res = {}
+        for method in ("propagator", "bruteforce"):
+            calls.clear()
+            res[method] = leg.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max,
+                                           method=method, max_iter=20, lm_init=1e-3,
+                                           S_window=10, wrap_idx=wrap_idx, use_central_diff=True)
+            bf = [c for kind, c in calls if kind == "bf"][-1]
+            pr = [c for kind, c in calls if kind == "prop"][-1]
+            if method == "bruteforce":
+                for key in ("A", "B", "X", "U", "J"):
+                    d[f"bf_{key}"] = bf[key]
+            else:
+                for key in ("A", "B", "Q", "QT", "z0", "R_inv", "J"):
+                    d[f"prop_{key}"] = pr[key]
+            d[f"{method}_T_star"] = int(res[method]["T_star"])
+            d[f"{method}_J_star"] = float(res[method]["J_hist"][-1])
+    finally:
+        leg.bruteforce_all_Jt_backward_expansion, leg.propagator_all_Jt_aug = real_bf, real_prop
+    with open(os.path.join(REF, "plots", f"{case}_Jt.csv")) as f:
+        rows = list(csv.DictReader(f))
+    d["csv_J_bruteforce"] = np.array([float(r["J_bruteforce"]) for r in rows])
+    d["csv_J_propagator"] = np.array([float(r["J_propagator"]) for r in rows])
+    with open(os.path.join(REF, "plots", "summary.csv")) as f:
+        for r in csv.DictReader(f):
+            if r["case"] == case and r["method"] in ("propagator", "bruteforce"):
+                d[f"csv_{r['method']}_T_star"] = int(r["T_star"])
+                d[f"csv_{r['method']}_J_star"] = float(r["J_star"])
+    np.savez_compressed(os.path.join(HERE, f"plots_{case}.npz"), **d)
+    rel = np.max(np.abs(d["bf_J"] - d["csv_J_bruteforce"]) / np.abs(d["csv_J_bruteforce"]))
+    print(f"plots_{case}: T*={d['bruteforce_T_star']}/{d['csv_bruteforce_T_star']} "
+          f"bf vs csv {rel:.2e}")
+
+
+def main_r2():
+    np.seterr(all="ignore")
+    synthetic_lft_wide("s13_m4_N100", 13, 4, 100, 11000, 16, 40, 100)
+    synthetic_lft_wide("s13_m4_N128", 13, 4, 128, 12000, 16, 40, 128)
+    synthetic_lft_wide("s5_m1_N200", 5, 1, 200, 13000, 16, 20, 200)
+    synthetic_lft_wide("s3_m1_N50", 3, 1, 50, 14000, 16, 10, 50)
+    config5_golden()
+    lu_slot_cases()
+    for case in LEGACY_CASES:
+        legacy_plots(case)
+
+
 if __name__ == "__main__":
-    if "--traj" in sys.argv:  # only the trajectory-form fixtures
+    if "--r2" in sys.argv:  # round-2 fixtures only
+        main_r2()
+    elif "--traj" in sys.argv:  # only the trajectory-form fixtures
         main_traj()
     elif "--lin" in sys.argv:  # only the dynamics / linearisation fixtures
         main_lin()

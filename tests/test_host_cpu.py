@@ -538,3 +538,30 @@ def test_traj_entry_validation_and_workspace_query(lib):
     need = ws(7, 30, 15, 6, 8, 0)
     assert need >= 8 * steps * (3 * s * s + s * m)
     assert ws(0, 30, 15, 6, 8, 0) == 0
+
+
+def test_block_decoupled_packing_matches_oracle_embedding():
+    """packing.pack_mixed (torch, device-agnostic plumbing) builds exactly the
+    oracle's block-decoupled embedding, and the embedded problems keep their
+    true-shape J."""
+    import torch
+    from time_opt_ilqr_amd.packing import pack_mixed
+    N = 9
+    probs = [orc.synth_config5_problem(300, i, N) for i in range(7)]
+    groups = []
+    for g in range(3):
+        mem = [p for i, p in enumerate(probs) if i % 3 == g]
+        t = lambda j: torch.as_tensor(np.stack([p[j] for p in mem]))  # noqa: E731
+        groups.append((t(0), t(1), t(2), t(4), torch.as_tensor(mem[0][5]), t(6)))
+    mb = pack_mixed(groups, np.arange(7) % 3, 13, 4)
+    for i, p in enumerate(probs):
+        A, Bm, Q, R, Ri, z0, QT = p
+        ref = orc.embed_block_decoupled(A, Bm, Q, Ri, z0, QT, 13, 4)
+        got = (mb.A[i], mb.B[i], mb.Q[i], mb.R_inv[i], mb.z0[i], mb.QT[i])
+        for a, b in zip(got, ref):
+            assert np.array_equal(a.numpy(), b)
+        J0 = orc.lft_sweep(A, Bm, Q, Ri, z0, QT)["J"]
+        J1 = orc.lft_sweep(*ref)["J"]
+        assert np.max(np.abs(J1 - J0) / J0) <= 1e-12
+    assert mb.true_s.tolist() == [5, 5, 13, 5, 5, 13, 5]
+    assert mb.true_m.tolist() == [1, 1, 4, 1, 1, 4, 1]

@@ -35,3 +35,24 @@ def device_batch(batch: int, s: int, m: int, N: int, *, seed: int = 0, device=No
     z0[-1] = 1.0
     out = (A, Bm, Q, Rinv, z0, QT)
     return tuple(t.to(dtype).contiguous() for t in out)
+
+
+CONFIG5_KINDS = (("segway", 5, 1), ("cartpole", 5, 1), ("quadrotor", 13, 4))
+
+
+def config5_batch(batch: int, N: int = 128, *, seed: int = 0, device=None, dtype=None,
+                  s_out: int = 13, m_out: int = 4):
+    """Config 5: member i is Segway- / Cartpole- / Quadrotor-shaped
+    by i mod 3, each drawn at its true (s, m) with ``device_batch`` and embedded
+    block-decoupled into (s_out, m_out) (packing.pack_mixed).  Returns
+    (MixedBatch, groups) where groups holds the true-shape tensors (for spot
+    checks against the oracle)."""
+    import torch
+    from .packing import pack_mixed
+    order = torch.arange(batch) % 3
+    groups = []
+    for g, (_, s, m) in enumerate(CONFIG5_KINDS):
+        cnt = int((order == g).sum())
+        groups.append(device_batch(max(cnt, 1), s, m, N, seed=seed * 7 + 101 * g, device=device,
+                                   dtype=dtype))
+    return pack_mixed(groups, order, s_out, m_out), groups
