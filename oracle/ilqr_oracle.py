@@ -122,11 +122,21 @@ def forward_linesearch(sys_id, dt, X, U, xg, u_ref, Q, R, Qf, w, T_star, k_list,
 
 def ilqr_timeopt(sys_id, dt, x0, xg, u_ref, Q, R, Qf, w, N, T_min, T_max, max_iter=15,
                  lm_init=1e-3, wrap_idx=None, central=True, obstacles=None,
-                 alphas=ALPHAS):
+                 alphas=ALPHAS, U_init=None):
     """solver.py:449-765, method="propagator" (augmentation with the default
-    q_reg 1e-9 / rho_reg 1e-12, the propagator J curve at T_use = T_max)."""
+    q_reg 1e-9 / rho_reg 1e-12, the propagator J curve at T_use = T_max).
+    U_init as solver.py:480-490 (1-D = one control per step, padded with its
+    last row, truncated to N)."""
     extra = _extra_fn(obstacles)
-    U = np.tile(np.asarray(u_ref, dtype=float).reshape(1, -1), (N, 1))
+    if U_init is None:
+        U = np.tile(np.asarray(u_ref, dtype=float).reshape(1, -1), (N, 1))
+    else:
+        U = np.asarray(U_init, dtype=float)
+        if U.ndim == 1:
+            U = U.reshape(-1, 1)
+        if U.shape[0] < N:
+            U = np.vstack([U, np.tile(U[-1:], (N - U.shape[0], 1))])
+        U = U[:N]
     X = rollout(sys_id, dt, x0, U)
     J_hist, T_hist = [], []
     lm = float(lm_init)

@@ -391,7 +391,7 @@ def ilqr_capture(tag, maker, maker_kwargs, T_min, T_max, max_iter, central, keep
              wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64),
              X0=ref_solver.rollout(F, x0, U0), X=sol["X"], U=sol["U"],
              J_hist=np.array(sol["J_hist"]), T_hist=np.array(sol["T_hist"]),
-             T_star=int(sol["T_star"]), n_fwd=len(calls))
+             T_star=int(sol["T_star"]), n_fwd=len(calls), J_curve=np.array(sol["J_curve"]))
     for i, c in enumerate(calls):
         for key, v in c.items():
             d[f"f{i}_{key}"] = v
@@ -570,6 +570,38 @@ def legacy_plots(case):
           f"bf vs csv {rel:.2e}")
 
 
+def legacy_twin_cases(seed=9700):
+    """The legacy twin's chol_inv (ilqr_propagator.py:21-31: 4 tries, then
+    np.linalg.inv at eps = 1e-5) inside its propagator (ilqr_propagator.py:209-232):
+    problem 0 has a Q block that needs the 3rd jitter (min eigenvalue -5e-8),
+    problem 1 a QT block that exhausts the 4 tries (non-diagonal, indefinite),
+    problem 2 is clean."""
+    import ilqr_propagator as leg
+    rng = np.random.default_rng(seed)
+    d = {}
+    for tag, s, m, N in (("s13_m4_N20", 13, 4, 20), ("s5_m1_N20", 5, 1, 20)):
+        probs = [list(orc.synth_lft_problem(seed + 10 + i, s, m, N)) for i in range(3)]
+        Qb = probs[0][2][4].copy()
+        Qb = Qb - np.eye(s) * (np.linalg.eigvalsh(Qb).min() + 5e-8)
+        probs[0][2] = probs[0][2].copy()
+        probs[0][2][4] = Qb
+        Qm, _ = np.linalg.qr(rng.standard_normal((s, s)))
+        ev = rng.uniform(0.5, 3.0, s) * np.where(np.arange(s) % 2 == 0, 1.0, -1.0)
+        probs[1][6] = probs[1][6].copy()
+        probs[1][6][7] = Qm @ np.diag(ev) @ Qm.T
+        d[f"{tag}_Q04"] = Qb
+        d[f"{tag}_QT17"] = probs[1][6][7]
+        d[f"{tag}_base_seed"] = seed + 10
+        J = []
+        for p in probs:
+            A, Bm, Q, R, R_inv, z0, QT = p
+            J.append(leg.propagator_all_Jt_aug(list(A), list(Bm), list(Q), [R] * N, z0, list(QT),
+                                               T_use=N, R_inv_cached=R_inv))
+        d[f"{tag}_J"] = np.array(J)
+    np.savez_compressed(os.path.join(HERE, "legacy_twin_cases.npz"), **d)
+    print("legacy_twin_cases:", sorted(d))
+
+
 def main_r2():
     np.seterr(all="ignore")
     synthetic_lft_wide("s13_m4_N100", 13, 4, 100, 11000, 16, 40, 100)
@@ -578,6 +610,7 @@ def main_r2():
     synthetic_lft_wide("s3_m1_N50", 3, 1, 50, 14000, 16, 10, 50)
     config5_golden()
     lu_slot_cases()
+    legacy_twin_cases()
     for case in LEGACY_CASES:
         legacy_plots(case)
 
@@ -585,6 +618,9 @@ def main_r2():
 if __name__ == "__main__":
     if "--r2" in sys.argv:  # round-2 fixtures only
         main_r2()
+    elif "--legacy" in sys.argv:
+        np.seterr(all="ignore")
+        legacy_twin_cases()
     elif "--traj" in sys.argv:  # only the trajectory-form fixtures
         main_traj()
     elif "--lin" in sys.argv:  # only the dynamics / linearisation fixtures

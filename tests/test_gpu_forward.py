@@ -197,6 +197,14 @@ def test_ilqr_outer_loop_vs_reference(dev, golden_dir, tag):
     assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= tol
     assert sol["T_star"] == int(d["T_star"])
     assert _rel(np.nan_to_num(sol["X"]), np.nan_to_num(d["X"])) <= 100 * tol
+    # the last select's J curve (solver.py:751-762), as the reference driver plots it;
+    # these real terminal blocks are ill-conditioned: real-capture bar
+    assert sol["J_curve"].shape == d["J_curve"].shape
+    jc_tol = 1e-3 if tag in ("di", "pointmass") else 5e-2
+    fin = np.isfinite(d["J_curve"])
+    assert np.array_equal(np.isfinite(sol["J_curve"]), fin)
+    assert np.max(np.abs(sol["J_curve"][fin] - d["J_curve"][fin]) /
+                  np.abs(d["J_curve"][fin])) <= jc_tol
 
 
 def test_ilqr_batch_mixed_problems_vs_oracle(dev):
@@ -265,3 +273,40 @@ def test_linesearch_nondefault_wrap_vs_oracle(dev, golden_dir, wrap):
     Jg = float(r.J[0])
     assert abs(Jg - Jo) <= 1e-12 * max(1.0, abs(Jo)) or (np.isinf(Jo) and np.isinf(Jg))
     assert _rel(_np(r.U[0]), Uo) <= 1e-11
+
+
+def test_dropin_input_shapes_like_the_reference(dev):
+    """Reference input conventions the drop-ins keep:
+    a 1-D U_init on an m=1 system is one control per step (solver.py:484-485);
+    a [1, N, m] U_init is shared by a batch; cost_timeopt_true reads only
+    X[:T+1] and U[:T] (solver.py:80-102); a per-problem Qf is rejected, never
+    symmetrised across problems; timers are the reference's four keys and NaN
+    when the stages are not synchronised."""
+    import torch
+    from time_opt_ilqr_amd import solver, systems
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, _ = \
+        systems.make_double_integrator(N=50)
+    U1 = 0.05 * np.sin(np.arange(40))
+    sol = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, 50, 10, 50, U_init=U1,
+                              max_iter=3, use_central_diff=False)
+    o = io.ilqr_timeopt(0, F.dt, x0, xg, u_ref, Q, R, np.asarray(io.orc.terminal_weight(alpha, 2)),
+                        w, 50, 10, 50, max_iter=3, central=False,
+                        U_init=U1)
+    assert sol["T_hist"] == o["T_hist"]
+    assert sorted(sol["timers"]) == ["backward", "forward", "linearize", "select"]
+    Qf = np.asarray(io.orc.terminal_weight(alpha, 2))
+    X0 = np.stack([x0, x0 + 0.3])
+    res = solver.ilqr_timeopt_batch(0, X0, xg, u_ref, Q, R, Qf, w, 50, 10, 50, dt=F.dt,
+                                    U_init=U1.reshape(1, -1, 1), max_iter=2,
+                                    use_central_diff=False, stage_timers=False)
+    assert all(np.isnan(v) for v in res["timers"].values())
+    assert res["J_curve"].shape == (2, 50)
+    with pytest.raises(ValueError):
+        solver.ilqr_timeopt_batch(0, X0, xg, u_ref, Q, R, np.stack([Qf, Qf]), w, 50, 10, 50,
+                                  dt=F.dt, max_iter=1)
+    X, U = sol["X"], sol["U"]
+    T = sol["T_star"]
+    full = solver.cost_timeopt_true(X, U, xg, u_ref, Q, R, alpha, w, T)
+    short = solver.cost_timeopt_true(X[:T + 1], U[:T], xg, u_ref, Q, R, alpha, w, T)
+    assert full == short
+    del torch

@@ -98,19 +98,33 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     if R_np is None:
         raise ValueError("R must be one [m, m] matrix shared by the batch")
     R_inv = tt(chol_inv(_sym(R_np)))
-    P = tt(_sym(Qf_t.cpu().numpy()))
+    if Qf_t.dim() != 2:
+        raise ValueError("Qf must be one [n, n] terminal weight shared by the batch "
+                         "(as_terminal_weight(alpha))")
+    P = 0.5 * (Qf_t + Qf_t.transpose(-1, -2))  # _sym on the device
     obs = None if obstacles is None or len(obstacles) == 0 else tt(obstacles)
     cost = engine.CostParams(xg_t, ur_t, Q_t, R_t, Qf_t, float(w), obs, wrap_idx)
     if U_init is None:
         U = ur_t.reshape(-1, m).expand(Bn, m)[:, None, :].expand(Bn, N, m).contiguous()
     else:
         U = tt(U_init)
+        if U.dim() == 1:  # solver.py:484-485: a 1-D U_init is one control per step
+            U = U.reshape(-1, 1)
         if U.dim() == 2:
-            U = U[None].expand(Bn, -1, -1)
+            U = U[None]
+        if U.dim() != 3 or U.shape[-1] != m or U.shape[0] not in (1, Bn):
+            raise ValueError(f"U_init must be [N', {m}] or [B or 1, N', {m}]")
+        U = U.expand(Bn, -1, -1)
         if U.shape[1] < N:  # pad with the last control, as the reference does
             U = torch.cat([U, U[:, -1:].expand(Bn, N - U.shape[1], m)], 1)
         U = U[:, :N].contiguous()
-    timers = {"rollout": 0.0, "linearize": 0.0, "select": 0.0, "backward": 0.0, "forward": 0.0}
+    # the reference's four timers (solver.py:497); its initial rollout is untimed and
+    # is reported separately here.  Without stage_timers the stages are not
+    # synchronised, so their times are unknown: NaN, not 0.
+    nan = float("nan")
+    timers = {k: (0.0 if stage_timers else nan)
+              for k in ("linearize", "select", "backward", "forward")}
+    t_rollout = 0.0 if stage_timers else nan
 
     def clock(key, t0):
         if stage_timers:
@@ -119,7 +133,9 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
 
     t0 = time.perf_counter()
     X = engine.rollout(sid, x0, U, dt)
-    clock("rollout", t0)
+    if stage_timers:
+        torch.cuda.synchronize(dev)
+        t_rollout = time.perf_counter() - t0
     H = int(max_iter) + 1
     st = IlqrState(X, U, torch.full((Bn,), float(lm_init), dtype=f64, device=dev),
                    torch.zeros((Bn,), dtype=torch.int32, device=dev),
@@ -129,6 +145,8 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
                    torch.zeros((Bn,), dtype=torch.int32, device=dev),
                    torch.zeros((Bn,), dtype=torch.int32, device=dev))
     bad = _lib.ST_FAIL | _lib.ST_NONFINITE
+    # the last select's J curve of every problem (solver.py:751-762 returns it)
+    J_curve = torch.full((Bn, T_max), float("nan"), dtype=f64, device=dev)
 
     def iterate(s, warm):
         """one update (solver.py:541-553 when warm, else 578-752) of the problems in s"""
@@ -166,7 +184,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
             s.T_bar.copy_(T_star)
         s.X, s.U = fw.X, fw.U
         clock("forward", t0)
-        return sel.status
+        return sel.status, sel.J
 
     # Problems that met the stop rule (or whose select raised) leave the batch: the
     # remaining ones are gathered into a compact batch, so finished problems cost
@@ -174,7 +192,9 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     # launch every iteration).  Needs the cost blocks shared by the batch.
     compact = all(t.dim() == d for t, d in ((xg_t, 1), (ur_t, 1), (Q_t, 2), (Qf_t, 2)))
     fields = ("X", "U", "lm", "T_bar", "J_hist", "T_hist", "n_hist", "done", "crashed")
-    status_log = [iterate(st, True)]
+    stat, J_sel = iterate(st, True)
+    J_curve.copy_(J_sel)
+    status_log = [stat]
     iters = 0
     for _ in range(int(max_iter)):
         live = st.done == 0
@@ -182,13 +202,16 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         if n_live == 0:
             break
         if n_live == Bn or not compact:
-            status_log.append(iterate(st, False))
+            stat, J_sel = iterate(st, False)
+            J_curve[live] = J_sel[live]  # problems that had stopped ran no select
+            status_log.append(stat)
         else:
             idx = live.nonzero()[:, 0]
             sub = IlqrState(*[getattr(st, f).index_select(0, idx) for f in fields])
-            stat = iterate(sub, False)
+            stat, J_sel = iterate(sub, False)
             for f in fields:
                 getattr(st, f).index_copy_(0, idx, getattr(sub, f))
+            J_curve.index_copy_(0, idx, J_sel)
             status_log.append(torch.zeros((Bn,), dtype=stat.dtype, device=dev)
                               .index_copy_(0, idx, stat))
         iters += 1
@@ -197,7 +220,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     T_out = torch.where(nh > 0, st.T_hist.gather(1, last[:, None])[:, 0], st.T_bar)
     return dict(X=st.X, U=st.U, J_hist=st.J_hist, T_hist=st.T_hist, n_hist=nh, T_star=T_out,
                 crashed=st.crashed, lm=st.lm, iterations=iters, timers=timers,
-                select_status=torch.stack(status_log, 1))
+                t_rollout=t_rollout, J_curve=J_curve, select_status=torch.stack(status_log, 1))
 
 
 # ---------------------------------------------------------------------------
@@ -258,8 +281,8 @@ def cost_timeopt_true(X, U, xg, u_ref, Q, R, alpha, w, T_star, wrap_idx=None,
         raise IndexError("index out of range")
     sid = _system_for(system, X.shape[1], U.shape[1])
     cost = _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost)
-    N = len(U)
-    J = engine.cost_true(sid, _t(X[:N + 1])[None], _t(U)[None], [T], cost)
+    # the reference reads only X[:T+1] and U[:T] (solver.py:80-102)
+    J = engine.cost_true(sid, _t(X[:T + 1])[None], _t(U[:T])[None], [T], cost)
     return float(J[0].item())
 
 
@@ -323,7 +346,8 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
     return {"X": res["X"][0].cpu().numpy(), "U": res["U"][0].cpu().numpy(),
             "J_hist": [float(v) for v in res["J_hist"][0, :nh].cpu().numpy()],
             "T_hist": [int(v) for v in res["T_hist"][0, :nh].cpu().numpy()],
-            "timers": res["timers"], "J_curve": None, "T_star": int(res["T_star"][0].item()),
+            "timers": res["timers"], "J_curve": res["J_curve"][0].cpu().numpy(),
+            "T_star": int(res["T_star"][0].item()),
             "onepass_error": None}
 
 
