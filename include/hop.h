@@ -52,6 +52,32 @@ int hop_abi_version(void);
 const char* hop_last_error(void);
 
 /*
+ * Test / diagnostic controls.  Not part of any reference interface and never
+ * needed by a caller: every entry point runs its default kernels with all flags
+ * 0.  Process-wide, read by the dispatchers at launch time (no environment
+ * variables are consulted); set from one host thread between launches.
+ *   HOP_OPT_FORCE_GENERIC   every sweep / Riccati pass on the generic kernels
+ *                           (lft_sweep.hip, riccati.hip): the fast paths'
+ *                           cross-check
+ *   HOP_OPT_FORCE_HANDOVER  the conditioned-prefix kernels hand EVERY problem to
+ *                           their rerun launch (tests the hand-over path)
+ *   HOP_OPT_REFERENCE_ASSOC s = 13 fp64 / fp32: only the reference-association
+ *                           kernel (no conditioned prefix)
+ *   HOP_OPT_TRAJ_UNFUSED    trajectory form through hop_augment + the sweep
+ *   HOP_OPT_STAMPS          section-stamped instantiations (developer builds)
+ * `variant` selects an A/B schedule; only developer builds (HOP_DEV_BUILD=1 at
+ * build time, hop_build_flags() & 1) compile them -- product builds return
+ * HOP_E_ARG for variant != 0 or HOP_OPT_STAMPS.
+ */
+#define HOP_OPT_FORCE_GENERIC 1u
+#define HOP_OPT_FORCE_HANDOVER 2u
+#define HOP_OPT_REFERENCE_ASSOC 4u
+#define HOP_OPT_TRAJ_UNFUSED 8u
+#define HOP_OPT_STAMPS 16u
+int hop_set_options(uint32_t flags, int32_t variant);
+int hop_build_flags(void); /* bit 0: developer build (A/B schedules and stamps compiled) */
+
+/*
  * hop_lft_sweep_f64 / _f32
  * Replaces propagator_all_Jt_aug(A_aug, B_aug, Q_aug, R_list, z0, QT_aug_list,
  *                                T_use, R_inv_cached)

@@ -329,12 +329,16 @@ def test_real_DI_dropins(dev, golden_dir):
 
 
 @pytest.mark.parametrize("schedule", ["2", "8", "10", "12", "14", "30", "40"])
-def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch, schedule):
-    """Every schedule of the exact-size fp64 kernel (LDS-DMA streamed, s=13/m=4:
-    2 select pivots, 8 offset-form C++ chain, 10 hand-scheduled asm sweep) and
-    the generic kernel agree, including the jitter / LU retry paths and batch tails."""
-    from time_opt_ilqr_amd import engine
-    monkeypatch.setenv("HOP_LFT_VARIANT", schedule)
+def test_lft_fast_path_matches_generic_kernel(dev, schedule):
+    """Every schedule of the exact-size fp64 kernel (LDS-DMA streamed, s=13/m=4)
+    and the generic kernel agree, including the jitter / LU retry paths and batch
+    tails.  Product builds carry the default (40: conditioned prefix + rerun) and
+    the reference association (30, HOP_OPT_REFERENCE_ASSOC); the A/B schedules
+    (2 select pivots, 8 offset-form C++ chain, 10/12/14 hand-scheduled asm) exist
+    only in developer builds."""
+    from time_opt_ilqr_amd import _lib, engine
+    if schedule not in ("30", "40") and not _lib.dev_build():
+        pytest.skip("A/B schedule: developer builds only (HOP_DEV_BUILD=1)")
     Bn, s, m, N = 37, 13, 4, 30
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(700, Bn, s, m, N)
     Q = Q.copy()
@@ -343,10 +347,12 @@ def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch, schedule):
     QT = QT.copy()
     QT[36, 2] = QT[36, 2] - np.eye(s) * (np.linalg.eigvalsh(QT[36, 2]).min() + 5e-6)
     args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
-    fast = engine.propagate(*args, t_min=5, t_max=30)
-    monkeypatch.setenv("HOP_FORCE_GENERIC", "1")
-    gen = engine.propagate(*args, t_min=5, t_max=30)
-    monkeypatch.delenv("HOP_FORCE_GENERIC")
+    kw = dict(reference_assoc=True) if schedule == "30" else (
+        {} if schedule == "40" else dict(variant=int(schedule)))
+    with _lib.options(**kw):
+        fast = engine.propagate(*args, t_min=5, t_max=30)
+    with _lib.options(force_generic=True):
+        gen = engine.propagate(*args, t_min=5, t_max=30)
     st_f, st_g = fast.status.cpu().numpy(), gen.status.cpu().numpy()
     assert st_f.tolist() == st_g.tolist()
     assert st_f[3] & orc.ST_JITTER and st_f[20] & orc.ST_LU and st_f[36] & orc.ST_JITTER
@@ -361,12 +367,12 @@ def test_lft_fast_path_matches_generic_kernel(dev, monkeypatch, schedule):
 
 @pytest.mark.parametrize("s,m,dt,tol", [(5, 1, "f32", 2e-3), (3, 1, "f64", 1e-10),
                                         (4, 2, "f64", 1e-10)])
-def test_lft_small_path_matches_generic_and_oracle(dev, monkeypatch, s, m, dt, tol):
+def test_lft_small_path_matches_generic_and_oracle(dev, s, m, dt, tol):
     """The one-problem-per-lane kernel (lft_small.hip, s <= 5) agrees with the
     generic kernel and the oracle, including jitter / LU-slot problems and a
     batch that is not a multiple of the 64-lane wave."""
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
     Bn, N = 131, 40
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(900 + s, Bn, s, m, N)
     Q = Q.copy()
@@ -376,9 +382,8 @@ def test_lft_small_path_matches_generic_and_oracle(dev, monkeypatch, s, m, dt, t
     args = [torch.as_tensor(np.ascontiguousarray(x), dtype=td, device=dev)
             for x in (A, Bm, Q, Ri, z0[0], QT)]
     small = engine.propagate(*args, t_min=3, t_max=N)
-    monkeypatch.setenv("HOP_FORCE_GENERIC", "1")
-    gen = engine.propagate(*args, t_min=3, t_max=N)
-    monkeypatch.delenv("HOP_FORCE_GENERIC")
+    with _lib.options(force_generic=True):
+        gen = engine.propagate(*args, t_min=3, t_max=N)
     ss = small.status.cpu().numpy()
     assert ss[7] & orc.ST_JITTER and ss[70] & orc.ST_LU
     ok = [i for i in range(Bn) if i not in (7, 70)]
@@ -393,20 +398,22 @@ def test_lft_small_path_matches_generic_and_oracle(dev, monkeypatch, s, m, dt, t
         assert small.t_star.cpu().numpy()[ok].tolist() == gen.t_star.cpu().numpy()[ok].tolist()
 
 
-def test_cond_kernel_alone_matches_lft_kernel(dev, monkeypatch):
-    """The conditioned-prefix kernel by itself (variant 41: no rerun launch) on
-    clean inputs: no problem handed over (status 0), J within 1e-10 of the
-    reference-association kernel (variant 30) and of the oracle, same T*/J*,
-    batch tail included (B = 53)."""
-    from time_opt_ilqr_amd import engine
+def test_cond_kernel_alone_matches_lft_kernel(dev):
+    """The conditioned-prefix kernel on clean inputs: no problem is handed over
+    (status 0, and the result is NOT bitwise the reference-association kernel's,
+    so the conditioned kernel produced it), J within 1e-10 of the reference
+    association (HOP_OPT_REFERENCE_ASSOC) and of the oracle, same T*/J*, batch
+    tail included (B = 53)."""
+    import torch
+    from time_opt_ilqr_amd import _lib, engine
     Bn, s, m, N = 53, 13, 4, 100
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(4242, Bn, s, m, N)
     args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
-    monkeypatch.setenv("HOP_LFT_VARIANT", "41")
     cnd = engine.propagate(*args, t_min=30, t_max=100)
-    monkeypatch.setenv("HOP_LFT_VARIANT", "30")
-    ref = engine.propagate(*args, t_min=30, t_max=100)
+    with _lib.options(reference_assoc=True):
+        ref = engine.propagate(*args, t_min=30, t_max=100)
     assert cnd.status.cpu().numpy().tolist() == [0] * Bn
+    assert not torch.equal(cnd.J, ref.J)
     assert _elem_rel(cnd.J.cpu().numpy(), ref.J.cpu().numpy()) <= 1e-10
     Jo, _ = orc.lft_sweep_batch(A[:6], Bm[:6], Q[:6], Ri[:6], z0[0], QT[:6])
     assert _elem_rel(cnd.J.cpu().numpy()[:6], Jo) <= 1e-10
@@ -414,68 +421,69 @@ def test_cond_kernel_alone_matches_lft_kernel(dev, monkeypatch):
     assert _elem_rel(cnd.j_star.cpu().numpy(), ref.j_star.cpu().numpy()) <= 1e-10
 
 
-def test_cond_forced_handover_is_the_lft_kernel(dev, monkeypatch):
-    """HOP_COND_FORCE=1 flags every problem: the rerun launch then recomputes the
-    whole batch with the reference association, bitwise equal to variant 30."""
+def test_cond_forced_handover_is_the_lft_kernel(dev):
+    """HOP_OPT_FORCE_HANDOVER flags every problem: the rerun launch then recomputes
+    the whole batch with the reference association, bitwise equal to
+    HOP_OPT_REFERENCE_ASSOC."""
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
     Bn, s, m, N = 21, 13, 4, 40
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(4343, Bn, s, m, N)
     Q = Q.copy()
     Q[4, 7] = -np.eye(s)  # LU slot
     args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
-    monkeypatch.setenv("HOP_LFT_VARIANT", "40")
-    monkeypatch.setenv("HOP_COND_FORCE", "1")
-    f = engine.propagate(*args, t_min=5, t_max=40)
-    monkeypatch.delenv("HOP_COND_FORCE")
-    monkeypatch.setenv("HOP_LFT_VARIANT", "30")
-    r = engine.propagate(*args, t_min=5, t_max=40)
+    with _lib.options(force_handover=True):
+        f = engine.propagate(*args, t_min=5, t_max=40)
+    with _lib.options(reference_assoc=True):
+        r = engine.propagate(*args, t_min=5, t_max=40)
     assert torch.equal(f.J, r.J) and torch.equal(f.status, r.status)
     assert torch.equal(f.t_star, r.t_star) and torch.equal(f.j_star, r.j_star)
     assert int(r.status[4]) & orc.ST_LU
 
 
 @pytest.mark.parametrize("s,m,dt", [(5, 1, "f32"), (3, 1, "f64"), (4, 2, "f64")])
-def test_small_cond_kernel(dev, monkeypatch, s, m, dt):
-    """Small-s COND kernels (opt-in): alone (HOP_SMALL_COND=2) no problem is handed
-    over and J matches the LFT instantiation (HOP_SMALL_COND=0, the default); with
-    HOP_COND_FORCE=1 the rerun launch recomputes every problem bitwise like the LFT
-    instantiation; cond + rerun (1) keeps chol_inv's status bits on a bad block."""
+def test_small_cond_kernel(dev, s, m, dt):
+    """Small-s COND kernels (developer builds, opt-in): alone (variant 62) no
+    problem is handed over and J matches the LFT instantiation (the default); with
+    HOP_OPT_FORCE_HANDOVER the rerun launch recomputes every problem bitwise like
+    the LFT instantiation; cond + rerun (variant 61) keeps chol_inv's status bits
+    on a bad block."""
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
+    if not _lib.dev_build():
+        pytest.skip("small-s conditioned kernels: developer builds only (HOP_DEV_BUILD=1)")
     tdt = torch.float64 if dt == "f64" else torch.float32
     Bn, N = 131, 40
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(5150 + s, Bn, s, m, N)
     Q = Q.copy()
     Q[7, 11] = -np.eye(s)  # LU slot on the LFT path
     args = [_t(x, dev, tdt) for x in (A, Bm, Q, Ri, z0[0], QT)]
-    monkeypatch.setenv("HOP_SMALL_COND", "0")
     ref = engine.propagate(*args, t_min=4, t_max=N)
-    monkeypatch.setenv("HOP_SMALL_COND", "2")
-    alone = engine.propagate(*args, t_min=4, t_max=N)
+    with _lib.options(variant=62):
+        alone = engine.propagate(*args, t_min=4, t_max=N)
     st = alone.status.cpu().numpy()
     assert st[7] == 16 and (np.delete(st, 7) == 0).all()
     ok = [i for i in range(Bn) if i != 7]
     tol = 1e-10 if dt == "f64" else 1e-3
     assert _elem_rel(alone.J.cpu().numpy()[ok], ref.J.cpu().numpy()[ok]) <= tol
-    monkeypatch.setenv("HOP_SMALL_COND", "1")  # cond + rerun (not the default)
-    dflt = engine.propagate(*args, t_min=4, t_max=N)
+    with _lib.options(variant=61):  # cond + rerun (not the default)
+        dflt = engine.propagate(*args, t_min=4, t_max=N)
     assert torch.equal(dflt.status, ref.status) and int(dflt.status[7]) & orc.ST_LU
     assert torch.equal(dflt.J[7], ref.J[7])
-    monkeypatch.setenv("HOP_COND_FORCE", "1")
-    forced = engine.propagate(*args, t_min=4, t_max=N)
+    with _lib.options(variant=61, force_handover=True):
+        forced = engine.propagate(*args, t_min=4, t_max=N)
     assert torch.equal(forced.J, ref.J) and torch.equal(forced.status, ref.status)
     assert torch.equal(forced.t_star, ref.t_star)
 
 
-def test_cond_fp32_blocks_config5_shape(dev, monkeypatch, golden_dir):
+def test_cond_fp32_blocks_config5_shape(dev, golden_dir):
     """fp32 blocks at s=13, m=4 (config 5 shape, N=128): the conditioned kernel reads
     fp32 images and computes in fp64, so J is the reference's to fp32 input rounding
     (2e-5 here; the generic fp32 kernel is at its 2e-3 bar) with T* equal;
-    HOP_COND_FORCE=1 hands every problem to the generic fp32 kernel (bitwise equal
-    to HOP_FORCE_GENERIC); batch tail 5."""
+    HOP_OPT_FORCE_HANDOVER hands every problem to the generic fp32 kernel (bitwise
+    equal to HOP_OPT_FORCE_GENERIC); batch tail 5."""
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
     d = _load(golden_dir, "lft_synth_s13_m4_N128.npz")
     s, m, N, bs, cnt = (int(d[k]) for k in ("s", "m", "N", "base_seed", "count"))
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(bs, cnt, s, m, N)
@@ -487,11 +495,10 @@ def test_cond_fp32_blocks_config5_shape(dev, monkeypatch, golden_dir):
     assert _elem_rel(res.J.cpu().numpy(), d["J"]) <= 2e-5
     assert res.t_star.cpu().numpy().tolist() == d["T_star"].tolist()
     assert int(res.status.abs().sum()) == 0
-    monkeypatch.setenv("HOP_COND_FORCE", "1")
-    forced = engine.propagate(*args, **kw)
-    monkeypatch.delenv("HOP_COND_FORCE")
-    monkeypatch.setenv("HOP_FORCE_GENERIC", "1")
-    gen = engine.propagate(*args, **kw)
+    with _lib.options(force_handover=True):
+        forced = engine.propagate(*args, **kw)
+    with _lib.options(force_generic=True):
+        gen = engine.propagate(*args, **kw)
     assert torch.equal(forced.J, gen.J) and torch.equal(forced.status, gen.status)
     assert _elem_rel(gen.J.cpu().numpy(), d["J"]) <= 2e-3
 

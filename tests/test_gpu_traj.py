@@ -61,11 +61,22 @@ def _oracle(p, rho, n_use=None, extra=None):
 
 
 @pytest.fixture(params=["40", "53"])
-def traj_variant(request, monkeypatch):
+def traj_variant(request):
     """Fused s=13 trajectory kernels: 53 (default) closed-form stage inverses, 40 stage
-    inverses by Gauss-Jordan sweeps on the built images (both + the rerun launch)."""
-    monkeypatch.setenv("HOP_LFT_VARIANT", request.param)
-    return request.param
+    inverses by Gauss-Jordan sweeps on the built images (both + the rerun launch;
+    40 is an A/B schedule of developer builds)."""
+    from time_opt_ilqr_amd import _lib
+    if request.param == "40" and not _lib.dev_build():
+        pytest.skip("A/B schedule: developer builds only (HOP_DEV_BUILD=1)")
+    with _lib.options(variant=40 if request.param == "40" else 0):
+        yield request.param
+
+
+@pytest.fixture
+def unfused():
+    """Context: the trajectory form through hop_augment + the augmented-form sweep."""
+    from time_opt_ilqr_amd import _lib
+    return lambda on=True: _lib.options(traj_unfused=on)
 
 
 def _dev_args(st, dev, dtype=None):
@@ -99,12 +110,15 @@ def test_augment_kernel_matches_oracle_builders(dev, n, m, N, dt):
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_traj_sweep_vs_reference_goldens(dev, golden_dir, monkeypatch, fused, traj_variant):
+def test_traj_sweep_vs_reference_goldens(dev, golden_dir, fused, traj_variant, unfused):
     """s = 13, m = 4: in-kernel builders (fused) and hop_augment + sweep (unfused)
     against the reference's builders + propagator (traj_synth_n12_m4_N100)."""
+    with unfused(not fused):
+        _traj_sweep_vs_reference_goldens(dev, golden_dir)
+
+
+def _traj_sweep_vs_reference_goldens(dev, golden_dir):
     from time_opt_ilqr_amd import engine
-    if not fused:
-        monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
     d = _load(golden_dir, "traj_synth_n12_m4_N100.npz")
     n, m, N = int(d["n"]), int(d["m"]), int(d["N"])
     for rho in (1.0, 1e-12):
@@ -144,15 +158,15 @@ def test_traj_sweep_batch_vs_oracle(dev, monkeypatch, n, m, N, traj_variant):
     assert (res.status.cpu().numpy() == 0).all()
 
 
-def test_traj_fused_equals_unfused(dev, monkeypatch):
+def test_traj_fused_equals_unfused(dev, unfused):
     """The fused builder and hop_augment + the augmented-form sweep agree (1e-10:
     the s=13 augmented-form sweep runs the conditioned-prefix association)."""
     from time_opt_ilqr_amd import engine
     ps, st = _batch(range(970, 1003), 12, 4, 50)
     args = (*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
     a = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
-    monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
-    b = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
+    with unfused():
+        b = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0).J.cpu().numpy()
     assert _rel(a, b) <= 1e-10
 
 
@@ -220,12 +234,15 @@ def test_select_from_trajectory_dropin_DI(dev, golden_dir):
 
 
 @pytest.mark.parametrize("fused", [True, False])
-def test_traj_nonfinite_and_tiny_horizons(dev, monkeypatch, fused, traj_variant):
+def test_traj_nonfinite_and_tiny_horizons(dev, fused, traj_variant, unfused):
     """A NaN in one problem's trajectory flags only that problem (FloatingPointError
     in the reference); n_use = 1 and t_min = t_max work on both paths."""
+    with unfused(not fused):
+        _traj_nonfinite_and_tiny_horizons(dev)
+
+
+def _traj_nonfinite_and_tiny_horizons(dev):
     from time_opt_ilqr_amd import engine
-    if not fused:
-        monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
     n, m, N = 12, 4, 20
     ps, st = _batch(range(1100, 1105), n, m, N)
     X = st["X"].copy()
@@ -251,7 +268,7 @@ def test_traj_nonfinite_and_tiny_horizons(dev, monkeypatch, fused, traj_variant)
 
 @pytest.mark.parametrize("n,m,dt,tol", [(4, 1, "f32", 2e-3), (4, 2, "f32", 2e-3), (3, 2, "f64", 1e-9),
                                         (2, 1, "f64", 1e-9), (1, 1, "f64", 1e-9)])
-def test_traj_small_fused_vs_unfused_and_oracle(dev, monkeypatch, n, m, dt, tol):
+def test_traj_small_fused_vs_unfused_and_oracle(dev, unfused, n, m, dt, tol):
     """Small s: the in-register builders of lft_small_traj_kernel against
     hop_augment + the small-s sweep and against the oracle (tails: 67 problems)."""
     import torch
@@ -263,8 +280,8 @@ def test_traj_small_fused_vs_unfused_and_oracle(dev, monkeypatch, n, m, dt, tol)
             _t(st["w"], dev, dtype))
     kw = dict(wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=N)
     a = engine.propagate_traj(*args, **kw)
-    monkeypatch.setenv("HOP_TRAJ_UNFUSED", "1")
-    b = engine.propagate_traj(*args, **kw)
+    with unfused():
+        b = engine.propagate_traj(*args, **kw)
     Ja, Jb = a.J.double().cpu().numpy(), b.J.double().cpu().numpy()
     assert _rel(Ja, Jb) <= (1e-11 if dt == "f64" else 2e-3)  # fp32: the 2e-3 bar
     for i in (0, 33, 66):
@@ -278,20 +295,69 @@ def test_traj_small_fused_vs_unfused_and_oracle(dev, monkeypatch, n, m, dt, tol)
             assert int(a.t_star[i]) == int(T[0])
 
 
-def test_traj_closed_form_kernel_alone(dev, monkeypatch):
-    """The closed-form trajectory kernel by itself (variant 54, no rerun) against
-    the Gauss-Jordan one (41): nothing handed over at rho_reg = 1, J within 1e-10
-    (their only difference is how Q_aug^-1 and QT_aug^-1 are formed), same T*."""
-    from time_opt_ilqr_amd import engine
+def test_traj_closed_form_kernel_alone(dev):
+    """The closed-form trajectory kernel: nothing handed over at rho_reg = 1 (the
+    result is not bitwise the reference-association kernel's), J within 1e-10 of
+    the reference association (HOP_OPT_REFERENCE_ASSOC) and of the Gauss-Jordan
+    conditioned kernel (variant 41, developer builds), same T*."""
+    import torch
+    from time_opt_ilqr_amd import _lib, engine
     ps, st = _batch(range(1200, 1237), 12, 4, 60)
     args = (*_dev_args(st, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
-    monkeypatch.setenv("HOP_LFT_VARIANT", "54")
-    cf = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=60)
-    monkeypatch.setenv("HOP_LFT_VARIANT", "41")
-    gj = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=60)
+    kw = dict(wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=60)
+    cf = engine.propagate_traj(*args, **kw)
+    with _lib.options(reference_assoc=True):
+        ref = engine.propagate_traj(*args, **kw)
     assert (cf.status.cpu().numpy() == 0).all()
-    assert _rel(cf.J.cpu().numpy(), gj.J.cpu().numpy()) <= 1e-10
-    assert cf.t_star.cpu().tolist() == gj.t_star.cpu().tolist()
+    assert not torch.equal(cf.J, ref.J)
+    assert _rel(cf.J.cpu().numpy(), ref.J.cpu().numpy()) <= 1e-10
+    assert cf.t_star.cpu().tolist() == ref.t_star.cpu().tolist()
+    if _lib.dev_build():
+        with _lib.options(variant=54):
+            cf2 = engine.propagate_traj(*args, **kw)
+        with _lib.options(variant=41):
+            gj = engine.propagate_traj(*args, **kw)
+        assert (cf2.status.cpu().numpy() == 0).all()
+        assert _rel(cf2.J.cpu().numpy(), gj.J.cpu().numpy()) <= 1e-10
     for b in (0, 36):
         _, o = _oracle(ps[b], 1.0)
         assert _rel(cf.J[b].cpu().numpy(), o["J"]) <= 1e-9
+
+
+def test_reference_shaped_augmented_builders(dev):
+    """augmented.build_augmented_sequence_QR / build_terminal_aug_list (the
+    reference's names and return values, augmented.py:10-87) built on the device:
+    against the oracle's builders, with a wrapped state, per-step residuals from
+    the caller's F and an extra stage cost."""
+    from time_opt_ilqr_amd import augmented
+    rng = np.random.default_rng(0)
+    n, m, N = 4, 2, 6
+    A = [np.eye(n) + 0.1 * rng.standard_normal((n, n)) for _ in range(N)]
+    B = [0.1 * rng.standard_normal((n, m)) for _ in range(N)]
+    X = rng.standard_normal((N + 1, n))
+    X[:, 2] *= 5.0
+    U = rng.standard_normal((N, m))
+    xg = rng.standard_normal(n)
+    ur = rng.standard_normal(m)
+    Q = np.diag(rng.uniform(1, 2, n))
+    R = np.diag(rng.uniform(1, 2, m))
+
+    def F(x, u):
+        return 0.9 * x + 0.05 * np.concatenate([u, u])[:n]
+
+    def extra(x, u):
+        return 0.3 * float(x @ x), 0.6 * x, 0.6 * np.eye(n)
+
+    for esc in (None, extra):
+        Aa, Ba, Qa, Rl, z0, Ri = augmented.build_augmented_sequence_QR(
+            F, A, B, X, U, xg, ur, Q, R, 0.03, wrap_idx=[2], extra_stage_cost=esc)
+        res = [F(X[k], U[k]) - X[k + 1] for k in range(N)]
+        oA, oB, oQ, oR, oz, oRi = orc.augment_stage(A, B, res, X, U, xg, ur, Q, R, 0.03,
+                                                     wrap_idx=[2], extra=esc)
+        assert _rel(np.array(Aa), oA) <= 1e-14 and _rel(np.array(Qa), oQ) <= 1e-14
+        assert np.array_equal(np.array(Ba), oB) and np.allclose(Ri, oRi)
+        assert np.array_equal(z0, oz) and len(Rl) == N
+    alpha = np.array([1.0, 2.0, 3.0, 4.0])
+    QT = augmented.build_terminal_aug_list(X, xg, alpha, wrap_idx=[2])
+    oQT = orc.augment_terminal(X, xg, alpha, wrap_idx=[2])
+    assert len(QT) == N and _rel(np.array(QT), oQT) <= 1e-14

@@ -30,7 +30,7 @@ def _header_functions():
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 22
+    assert len(names) == 24
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:
@@ -39,6 +39,24 @@ def test_header_symbols_exported(lib):
     for n in names:
         assert re.search(rf"\bT {n}\b", out), n
     assert lib.hop_abi_version() == 1
+
+
+def test_options_are_explicit_and_product_build_has_no_ab_schedules(lib):
+    """Test/diagnostic controls go through hop_set_options only (no environment
+    variable is read by the library); a product build rejects A/B schedule numbers
+    and stamps, and carries no getenv import."""
+    from time_opt_ilqr_amd import _lib
+    assert lib.hop_build_flags() == 0
+    assert lib.hop_set_options(0, 41) == -1 and b"developer builds" in lib.hop_last_error()
+    assert lib.hop_set_options(_lib.OPT_STAMPS, 0) == -1
+    assert lib.hop_set_options(1 << 9, 0) == -1
+    with _lib.options(force_generic=True):
+        with _lib.options(traj_unfused=True):
+            assert _lib._opts == (_lib.OPT_FORCE_GENERIC | _lib.OPT_TRAJ_UNFUSED, 0)
+        assert _lib._opts == (_lib.OPT_FORCE_GENERIC, 0)
+    assert _lib._opts == (0, 0)
+    out = os.popen(f"nm -D {_lib.LIB_PATH}").read()
+    assert not re.search(r"\bU getenv\b", out)
 
 
 def test_library_is_gfx950_code_object(lib):
@@ -73,33 +91,6 @@ def test_product_path_has_no_cpu_fallback():
     with pytest.raises(HopError):
         engine.propagate(A, torch.zeros((1, 2, 3, 1), dtype=torch.float64), A,
                          torch.eye(1, dtype=torch.float64), torch.zeros(3, dtype=torch.float64), A)
-
-
-def test_augmented_builders_match_oracle():
-    from time_opt_ilqr_amd import augmented
-    rng = np.random.default_rng(0)
-    n, m, N = 4, 2, 6
-    A = [np.eye(n) + 0.1 * rng.standard_normal((n, n)) for _ in range(N)]
-    B = [0.1 * rng.standard_normal((n, m)) for _ in range(N)]
-    X = rng.standard_normal((N + 1, n))
-    U = rng.standard_normal((N, m))
-    xg = rng.standard_normal(n)
-    ur = rng.standard_normal(m)
-    Q = np.diag(rng.uniform(1, 2, n))
-    R = np.diag(rng.uniform(1, 2, m))
-
-    def F(x, u):
-        return 0.9 * x + 0.05 * np.concatenate([u, u])[:n]
-
-    Aa, Ba, Qa, Rl, z0, Ri = augmented.build_augmented_sequence_QR(F, A, B, X, U, xg, ur, Q, R,
-                                                                   0.03, wrap_idx=[2])
-    res = [F(X[k], U[k]) - X[k + 1] for k in range(N)]
-    oA, oB, oQ, oR, oz, oRi = orc.augment_stage(A, B, res, X, U, xg, ur, Q, R, 0.03, wrap_idx=[2])
-    assert np.allclose(np.array(Aa), oA, atol=1e-15) and np.allclose(np.array(Qa), oQ, atol=1e-15)
-    assert np.allclose(np.array(Ba), oB) and np.allclose(Ri, oRi) and np.array_equal(z0, oz)
-    QT = augmented.build_terminal_aug_list(X, xg, np.array([1.0, 2.0, 3.0, 4.0]), wrap_idx=[2])
-    oQT = orc.augment_terminal(X, xg, np.array([1.0, 2.0, 3.0, 4.0]), wrap_idx=[2])
-    assert np.allclose(np.array(QT), oQT, atol=1e-15)
 
 
 def test_wrap_and_terminal_weight():

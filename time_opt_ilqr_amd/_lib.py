@@ -7,6 +7,7 @@ fallback: without the built library or a GPU every entry point raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -47,6 +48,8 @@ _COST = [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _
 SIGNATURES = {
     "hop_abi_version": (C.c_int, []),
     "hop_last_error": (C.c_char_p, []),
+    "hop_set_options": (C.c_int, [_U32, _I32]),
+    "hop_build_flags": (C.c_int, []),
     "hop_lft_sweep_f64": (C.c_int, _LFT),
     "hop_lft_sweep_f32": (C.c_int, _LFT),
     "hop_select_horizon_f64": (C.c_int, _SEL),
@@ -103,6 +106,47 @@ def load(path: str | None = None):
         if path is None:
             _lib = lib
         return lib
+
+
+# test / diagnostic controls (include/hop.h HOP_OPT_*); never needed by a caller
+OPT_FORCE_GENERIC = 1
+OPT_FORCE_HANDOVER = 2
+OPT_REFERENCE_ASSOC = 4
+OPT_TRAJ_UNFUSED = 8
+OPT_STAMPS = 16
+
+
+def dev_build() -> bool:
+    """True when libhop_amd.so is a developer build (A/B schedules, stamps)."""
+    return bool(load().hop_build_flags() & 1)
+
+
+@contextlib.contextmanager
+def options(*, force_generic=None, force_handover=None, reference_assoc=None,
+            traj_unfused=None, stamps=None, variant=None):
+    """Set hop_set_options for the duration of a `with` block (tests, tools).
+    Arguments left at None keep the enclosing block's setting; the previous
+    controls are restored afterwards.  The library reads them at launch."""
+    global _opts
+    prev = _opts
+    flags, var = prev
+    for on, bit in ((force_generic, OPT_FORCE_GENERIC), (force_handover, OPT_FORCE_HANDOVER),
+                    (reference_assoc, OPT_REFERENCE_ASSOC), (traj_unfused, OPT_TRAJ_UNFUSED),
+                    (stamps, OPT_STAMPS)):
+        if on is not None:
+            flags = (flags | bit) if on else (flags & ~bit)
+    if variant is not None:
+        var = int(variant)
+    check(load().hop_set_options(flags, var))
+    _opts = (flags, var)
+    try:
+        yield
+    finally:
+        load().hop_set_options(*prev)
+        _opts = prev
+
+
+_opts = (0, 0)
 
 
 def check(rc: int):

@@ -15,13 +15,24 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
-SOURCES = ["capi.hip", "augment.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip", "lft_small_noslp.hip",
-           "riccati.hip", "linearize.hip", "forward.hip"]
+SOURCES = ["capi.hip", "augment.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip",
+           "riccati.hip", "riccati_fast.hip", "linearize.hip", "forward.hip"]
+# developer builds (HOP_DEV_BUILD=1 or --dev): the A/B schedules, stamped
+# instantiations and the s <= 5 build without SLP vectorisation, selected at run
+# time by hop_set_options' variant number; product builds compile none of them
+DEV = os.environ.get("HOP_DEV_BUILD", "0") not in ("", "0") or "--dev" in sys.argv
+DEV_SOURCES = ["lft_small_noslp.hip"]
+if DEV:  # a separate library (load it with HOP_LIB=<path>): the product .so stays product
+    LIB = os.path.join(HERE, "libhop_amd_dev.so")
 EXTRA = {"lft_small_noslp.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp", "wrap.hpp", "dynamics.hpp"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",
-         "-Wno-unused-but-set-variable"]
+         "-Wno-unused-but-set-variable"] + (["-DHOP_DEV=1"] if DEV else [])
+
+
+def _sources():
+    return SOURCES + (DEV_SOURCES if DEV else [])
 
 
 def _hipcc():
@@ -33,7 +44,7 @@ def _hipcc():
 
 def _digest():
     h = hashlib.sha256()
-    for name in SOURCES + HEADERS:
+    for name in SOURCES + DEV_SOURCES + HEADERS:
         with open(os.path.join(CSRC, name), "rb") as f:
             h.update(f.read())
     with open(os.path.join(REPO, "include", "hop.h"), "rb") as f:
@@ -59,7 +70,7 @@ def check_hazards(objdir, verbose=True):
     write hazard window (tools/check_dpp_hazards.py; hipcc does not pad asm)."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import check_dpp_hazards as chk
-    for src in SOURCES:
+    for src in _sources():
         s = os.path.join(objdir, src.replace(".hip", "") + f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")
         n, bad = chk.check(s)
         if verbose:
@@ -79,11 +90,11 @@ def build(force=False, jobs=None, verbose=True):
             print("[hop] libhop_amd.so up to date")
         return LIB
     hipcc = _hipcc()
-    objdir = os.path.join(HERE, "_obj")
+    objdir = os.path.join(HERE, "_obj_dev" if DEV else "_obj")
     os.makedirs(objdir, exist_ok=True)
     procs = []
     objs = []
-    for src in SOURCES:
+    for src in _sources():
         obj = os.path.join(objdir, src.replace(".hip", ".o"))
         objs.append(obj)
         # -save-temps=obj keeps the device assembly for the DPP hazard check

@@ -9,6 +9,11 @@
 #include "hop_kernels.hpp"
 #include "dynamics.hpp"
 
+namespace hop {
+unsigned g_opt_flags = 0u;
+int g_opt_variant = 0;
+}  // namespace hop
+
 namespace {
 
 thread_local char g_err[512] = "";
@@ -88,7 +93,7 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
     if (e != hipErrorNotSupported) return hip_status(e);
     return fail(HOP_E_SIZE, "no fused trajectory-form sweep for this shape");
   }
-  if (!getenv("HOP_FORCE_GENERIC")) {
+  if (!hop::opt(HOP_OPT_FORCE_GENERIC)) {
     if constexpr (sizeof(T) == 8) {
       const hipError_t e = hop::dispatch_lft_v2(a, (hipStream_t)stream);
       if (e != hipErrorNotSupported) return hip_status(e);
@@ -96,10 +101,13 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
       const hipError_t e = hop::dispatch_lft_v2_f32(a, (hipStream_t)stream);
       if (e != hipErrorNotSupported) return hip_status(e);
     }
-    const char* sv = getenv("HOP_SMALL_VARIANT");  // same-process A/B of the s <= 5 build
-    const hipError_t e = (sv && atoi(sv) == 1)
-                             ? hop::dispatch_lft_small_noslp<T>(a, (hipStream_t)stream)
-                             : hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
+    hipError_t e;
+#ifdef HOP_DEV
+    if (hop::g_opt_variant == 71)  // A/B: the s <= 5 build without SLP vectorisation
+      e = hop::dispatch_lft_small_noslp<T>(a, (hipStream_t)stream);
+    else
+#endif
+      e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
     if (e != hipErrorNotSupported) return hip_status(e);
   }
   return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));
@@ -183,7 +191,7 @@ hop::TrajArgs<T> traj_args(const T* A, const T* Bm, const T* a_res, const T* X, 
 // the sweep builds the blocks itself (no workspace) for these shapes: the
 // exact-size s = 13 kernel (fp64) and the small-s instantiations (lft_small.hip)
 bool traj_fused(int32_t n, int32_t m, int32_t elem_bytes, bool has_extra) {
-  if (getenv("HOP_FORCE_GENERIC") || getenv("HOP_TRAJ_UNFUSED") || has_extra) return false;
+  if (hop::opt(HOP_OPT_FORCE_GENERIC | HOP_OPT_TRAJ_UNFUSED) || has_extra) return false;
   if (elem_bytes == 8 && n == 12 && m == 4) return true;
   const int s = n + 1;
   const bool both = (s == 2 && m == 1) || (s == 3 && m == 1) || (s == 4 && (m == 1 || m == 2));
@@ -251,6 +259,20 @@ int lft_traj_entry(const hop::TrajArgs<T>& t, const T* R_inv, int64_t r_bs, int6
 }  // namespace
 
 extern "C" {
+
+int hop_set_options(uint32_t flags, int32_t variant) {
+  if (flags & ~(HOP_OPT_FORCE_GENERIC | HOP_OPT_FORCE_HANDOVER | HOP_OPT_REFERENCE_ASSOC |
+                HOP_OPT_TRAJ_UNFUSED | HOP_OPT_STAMPS))
+    return fail(HOP_E_ARG, "unknown option flag");
+  if (!hop::kDevBuild && (variant != 0 || (flags & HOP_OPT_STAMPS)))
+    return fail(HOP_E_ARG, "A/B schedules and stamps exist only in developer builds "
+                           "(HOP_DEV_BUILD=1 python -m time_opt_ilqr_amd.build)");
+  hop::g_opt_flags = flags;
+  hop::g_opt_variant = variant;
+  return HOP_OK;
+}
+
+int hop_build_flags(void) { return hop::kDevBuild ? 1 : 0; }
 
 int hop_abi_version(void) { return HOP_ABI_VERSION; }
 const char* hop_last_error(void) { return g_err; }

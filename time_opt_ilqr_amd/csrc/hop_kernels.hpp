@@ -3,6 +3,20 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/hop.h"
+
+namespace hop {
+// test / diagnostic controls (hop_set_options, include/hop.h); 0 = product defaults
+extern unsigned g_opt_flags;
+extern int g_opt_variant;
+inline bool opt(unsigned f) { return (g_opt_flags & f) != 0u; }
+#ifdef HOP_DEV
+inline constexpr bool kDevBuild = true;
+#else
+inline constexpr bool kDevBuild = false;
+#endif
+}  // namespace hop
+
 namespace hop {
 
 // Trajectory form of the LFT inputs (augmented.py:10-87 done on the device):
@@ -183,5 +197,7 @@ template <class T>
 hipError_t dispatch_augment(const AugArgs<T>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream);
+// exact-size fp64 Riccati kernel (n = 12, m = 4; riccati_fast.hip), NotSupported otherwise
+hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t stream);
 
 }  // namespace hop

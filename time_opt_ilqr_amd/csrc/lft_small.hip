@@ -16,7 +16,7 @@
 #include "hop_kernels.hpp"
 
 // lft_small_noslp.hip re-compiles this file under another namespace with
-// -fno-slp-vectorize (same-process A/B, HOP_SMALL_VARIANT=1)
+// -fno-slp-vectorize (developer builds: same-process A/B, variant 71)
 #ifndef HOP_SMALL_NS
 #define HOP_SMALL_NS small
 #define HOP_SMALL_DISPATCH dispatch_lft_small
@@ -487,22 +487,24 @@ template <class T>
 hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
   if (a.traj && (a.tr.n != a.s - 1 || a.tr.m != a.m || !a.r_is_inv)) return hipErrorNotSupported;
-  // HOP_SMALL_COND=1: the conditioned-prefix kernel, then the LFT instantiation in
-  // rerun mode for the problems it flagged (2: the COND kernel alone, A/B).  Off by
-  // default: one problem per lane at one wave per SIMD is latency-bound, and the
+  // Developer builds also carry the conditioned-prefix instantiation (variant 61:
+  // it, then the LFT instantiation in rerun mode for the problems it flagged; 62:
+  // the COND kernel alone, A/B).  Off by default and absent from product builds:
+  // one problem per lane at one wave per SIMD is latency-bound, and the
   // conditioned step measured slower here (config 3: 30.5 M vs 39.7 M sweeps/s)
   // although it issues half the FLOPs
-  const char* cv = getenv("HOP_SMALL_COND");
-  const int cmode = cv ? atoi(cv) : 0;
-  auto go2 = [&](auto kc, auto kl, int bytes) {
+  auto go1 = [&](auto kl, int bytes) {
     const long long blocks = (a.batch + 255) / 256;
-    if (cmode == 0) {
-      hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
-      return hipGetLastError();
-    }
+    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+    return hipGetLastError();
+  };
+#ifdef HOP_DEV
+  const int cmode = g_opt_variant == 61 ? 1 : g_opt_variant == 62 ? 2 : 0;
+  auto go2 = [&](auto kc, auto kl, int bytes) {
+    if (cmode == 0) return go1(kl, bytes);
+    const long long blocks = (a.batch + 255) / 256;
     LftArgs<T> c = a;
-    const char* fv = getenv("HOP_COND_FORCE");
-    c.cond = (fv && atoi(fv) == 1) ? 2 : 0;  // 2: hand every problem over (tests)
+    c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
     hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
     if (cmode == 2) return hipGetLastError();
     LftArgs<T> r = a;
@@ -518,6 +520,14 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
                   : go2(small::lft_small_kernel<T, S_, M_, true>,                         \
                         small::lft_small_kernel<T, S_, M_, false>,                        \
                         small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+#else
+#define HOP_SMALL(S_, M_)                                                                 \
+  if (a.s == S_ && a.m == M_)                                                             \
+    return a.traj ? go1(small::lft_small_traj_kernel<T, S_, M_, false>,                   \
+                        small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                          \
+                  : go1(small::lft_small_kernel<T, S_, M_, false>,                        \
+                        small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+#endif
   if constexpr (sizeof(T) == 4) {
     HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)
     HOP_SMALL(5, 2)  // s = 6 spills: generic kernel

@@ -25,7 +25,8 @@
 // lft_cond_cf_kernel), the default for s = 13, m = 4, which hand
 // the problems they cannot take to lft_sweep_v2_kernel in rerun mode.
 //
-// Schedules are runtime-selectable (HOP_LFT_VARIANT) for same-process A/B:
+// Schedules other than the defaults are compiled only in developer builds
+// (HOP_DEV, build.py --dev) and selected by hop_set_options' variant number:
 //   2  Select : compiler-scheduled pivots with lane-p selects (first v2)
 //   8  Chain  : offset form, short C++ pivot chain, pad-free DPP blocks
 //   10 Sched  : offset form, whole-sweep asm blocks
@@ -1904,112 +1905,98 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
 
 }  // namespace v2
 
-// exact-size fast path: returns hipErrorNotSupported when the shape has none
+// exact-size fast path: returns hipErrorNotSupported when the shape has none.
+// Product builds: the conditioned-prefix kernel + the rerun launch of the
+// reference association for the problems it flagged (HOP_OPT_REFERENCE_ASSOC:
+// the reference association alone; HOP_OPT_FORCE_HANDOVER: every problem handed
+// over).  Developer builds (HOP_DEV) add the A/B schedules of DESIGN.md 3.2 by
+// number (hop_set_options variant).
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv) return hipErrorNotSupported;
-  if (a.traj) {  // in-kernel augmentation (capi routes only s = 13, m = 4 here)
-    if (a.s != 13 || a.m != 4 || a.tr.n != 12 || a.tr.m != 4) return hipErrorNotSupported;
-    const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
-    const size_t bytes = (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock);
-    const char* ev = getenv("HOP_LFT_VARIANT");
-    const int tv = ev ? atoi(ev) : 53;  // default: closed-form stage inverses
-    if (tv == 53 || tv == 54) {  // closed-form stage inverses (+ rerun unless 54)
-      LftArgs<double> c = a;
-      const char* fv = getenv("HOP_COND_FORCE");
-      c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
-      hipLaunchKernelGGL((v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>),
-                         dim3((unsigned)blocks), dim3(256), bytes, stream, c);
-      if (tv == 54) return hipGetLastError();
-      LftArgs<double> r = a;
-      r.cond = 1;
-      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>),
-                         dim3((unsigned)blocks), dim3(256), bytes, stream, r);
-      return hipGetLastError();
-    }
-    if (tv == 40 || tv == 41) {  // conditioned prefix + rerun of the flagged problems
-      LftArgs<double> c = a;
-      const char* fv = getenv("HOP_COND_FORCE");
-      c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
-      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondTraj, 13, 4>), dim3((unsigned)blocks),
-                         dim3(256), bytes, stream, c);
-      if (tv == 41) return hipGetLastError();
-      LftArgs<double> r = a;
-      r.cond = 1;
-      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>),
-                         dim3((unsigned)blocks), dim3(256), bytes, stream, r);
-      return hipGetLastError();
-    }
-    if (ev && atoi(ev) == 24)  // section stamps (tools/stamps.py --traj)
-      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTrajStamped, 13, 4>),
-                         dim3((unsigned)blocks), dim3(256), bytes, stream, a);
-    else
-      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>),
-                         dim3((unsigned)blocks), dim3(256), bytes, stream, a);
-    return hipGetLastError();
-  }
-  auto go = [&](auto kern, int bytes) {
-    const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+  const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+  const int variant = g_opt_variant;
+  auto launch = [&](auto kern, size_t bytes, const LftArgs<double>& args) {
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), bytes, stream, args);
     return hipGetLastError();
   };
-  const char* ev = getenv("HOP_LFT_VARIANT");  // read per call: same-process A/B
-  const int variant = ev ? atoi(ev) : 40;
-  if (a.s == 13 && a.m == 4) {
-    constexpr int bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
-    if (variant == 42)  // stamps (tools/stamps.py --cond), no rerun
-      return go(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes);
-    if (variant == 43)  // A/B: image reads not overlapped with the sweeps, no rerun
-      return go(v2::lft_cond_kernel<v2::SchedCond, 13, 4>, bytes);
-    if (variant == 40 || variant == 41) {
-      // conditioned prefix, then the reference association for the problems it
-      // flagged (ST_RERUN); HOP_COND_FORCE=1 flags every problem (tests)
-      LftArgs<double> c = a;
-      const char* fv = getenv("HOP_COND_FORCE");
-      c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
-      hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondL, 13, 4>),
-                         dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
-                         dim3(256), (size_t)bytes, stream, c);
-      if (variant == 41) return hipGetLastError();  // no rerun (A/B timing of the kernel alone)
-      LftArgs<double> r = a;
-      r.cond = 1;
-      hipLaunchKernelGGL((v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>),
-                         dim3((unsigned)((a.batch + kProbPerBlock - 1) / kProbPerBlock)),
-                         dim3(256), (size_t)bytes, stream, r);
-      return hipGetLastError();
-    }
-    if (variant == 2) return go(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes);
-    if (variant == 8) return go(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes);
-    if (variant == 10) return go(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes);
-    if (variant == 12) return go(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes);
-    if (variant == 20) return go(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes);
-    if (variant == 30) return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes);
-    if (variant == 32) return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDmaStamped, 13, 4>, bytes);
-    if (variant == 14) return go(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes);
-    return go(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes);
+  // conditioned kernel, then the rerun launch (cond = 1) of the flagged problems
+  auto cond_rerun = [&](auto kc, auto kr, size_t bytes, bool rerun) {
+    LftArgs<double> c = a;
+    c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+    hipError_t e = launch(kc, bytes, c);
+    if (e != hipSuccess || !rerun) return e;
+    LftArgs<double> r = a;
+    r.cond = 1;
+    return launch(kr, bytes, r);
+  };
+  if (a.traj) {  // in-kernel augmentation (capi routes only s = 13, m = 4 here)
+    if (a.s != 13 || a.m != 4 || a.tr.n != 12 || a.tr.m != 4) return hipErrorNotSupported;
+    const size_t bytes = (size_t)(v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock);
+    if (opt(HOP_OPT_REFERENCE_ASSOC))
+      return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, a);
+#ifdef HOP_DEV
+    if (variant == 54)  // closed-form stage inverses without the rerun launch
+      return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, false);
+    if (variant == 40 || variant == 41)  // Gauss-Jordan stage inverses (+ rerun unless 41)
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondTraj, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, variant == 40);
+    if (variant == 24 || opt(HOP_OPT_STAMPS))  // section stamps (tools/stamps.py --traj)
+      return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlTrajStamped, 13, 4>, bytes, a);
+#endif
+    // default: closed-form stage inverses + rerun
+    return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
+                      v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
   }
-  return hipErrorNotSupported;
+  if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
+  constexpr size_t bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
+  if (opt(HOP_OPT_REFERENCE_ASSOC) || variant == 30)
+    return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, a);
+#ifdef HOP_DEV
+  switch (variant) {
+    case 42:  // stamps (tools/stamps.py --cond), no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes, a);
+    case 43:  // image reads not overlapped with the sweeps, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCond, 13, 4>, bytes, a);
+    case 41:  // conditioned kernel without the rerun launch (A/B timing of it alone)
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
+    case 2: return launch(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes, a);
+    case 8: return launch(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes, a);
+    case 10: return launch(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes, a);
+    case 12: return launch(v2::lft_sweep_v2_kernel<v2::SchedRow, 13, 4>, bytes, a);
+    case 14: return launch(v2::lft_sweep_v2_kernel<v2::SchedLdl, 13, 4>, bytes, a);
+    case 20: return launch(v2::lft_sweep_v2_kernel<v2::SchedStamped, 13, 4>, bytes, a);
+    case 32: return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDmaStamped, 13, 4>, bytes, a);
+    default: break;
+  }
+  if (opt(HOP_OPT_STAMPS))
+    return launch(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes, a);
+#endif
+  // default (variant 40): conditioned prefix + rerun of the problems it flagged
+  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
+                    v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
 }
 
 }  // namespace hop
 
 // fp32 blocks at s = 13, m = 4: the conditioned-prefix kernel on fp32 images
 // (fp64 arithmetic), then the generic fp32 kernel in rerun mode for the problems
-// it flagged.  HOP_LFT_VARIANT=30 (or any LFT schedule) keeps the generic path.
+// it flagged.  HOP_OPT_REFERENCE_ASSOC keeps the generic path.
 namespace hop {
 hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv || a.traj) return hipErrorNotSupported;
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
-  const char* ev = getenv("HOP_LFT_VARIANT");
-  const int variant = ev ? atoi(ev) : 40;
-  if (variant != 40 && variant != 41) return hipErrorNotSupported;
+  if (opt(HOP_OPT_REFERENCE_ASSOC) || (g_opt_variant != 0 && g_opt_variant != 40 &&
+                                       g_opt_variant != 41))
+    return hipErrorNotSupported;
   using G = v2::Geo<13, 4, 4>;
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   LftArgs<float> c = a;
-  const char* fv = getenv("HOP_COND_FORCE");
-  c.cond = (fv && atoi(fv) == 1) ? 2 : 0;
+  c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
   hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4, float>), dim3((unsigned)blocks),
                      dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
-  if (variant == 41) return hipGetLastError();
+  if (g_opt_variant == 41) return hipGetLastError();
   LftArgs<float> r = a;
   r.cond = 1;
   return dispatch_lft<float>(r, stream);
@@ -2017,7 +2004,7 @@ hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
 }  // namespace hop
 
 // Diagnostic (not part of include/hop.h): read (and optionally reset) the
-// section stamps of the stamped variant (HOP_LFT_VARIANT=20).
+// section stamps of the stamped variants (developer builds).
 extern "C" int hop_debug_stamps(unsigned long long* host16, int reset) {
   if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(hop::v2::g_hop_stamp),
                           16 * sizeof(unsigned long long)) != hipSuccess)

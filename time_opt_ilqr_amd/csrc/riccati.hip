@@ -360,18 +360,26 @@ template <class T, int S, int MM>
 hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   const size_t lds = (size_t)2 * kProbPerBlock * kLdsTile * sizeof(T);
-  const char* ev = getenv("HOP_RIC_STAMP");  // diagnostic: section stamps
-  if (ev && atoi(ev) == 1)
+#ifdef HOP_DEV
+  if (opt(HOP_OPT_STAMPS)) {  // diagnostic: section stamps (tools/stamps_riccati.py)
     hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), dim3((unsigned)blocks), dim3(256), lds,
                        stream, a);
-  else
-    hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream,
-                       a);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream,
+                     a);
   return hipGetLastError();
 }
 
 template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
+  if constexpr (sizeof(T) == 8) {
+    if (!opt(HOP_OPT_FORCE_GENERIC | HOP_OPT_STAMPS)) {
+      const hipError_t e = dispatch_riccati_fast(a, stream);
+      if (e != hipErrorNotSupported) return e;
+    }
+  }
   if (a.m <= 4) {
     if (a.n <= 4) return launch_riccati<T, 4, 4>(a, stream);
     if (a.n <= 8) return launch_riccati<T, 8, 4>(a, stream);
@@ -387,7 +395,7 @@ template hipError_t dispatch_riccati<float>(const RiccatiArgs<float>&, hipStream
 }  // namespace hop
 
 // Diagnostic (not part of include/hop.h): read (and optionally reset) the Riccati
-// section stamps (HOP_RIC_STAMP=1).
+// section stamps (HOP_OPT_STAMPS, developer builds).
 extern "C" int hop_debug_ric_stamps(unsigned long long* host16, int reset) {
   if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(hop::g_ric_stamp), 16 * sizeof(unsigned long long)) !=
       hipSuccess)

@@ -1,4 +1,6 @@
-"""Same-process interleaved A/B of LFT kernel variants (HOP_LFT_VARIANT / HOP_FORCE_GENERIC).
+"""Same-process interleaved A/B of LFT kernel variants (hop_set_options: schedule
+numbers need a developer build, HOP_DEV_BUILD=1; "g" = HOP_OPT_FORCE_GENERIC,
+"r" = HOP_OPT_REFERENCE_ASSOC, "0" = the product default).
 
     python tools/ab_bench.py --variants 0,1,2,g --rounds 7 --iters 10
 
@@ -24,10 +26,9 @@ def main():
     ap.add_argument("--s", type=int, default=13)
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--dtype", choices=["f64", "f32"], default="f64")
-    ap.add_argument("--env", default="HOP_LFT_VARIANT", help="variable the variants set")
     args = ap.parse_args()
     import torch
-    from time_opt_ilqr_amd import engine, synth
+    from time_opt_ilqr_amd import _lib, engine, synth
     dev = torch.device("cuda", 0)
     dt = torch.float64 if args.dtype == "f64" else torch.float32
     A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, args.s, args.m, args.N, seed=5,
@@ -35,11 +36,8 @@ def main():
     variants = args.variants.split(",")
 
     def setv(v):
-        os.environ.pop("HOP_FORCE_GENERIC", None)
-        if v == "g":
-            os.environ["HOP_FORCE_GENERIC"] = "1"
-        else:
-            os.environ[args.env] = v
+        flags = {"g": _lib.OPT_FORCE_GENERIC, "r": _lib.OPT_REFERENCE_ASSOC}.get(v, 0)
+        _lib.check(_lib.load().hop_set_options(flags, 0 if v in "gr" else int(v)))
 
     ref = None
     for v in variants:  # warm + cross-check

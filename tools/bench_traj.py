@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=9)
     args = ap.parse_args()
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(11)
@@ -59,11 +59,8 @@ def main():
         return e0.elapsed_time(e1) / args.iters
 
     def traj_unfused():
-        os.environ["HOP_TRAJ_UNFUSED"] = "1"
-        try:
+        with _lib.options(traj_unfused=True):
             engine.propagate_traj(*targs, t_min=1, t_max=N)
-        finally:
-            del os.environ["HOP_TRAJ_UNFUSED"]
 
     paths = {
         "traj_fused": lambda: engine.propagate_traj(*targs, t_min=1, t_max=N),

@@ -3,9 +3,9 @@ import numpy as np
 sys.path.insert(0, os.getcwd())
 import torch
 from oracle import hop_oracle as orc
-from time_opt_ilqr_amd import engine
+from time_opt_ilqr_amd import _lib, engine
 dev = torch.device("cuda", 0)
-os.environ["HOP_FORCE_GENERIC"] = "1"
+_lib.check(_lib.load().hop_set_options(_lib.OPT_FORCE_GENERIC, 0))  # the generic kernel
 for s, m in ((4, 2), (4, 1), (3, 1), (5, 1), (5, 2)):
     Bn, N = 131, 40
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(900 + s, Bn, s, m, N)

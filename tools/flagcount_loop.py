@@ -7,7 +7,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from time_opt_ilqr_amd import engine, systems  # noqa: E402
+from time_opt_ilqr_amd import _lib, engine, systems  # noqa: E402
 from time_opt_ilqr_amd.utils import _sym, chol_inv  # noqa: E402
 from oracle import hop_oracle as orc  # noqa: E402
 
@@ -23,7 +23,8 @@ lin = engine.linearize(2, X, U, F.dt)
 P = t(_sym(orc.terminal_weight(alpha, 12)))
 Ri = t(chol_inv(_sym(R)))
 for var, rho in (("54", 1e-12), ("41", 1e-12), ("54", 1.0)):
-    os.environ["HOP_LFT_VARIANT"] = var  # the conditioned kernel alone: ST_RERUN (16) left set
+    # developer build: the conditioned kernel alone, ST_RERUN (16) left set
+    _lib.check(_lib.load().hop_set_options(0, int(var)))
     r = engine.propagate_traj(lin.A, lin.B, lin.a_res, X, U, t(xg), t(u_ref), t(Q), Ri, P, w,
                               wrap_idx=wrap, t_min=20, t_max=100, rho_reg=rho)
     st = r.status.cpu().numpy()

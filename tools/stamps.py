@@ -54,7 +54,7 @@ def main():
         NAMES[:8] = ["top wait (DMA of step k)", "J store + diag offsets", "Q/QT image reads (sym)",
                      "E/Xt sweeps", "A/B reads + DMA issue", "update (CondLdl)", "predict products",
                      "query (ElimQ)"]
-    os.environ["HOP_LFT_VARIANT"] = str(args.variant)
+    _lib.check(_lib.load().hop_set_options(0, int(args.variant)))  # developer build
     buf = (C.c_ulonglong * 16)()
     run()
     torch.cuda.synchronize()

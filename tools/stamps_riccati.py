@@ -1,4 +1,4 @@
-"""Per-section cycle breakdown of the Riccati kernel (HOP_RIC_STAMP=1 instantiation).
+"""Per-section cycle breakdown of the Riccati kernel (HOP_OPT_STAMPS instantiation of a developer build).
 
     python tools/stamps_riccati.py [--batch 4096] [--N 100] [--mode 0]
 """
@@ -36,7 +36,7 @@ def main():
     M = torch.randn((n, n), **kw)
     Q = M @ M.T / n + 0.5 * eye
     R = torch.eye(m, device=dev, dtype=torch.float64)
-    os.environ["HOP_RIC_STAMP"] = "1"
+    _lib.check(_lib.load().hop_set_options(_lib.OPT_STAMPS, 0))  # developer build
     buf = (C.c_ulonglong * 16)()
     run = lambda: engine.riccati(A, Bm, X, U, torch.zeros(n, **{k: v for k, v in kw.items() if k != "generator"}),  # noqa: E731
                                  torch.zeros(m, device=dev, dtype=torch.float64), Q, R, 10 * eye, N,
