@@ -375,7 +375,7 @@ hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
 template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   if constexpr (sizeof(T) == 8) {
-    if (!opt(HOP_OPT_FORCE_GENERIC | HOP_OPT_STAMPS)) {
+    if (!opt(HOP_OPT_FORCE_GENERIC)) {  // (HOP_OPT_STAMPS: the fast kernel's own stamps)
       const hipError_t e = dispatch_riccati_fast(a, stream);
       if (e != hipErrorNotSupported) return e;
     }

@@ -82,8 +82,9 @@ __device__ __forceinline__ void dma9(const unsigned (&va)[5], const unsigned (&v
 #undef HOP_P
 }
 
-// [A|B] rows (12 registers, column c per lane), x_c and u_c from image IMG:
-// 14 ds_read_b64 in flight, one wait, one asm statement (early-clobber outputs)
+// [A|B] rows (12 registers, column c per lane), x_c and u_c from image IMG, and
+// (VT) the transpose of the previous step's value update parked in the tile:
+// every read in flight, one wait, one asm statement (early-clobber outputs)
 template <int IMG>
 __device__ __forceinline__ void read_step(const unsigned (&ad)[NX], unsigned xa, unsigned ua,
                                           double (&ab)[NX], double& x, double& u) {
@@ -111,8 +112,157 @@ __device__ __forceinline__ void read_step(const unsigned (&ad)[NX], unsigned xa,
         "i"(IMG)
       : "memory");
 }
+template <int IMG>
+__device__ __forceinline__ void read_step_vt(const unsigned (&ad)[NX], unsigned xa, unsigned ua,
+                                             unsigned ra, double (&ab)[NX], double& x, double& u,
+                                             double (&t)[NX]) {
+  asm volatile(
+      "ds_read_b64 %0, %26 offset:%c41\n\t"
+      "ds_read_b64 %1, %27 offset:%c41\n\t"
+      "ds_read_b64 %2, %28 offset:%c41\n\t"
+      "ds_read_b64 %3, %29 offset:%c41\n\t"
+      "ds_read_b64 %4, %30 offset:%c41\n\t"
+      "ds_read_b64 %5, %31 offset:%c41\n\t"
+      "ds_read_b64 %6, %32 offset:%c41\n\t"
+      "ds_read_b64 %7, %33 offset:%c41\n\t"
+      "ds_read_b64 %8, %34 offset:%c41\n\t"
+      "ds_read_b64 %9, %35 offset:%c41\n\t"
+      "ds_read_b64 %10, %36 offset:%c41\n\t"
+      "ds_read_b64 %11, %37 offset:%c41\n\t"
+      "ds_read_b64 %12, %38 offset:%c41\n\t"
+      "ds_read_b64 %13, %39 offset:%c41\n\t"
+      "ds_read_b64 %14, %40 offset:0\n\t"
+      "ds_read_b64 %15, %40 offset:8\n\t"
+      "ds_read_b64 %16, %40 offset:16\n\t"
+      "ds_read_b64 %17, %40 offset:24\n\t"
+      "ds_read_b64 %18, %40 offset:32\n\t"
+      "ds_read_b64 %19, %40 offset:40\n\t"
+      "ds_read_b64 %20, %40 offset:48\n\t"
+      "ds_read_b64 %21, %40 offset:56\n\t"
+      "ds_read_b64 %22, %40 offset:64\n\t"
+      "ds_read_b64 %23, %40 offset:72\n\t"
+      "ds_read_b64 %24, %40 offset:80\n\t"
+      "ds_read_b64 %25, %40 offset:88\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]),
+        "=&v"(ab[6]), "=&v"(ab[7]), "=&v"(ab[8]), "=&v"(ab[9]), "=&v"(ab[10]), "=&v"(ab[11]),
+        "=&v"(x), "=&v"(u), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]),
+        "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]),
+        "=&v"(t[11])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]),
+        "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(xa), "v"(ua),
+        "v"(ra), "i"(IMG)
+      : "memory");
+}
+
+// park x (column c per lane) in the problem's tile: row i at wa + 136 i (no wait:
+// the wave's LDS operations execute in order, the next reads see these writes)
+__device__ __forceinline__ void lds_park12(const double (&x)[NX], unsigned wa) {
+  asm volatile(
+      "ds_write_b64 %12, %0 offset:0\n\t"
+      "ds_write_b64 %12, %1 offset:136\n\t"
+      "ds_write_b64 %12, %2 offset:272\n\t"
+      "ds_write_b64 %12, %3 offset:408\n\t"
+      "ds_write_b64 %12, %4 offset:544\n\t"
+      "ds_write_b64 %12, %5 offset:680\n\t"
+      "ds_write_b64 %12, %6 offset:816\n\t"
+      "ds_write_b64 %12, %7 offset:952\n\t"
+      "ds_write_b64 %12, %8 offset:1088\n\t"
+      "ds_write_b64 %12, %9 offset:1224\n\t"
+      "ds_write_b64 %12, %10 offset:1360\n\t"
+      "ds_write_b64 %12, %11 offset:1496"
+      :
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+        "v"(x[8]), "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(wa)
+      : "memory");
+}
+
+// the 12 transposed reads of a parked matrix and their wait (epilogue)
+__device__ __forceinline__ void lds_read_t12(double (&t)[NX], unsigned ra) {
+  asm volatile(
+      "ds_read_b64 %0, %12 offset:0\n\t"
+      "ds_read_b64 %1, %12 offset:8\n\t"
+      "ds_read_b64 %2, %12 offset:16\n\t"
+      "ds_read_b64 %3, %12 offset:24\n\t"
+      "ds_read_b64 %4, %12 offset:32\n\t"
+      "ds_read_b64 %5, %12 offset:40\n\t"
+      "ds_read_b64 %6, %12 offset:48\n\t"
+      "ds_read_b64 %7, %12 offset:56\n\t"
+      "ds_read_b64 %8, %12 offset:64\n\t"
+      "ds_read_b64 %9, %12 offset:72\n\t"
+      "ds_read_b64 %10, %12 offset:80\n\t"
+      "ds_read_b64 %11, %12 offset:88\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]),
+        "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11])
+      : "v"(ra)
+      : "memory");
+}
 
 __device__ __forceinline__ void vm_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// all but the N youngest vector-memory operations done (loads, stores and
+// LDS-DMA count together in issue order)
+template <int N>
+__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+
+// x <- 0.5 (x + x^T) through the problem's LDS tile in ONE asm statement: the
+// wave's LDS operations execute in order, so the transposed reads follow the
+// writes without a wait in between; one lgkmcnt wait at the end
+template <int S>
+__device__ __forceinline__ void lds_transpose(const double (&x)[S], double (&t)[S], unsigned wa,
+                                              unsigned ra);
+template <>
+__device__ __forceinline__ void lds_transpose<12>(const double (&x)[12], double (&t)[12],
+                                                  unsigned wa, unsigned ra) {
+  asm volatile(
+      "ds_write_b64 %24, %12 offset:0\n\t"
+      "ds_write_b64 %24, %13 offset:136\n\t"
+      "ds_write_b64 %24, %14 offset:272\n\t"
+      "ds_write_b64 %24, %15 offset:408\n\t"
+      "ds_write_b64 %24, %16 offset:544\n\t"
+      "ds_write_b64 %24, %17 offset:680\n\t"
+      "ds_write_b64 %24, %18 offset:816\n\t"
+      "ds_write_b64 %24, %19 offset:952\n\t"
+      "ds_write_b64 %24, %20 offset:1088\n\t"
+      "ds_write_b64 %24, %21 offset:1224\n\t"
+      "ds_write_b64 %24, %22 offset:1360\n\t"
+      "ds_write_b64 %24, %23 offset:1496\n\t"
+      "ds_read_b64 %0, %25 offset:0\n\t"
+      "ds_read_b64 %1, %25 offset:8\n\t"
+      "ds_read_b64 %2, %25 offset:16\n\t"
+      "ds_read_b64 %3, %25 offset:24\n\t"
+      "ds_read_b64 %4, %25 offset:32\n\t"
+      "ds_read_b64 %5, %25 offset:40\n\t"
+      "ds_read_b64 %6, %25 offset:48\n\t"
+      "ds_read_b64 %7, %25 offset:56\n\t"
+      "ds_read_b64 %8, %25 offset:64\n\t"
+      "ds_read_b64 %9, %25 offset:72\n\t"
+      "ds_read_b64 %10, %25 offset:80\n\t"
+      "ds_read_b64 %11, %25 offset:88\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]),
+        "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11])
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+        "v"(x[8]), "v"(x[9]), "v"(x[10]), "v"(x[11]), "v"(wa), "v"(ra)
+      : "memory");
+}
+template <>
+__device__ __forceinline__ void lds_transpose<4>(const double (&x)[4], double (&t)[4], unsigned wa,
+                                                 unsigned ra) {
+  asm volatile(
+      "ds_write_b64 %8, %4 offset:0\n\t"
+      "ds_write_b64 %8, %5 offset:136\n\t"
+      "ds_write_b64 %8, %6 offset:272\n\t"
+      "ds_write_b64 %8, %7 offset:408\n\t"
+      "ds_read_b64 %0, %9 offset:0\n\t"
+      "ds_read_b64 %1, %9 offset:8\n\t"
+      "ds_read_b64 %2, %9 offset:16\n\t"
+      "ds_read_b64 %3, %9 offset:24\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(wa), "v"(ra)
+      : "memory");
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   const unsigned nrec = bytes > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)(bytes > 0 ? bytes : 0);
@@ -124,9 +274,26 @@ __device__ __forceinline__ void st64(double v, __amdgpu_buffer_rsrc_t r, unsigne
   __builtin_amdgcn_raw_buffer_store_b64(as_u2(v), r, vo, so, 0);
 }
 
-template <int MODE>
+// section stamps of the diagnostic instantiation (developer builds,
+// tools/stamps_riccati.py --fast): per-wave shader-clock totals per section
+__device__ unsigned long long g_ricf_stamp[16];
+
+// EXP (developer builds, timing experiments only -- results are wrong): 1 drops
+// the stores, 2 the per-step LDS-DMA
+template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0>
 __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
   constexpr int S = NX, MM = MU;
+  unsigned long long sec[12] = {};
+  unsigned long long tprev = 0;
+  auto stamp = [&](int j) {
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      const unsigned long long tt = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+      if (j >= 0) sec[j] += tt - tprev;
+      tprev = tt;
+    }
+  };
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
@@ -144,7 +311,9 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   if (wave_prob0 >= a.batch) return;  // wave-uniform; no workgroup barrier in this kernel
   const long long pb0 = wave_prob0;
   const int NA = a.nalloc;
-  const long long left = a.batch - pb0;
+  // descriptors cover only the wave's problems: an out-of-range offset then
+  // always means "dropped" (the commit mask of the stores below relies on it)
+  const long long left = a.batch - pb0 < kProbPerWave ? a.batch - pb0 : kProbPerWave;
 
   // buffer descriptors based at the wave's first problem (exact bounds: OOB reads 0,
   // OOB writes dropped)
@@ -159,7 +328,10 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
                                rk = rsrc(a.k + pb0 * (pk / 8), left * pk);
   const long long pVxx = (long long)(NA + 1) * S * S * 8, pVx = (long long)(NA + 1) * S * 8,
                   pV0 = (long long)(NA + 1) * 8;
-  const bool wantv = MODE == 1 || a.Vxx;
+  constexpr bool wantv = WANTV;
+  // stores per step, all issued unconditionally (non-committing lanes write out of
+  // range): K 4, k 1 [+ Vxx 12 (of the step before), Vx 1, V0 1]
+  constexpr int NST = 5 + (WANTV ? 14 : 0);
   unsigned va[5], vb[2], vx_, vu_;
 #pragma unroll
   for (int j = 0; j < 5; ++j) va[j] = voff<CH_A>(j, lane, wave_prob0, pb0, a.batch, pA);
@@ -235,7 +407,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     LaneDot<S>::fma(vx, eT, qfrow);
     v0 = 0.5 * row_sum_dpp(c < S ? eT * vx : 0.0);
     symmetrize(V, tile, c);
-    if (alive && wantv) {
+    if (alive && wantv) {  // the terminal expansion (plain stores, before the loop)
       double* o = a.Vxx + (pb * (NA + 1) + L) * (long long)(S * S);
       if (c < S) {
 #pragma unroll
@@ -254,19 +426,55 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   const unsigned voVxx = pofs * (unsigned)pVxx + 8u * (c < S ? c : 0);
   const unsigned voVx = pofs * (unsigned)pVx + 8u * (c < S ? c : 0);
   const unsigned voV0 = pofs * (unsigned)pV0;
+  const unsigned twa = (unsigned)(uintptr_t)tile + 8u * c;         // (i, c): + 136 i
+  const unsigned tra = (unsigned)(uintptr_t)tile + 8u * kLdsRow * c;  // (c, i): + 8 i
+  constexpr unsigned OOB = 0x80000000u;
+
+  // Deferred symmetrisation: step i parks its value update Vn in the tile and
+  // carries it (Vp, with its commit flag) into step i-1, whose LDS read of the
+  // step's [A|B] image also reads Vn^T; V = sym(Vn) is formed there, so the
+  // transpose's LDS latency hides under the stores and the next step's DMA issue.
+  double Vp[S];
+  bool cprev = false;
+  zero(Vp);
 
   // one step (index i) reading image IMG; issues the DMA of step i-1 into the
   // other image first
-  auto step = [&](int i, auto IMGc) {
+  auto step = [&](int i, auto IMGc, auto FIRSTc) {
     constexpr int IMG = decltype(IMGc)::value;
+    constexpr bool FIRST = decltype(FIRSTc)::value;
     constexpr int NEXT = IMG == 0 ? BUF : 0;
-    vm_wait();  // this step's pieces landed (and the previous step's stores left)
-    if (i > 0)
+    // this step's pieces landed; the previous step's NST stores may still be in flight
+    stamp(-1);
+    if constexpr (FIRST) vm_wait();
+    else vm_wait_n<EXP == 1 ? 0 : NST>();
+    stamp(0);
+    if (EXP != 2 && i > 0)
       dma9<NEXT>(va, vb, vx_, vu_, rA, rB, rX, rU, wlds, (unsigned)(i - 1) * (S * S * 8),
                  (unsigned)(i - 1) * (S * MM * 8), (unsigned)(i - 1) * (S * 8),
                  (unsigned)(i - 1) * (MM * 8));
+    stamp(1);
     double ab[S], xi, ui;
-    read_step<IMG>(ad, xa, ua, ab, xi, ui);
+    if constexpr (FIRST) {
+      read_step<IMG>(ad, xa, ua, ab, xi, ui);
+    } else {
+      double t[S];
+      read_step_vt<IMG>(ad, xa, ua, tra, ab, xi, ui, t);
+#pragma unroll
+      for (int r = 0; r < S; ++r) {
+        const double vs = 0.5 * (Vp[r] + t[r]);  // _sym of step i+1's Vxx
+        V[r] = cprev ? vs : V[r];
+      }
+    }
+    // Vxx of step i+1 (mode 1 / requested): NST counts 12 stores here every step
+    // (the first step's are out of range) so vm_wait_n stays exact
+    if constexpr (WANTV && EXP != 1) {
+      const bool wr = !FIRST && cprev && c < S;
+      const unsigned sv = (unsigned)(i + 1) * (S * S * 8);
+#pragma unroll
+      for (int r = 0; r < S; ++r) st64(V[r], rVxx, wr ? voVxx + 8u * S * r : OOB, sv);
+    }
+    stamp(2);
     const bool act = alive && (i < L);
     double e = c < S ? xi - xg_c : 0.0;
     if (wrap_c) e = wrap_angle(e);
@@ -287,15 +495,22 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     LaneDot<S>::fma(qab, vx, ab);
     const double qx = lx + qab;                          // Qx = lx + A^T Vx (lanes < n)
     const double qu = lu + ror_row<kRowLanes - S>(qab);  // Qu = lu + B^T Vx (lanes < m)
+    stamp(3);
+    // products as one dependent DPP chain per output row (accumulator forwarded)
     double VA[S];
     zero(VA);
-    acc_xy<false>(VA, V, ab);
+    static_for<S>([&](auto I) { LaneDot<S>::fma(VA[I], V[I], ab); });  // V [A|B]
+    stamp(4);
     double Qxx[S];
     copy(Qxx, qcol);
-    acc_xty<false>(Qxx, ab, VA);  // Q + A^T V A (lanes < n)
+    static_for<S>([&](auto R) {  // Q + A^T V A (lanes < n), (A^T V B on lanes n..)
+      ColChain<S>::template fmaq<R>(Qxx[R], ab, VA);
+    });
     double QB[MM];
     zero(QB);
-    static_for<S>([&](auto J) { LaneBOff<MM, S>::fma(QB, ab[J], VA[J]); });  // B^T V [A|B]
+    static_for<MM>([&](auto R) {  // B^T V [A|B]
+      ColChain<S>::template fmaq<S + R>(QB[R], ab, VA);
+    });
     double Qux[MM], Quu[MM];
 #pragma unroll
     for (int r = 0; r < MM; ++r) {
@@ -303,40 +518,95 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
       Quu[r] = rcol[r] + ror_row<kRowLanes - S>(QB[r]);  // R + B^T V B (lanes < m)
     }
     // regularised solve
+    stamp(5);
     double QuuT[MM];
-    transpose(QuuT, Quu, tile, c);
-    double Qi[MM];
+    lds_transpose<MM>(Quu, QuuT, twa, tra);
+    stamp(6);
+    // First attempt as one offset-form asm sweep (SweepQ, the hot LFT kernel's
+    // block): the diagonal carries (value - 1), the sweep returns -(M+eps I)^-1 + I
+    // and its minimum pivot -- chol_solve's first try (eps = 1e-9; mode 1 at
+    // lam = max(lm, 1e-12)).  Mode 0's jitter-free cholesky(Quu_reg) check
+    // (solver.py:211-219) follows from the same sweep whenever
+    // trace((M + eps I)^-1) < 1e6: then lambda_min(M) > 1e-6 - eps > 0.  Rows
+    // outside that bound get the exact check (a second sweep without jitter), rows
+    // whose first try fails the generic jitter / lambda ladders (hop_device.hpp);
+    // both rare, wave-uniform branches.
+    double Qi[MM], Qs[MM];
     bool solved;
-    if constexpr (MODE == 0) {
+    {
+      const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+      double rj[MM];
 #pragma unroll
-      for (int r = 0; r < MM; ++r) Qi[r] = 0.5 * (Quu[r] + QuuT[r]) + ((c == r) ? lam0 : 0.0);
-      bool ok = true;
-      solved = spd_inverse_nofallback_chk(Qi, tile, c, 8, st, ok) && ok;
-    } else {
-      double lam = lam0 > 1e-12 ? lam0 : 1e-12;
-      int tries = 0;
+      for (int r = 0; r < MM; ++r) {
+        Qs[r] = 0.5 * (Quu[r] + QuuT[r]);
+        rj[r] = Qs[r] + ((c == r) ? lam1 + (1e-9 - 1.0) : 0.0);
+      }
+      double dj = 1.0;
+      SweepQ<MM>::run(rj, dj);
+      const bool okj = (dj > 0.0) && (bcast<0>(rj[0]) == bcast<0>(rj[0]));
+#pragma unroll
+      for (int r = 0; r < MM; ++r) Qi[r] = ((c == r) ? 1.0 : 0.0) - rj[r];  // +(M+eps I)^-1
+      bool ok0 = true;
+      if constexpr (MODE == 0) {
+        double dg = 0.0;  // this lane's diagonal entry of (M + eps I)^-1
+#pragma unroll
+        for (int r = 0; r < MM; ++r) dg = (c == r) ? Qi[r] : dg;
+        const double tr = row_sum_dpp(dg);
+        const bool sure = okj && (tr < 1e6);
+        if (__any(!sure)) {  // the exact jitter-free check
+          double rc[MM];
+#pragma unroll
+          for (int r = 0; r < MM; ++r) rc[r] = Qs[r] + ((c == r) ? lam1 - 1.0 : 0.0);
+          double dc = 1.0;
+          SweepQ<MM>::run(rc, dc);
+          const bool okc = (dc > 0.0) && (bcast<0>(rc[0]) == bcast<0>(rc[0]));
+          ok0 = sure || okc;
+        }
+      }
+      solved = okj && ok0;
+      if (__any(!okj && ok0)) {  // the jitter / lambda ladders for the rows that need them
+        const bool ladder = !okj && ok0;
+        if constexpr (MODE == 0) {
+          double Ql[MM];
+#pragma unroll
+          for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam0 : 0.0);
+          bool okc = true;
+          const bool good = spd_inverse_nofallback_chk(Ql, tile, c, 8, st, okc) && okc;
+#pragma unroll
+          for (int r = 0; r < MM; ++r) Qi[r] = ladder ? Ql[r] : Qi[r];
+          solved = ladder ? good : solved;
+        } else {
+          double lam = lam1;
+          int tries = 0;
+          bool okr = false;
+          double Ql[MM];
 #pragma unroll 1
-      while (true) {
+          while (true) {
 #pragma unroll
-        for (int r = 0; r < MM; ++r) Qi[r] = 0.5 * (Quu[r] + QuuT[r]) + ((c == r) ? lam : 0.0);
-        const bool okr = spd_inverse_nofallback(Qi, tile, c, 8, st);
-        ++tries;
-        solved = okr;
-        const bool done = okr || tries >= a.reg_max_tries;
-        if (!__any(!done && act)) break;
-        if (!done) lam *= 10.0;
+            for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam : 0.0);
+            okr = spd_inverse_nofallback(Ql, tile, c, 8, st);
+            ++tries;
+            const bool done = okr || tries >= a.reg_max_tries;
+            if (!__any(!done && act && ladder)) break;
+            if (!done) lam *= 10.0;
+          }
+#pragma unroll
+          for (int r = 0; r < MM; ++r) Qi[r] = ladder ? Ql[r] : Qi[r];
+          solved = ladder ? okr : solved;
+        }
       }
     }
     const bool fail_row = act && (bad || !solved);
+    stamp(7);
     // gains
     double K[MM];
     zero(K);
-    acc_xy<true, double, MM, MM>(K, Qi, Qux);  // K = -Quu_reg^-1 Qux (column c)
+    static_for<MM>([&](auto R) { LaneDot<MM>::fma_neg(K[R], Qi[R], Qux); });  // -Quu_reg^-1 Qux
     double kv = 0.0;
     LaneDot<MM>::fma_neg(kv, qu, Qi);          // k = -Quu_reg^-1 Qu  (lanes < m)
+    stamp(8);
     // value update
-    double Vn[S];
-    copy(Vn, Qxx);
+    double(&Vn)[S] = Qxx;  // the value update accumulates into Qxx in place
     double vxn = qx, v0n = v0;
     if constexpr (MODE == 0) {
       LaneDot<MM>::fma(vxn, qu, K);    // + K^T Qu
@@ -346,19 +616,26 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
       LaneDot<MM>::fma(vxn, qk, K);    // + K^T Quu k
       double QK[MM];
       copy(QK, Qux);
-      acc_xy<false, double, MM, MM>(QK, Quu, K);  // Qux + Quu K
-      acc_xty<false, double, S, MM>(Vn, K, QK);   // + K^T (Qux + Quu K)
-      acc_xty<false, double, S, MM>(Vn, Qux, K);  // + Qux^T K
+      static_for<MM>([&](auto R) { LaneDot<MM>::fma(QK[R], Quu[R], K); });  // Qux + Quu K
+      static_for<S>([&](auto R) {
+        ColChain<MM>::template fmaq<R>(Vn[R], K, QK);    // + K^T (Qux + Quu K)
+        ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);   // + Qux^T K
+      });
     } else {
-      acc_xty<false, double, S, MM>(Vn, Qux, K);  // Qxx - Qux^T Quu^-1 Qux
+      static_for<S>([&](auto R) {  // Qxx - Qux^T Quu^-1 Qux
+        ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);
+      });
       LaneDot<MM>::fma(vxn, kv, Qux);             // Qx - Qux^T Quu^-1 Qu
       v0n = l0 + v0 + 0.5 * row_sum_dpp(c < MM ? qu * kv : 0.0);
     }
-    symmetrize(Vn, tile, c);
-    bool vbad = !finite_val(vxn) || !finite_val(v0n);
+    stamp(9);
+    lds_park12(Vn, twa);  // its transpose is read with the next step's image
+    stamp(10);
+    // finiteness of the update: x * 0 is 0 for finite x, NaN otherwise
+    double z = __builtin_fma(vxn, 0.0, v0n * 0.0);
 #pragma unroll
-    for (int r = 0; r < S; ++r) vbad = vbad || !finite_val(Vn[r]);
-    const unsigned long long vbm = __ballot(vbad && c < S);
+    for (int r = 0; r < S; ++r) z = __builtin_fma(Vn[r], 0.0, z);
+    const unsigned long long vbm = __ballot(!(z == z) && c < S);
     const bool vfail = act && (((vbm >> (16 * g)) & 0xffffull) != 0ull);
     const bool commit = act && !fail_row && !vfail;
     if (act && (fail_row || vfail)) {
@@ -366,25 +643,26 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
       if (bad || vfail) st |= ST_NONFINITE;
       alive = false;
     }
-    if (commit) {
 #pragma unroll
-      for (int r = 0; r < S; ++r) V[r] = Vn[r];
-      vx = vxn;
-      v0 = v0n;
-    }
-    if (commit && c < S) {
+    for (int r = 0; r < S; ++r) Vp[r] = Vn[r];
+    cprev = commit;
+    vx = commit ? vxn : vx;
+    v0 = commit ? v0n : v0;
+    stamp(11);
+    // stores: every lane issues them (fixed count for vm_wait_n), lanes that do
+    // not commit address out of range (dropped by the descriptor's range check)
+    if constexpr (EXP != 1) {
+      const bool wr = commit && c < S;
       const unsigned so = (unsigned)i * (MM * S * 8);
 #pragma unroll
-      for (int r = 0; r < MM; ++r) st64(K[r], rK, voK + 8u * S * r, so);
-      if (wantv) {
-        const unsigned sv = (unsigned)i * (S * S * 8);
-#pragma unroll
-        for (int r = 0; r < S; ++r) st64(Vn[r], rVxx, voVxx + 8u * S * r, sv);
-        st64(vxn, rVx, voVx, (unsigned)i * (S * 8));
+      for (int r = 0; r < MM; ++r) st64(K[r], rK, wr ? voK + 8u * S * r : OOB, so);
+      st64(kv, rk, (commit && c < MM) ? vok : OOB, (unsigned)i * (MM * 8));
+      if constexpr (WANTV) {
+        st64(vxn, rVx, wr ? voVx : OOB, (unsigned)i * (S * 8));
+        st64(v0n, rV0, (commit && c == 0) ? voV0 : OOB, (unsigned)i * 8);
       }
     }
-    if (commit && c < MM) st64(kv, rk, vok, (unsigned)i * (MM * 8));
-    if (wantv && commit && c == 0) st64(v0n, rV0, voV0, (unsigned)i * 8);
+    stamp(1);  // section 1 = stores (closed here), reopened at the step top
   };
 
   using I0 = std::integral_constant<int, 0>;
@@ -393,25 +671,57 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     const int i0 = Lw - 1;
     dma9<0>(va, vb, vx_, vu_, rA, rB, rX, rU, wlds, (unsigned)i0 * (S * S * 8),
             (unsigned)i0 * (S * MM * 8), (unsigned)i0 * (S * 8), (unsigned)i0 * (MM * 8));
-    int i = i0;
+    using T1 = std::true_type;
+    using F0 = std::false_type;
+    step(i0, I0{}, T1{});
+    int i = i0 - 1;
 #pragma unroll 1
     while (i >= 1) {
-      step(i, I0{});
-      step(i - 1, I1{});
+      step(i, I1{}, F0{});
+      step(i - 1, I0{}, F0{});
       i -= 2;
     }
-    if (i == 0) step(0, I0{});
+    if (i == 0) step(0, I1{}, F0{});
+    if constexpr (WANTV) {  // Vxx of step 0
+      double t[S];
+      lds_read_t12(t, tra);
+      const bool wr = cprev && c < S;
+#pragma unroll
+      for (int r = 0; r < S; ++r) st64(0.5 * (Vp[r] + t[r]), rVxx, wr ? voVxx + 8u * S * r : OOB, 0u);
+    }
   }
   vm_wait();
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      for (int j = 0; j < 12; ++j) atomicAdd(&g_ricf_stamp[j], sec[j]);
+      atomicAdd(&g_ricf_stamp[15], 1ull);
+    }
+  }
   if (valid && c == 0) a.status[prob] = (int)st;
 }
 
-template <int MODE>
+template <int MODE, bool WANTV>
 hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   const size_t lds = (size_t)kWavesPerBlock * WAVE_BYTES;
-  hipLaunchKernelGGL((riccati_fast_kernel<MODE>), dim3((unsigned)blocks), dim3(256), lds, stream,
-                     a);
+#ifdef HOP_DEV
+  if (opt(HOP_OPT_STAMPS)) {
+    hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, true>), dim3((unsigned)blocks),
+                       dim3(256), lds, stream, a);
+    return hipGetLastError();
+  }
+  if (g_opt_variant == 81 || g_opt_variant == 82) {
+    if (g_opt_variant == 81)
+      hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 1>), dim3((unsigned)blocks),
+                         dim3(256), lds, stream, a);
+    else
+      hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 2>), dim3((unsigned)blocks),
+                         dim3(256), lds, stream, a);
+    return hipGetLastError();
+  }
+#endif
+  hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV>), dim3((unsigned)blocks), dim3(256), lds,
+                     stream, a);
   return hipGetLastError();
 }
 
@@ -423,9 +733,26 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
   if (a.n != ricf::NX || a.m != ricf::MU || a.qxx_extra || a.qx_extra || a.c_extra)
     return hipErrorNotSupported;
   // 32-bit buffer offsets: the per-wave tensors must stay below 4 GiB
+  // 32-bit buffer offsets: a wave's 4 problems must stay below 2 GiB per tensor
+  // (out-of-range store offsets start at 2 GiB)
   const long long NA = a.nalloc;
-  if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0xFFFFFFF0ll) return hipErrorNotSupported;
-  return a.mode == 0 ? ricf::launch<0>(a, stream) : ricf::launch<1>(a, stream);
+  if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0x7FFF0000ll) return hipErrorNotSupported;
+  if (a.mode == 1) return ricf::launch<1, true>(a, stream);
+  return a.Vxx ? ricf::launch<0, true>(a, stream) : ricf::launch<0, false>(a, stream);
 }
 
 }  // namespace hop
+
+// Diagnostic (not part of include/hop.h): read (and optionally reset) the section
+// stamps of the exact-size Riccati kernel (HOP_OPT_STAMPS, developer builds).
+extern "C" int hop_debug_ricf_stamps(unsigned long long* host16, int reset) {
+  if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(hop::ricf::g_ricf_stamp),
+                          16 * sizeof(unsigned long long)) != hipSuccess)
+    return -3;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(hop::ricf::g_ricf_stamp), z, sizeof(z)) != hipSuccess)
+      return -3;
+  }
+  return 0;
+}

@@ -1,15 +1,21 @@
 """Throughput of the batched Riccati passes on one GPU.
 
-    python tools/bench_riccati.py [--batch 4096] [--n 12] [--m 4] [--N 100]
+    python tools/bench_riccati.py [--batch 4096] [--n 12] [--m 4] [--N 100] [--variants 0,...]
 
 Synthetic trajectory-form inputs of the oracle's distribution (device RNG),
-horizon = N.  Prints one JSON line per mode: ms per launch, problems/s and the
-SURVEY.md 8(d) FLOP estimate (4n^3 + 10n^2 m) * T per problem.
+horizon = N.  The clocks are pre-warmed for --prewarm-s seconds, then every
+(variant, mode) is timed in interleaved rounds (same clock state for all; rule 24
+of cdna_hip_programming.md 5.4) and the median is reported: one JSON line per
+(variant, mode) with ms per launch, problems/s and the SURVEY.md 8(d) FLOP
+estimate (4n^3 + 10n^2 m) * T per problem.  Nonzero variants are developer-build
+experiments (HOP_LIB=<libhop_amd_dev.so>).
 """
 import argparse
 import json
 import os
+import statistics
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -20,10 +26,14 @@ def main():
     ap.add_argument("--n", type=int, default=12)
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--N", type=int, default=100)
-    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--prewarm-s", type=float, default=1.0)
+    ap.add_argument("--variants", default="0", help="comma list; nonzero needs HOP_LIB=<dev build>")
+    ap.add_argument("--generic", action="store_true", help="also time HOP_OPT_FORCE_GENERIC")
     args = ap.parse_args()
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(3)
@@ -40,24 +50,40 @@ def main():
     R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
     Qf = 10.0 * torch.eye(n, device=dev, dtype=torch.float64)
     flop = (4 * n ** 3 + 10 * n * n * m) * N
-    for mode in (0, 1):
-        run = lambda: engine.riccati(A, Bm, X, U, xg, ur, Q, R, Qf, N, 1e-3, mode=mode)  # noqa: E731
-        for _ in range(5):
-            r = run()
+    cases = [(v, md, False) for v in args.variants.split(",") for md in (0, 1)]
+    if args.generic:
+        cases += [("0", md, True) for md in (0, 1)]
+
+    def run(case):
+        v, md, gen = case
+        with _lib.options(variant=int(v), force_generic=gen):
+            return engine.riccati(A, Bm, X, U, xg, ur, Q, R, Qf, N, 1e-3, mode=md)
+
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < args.prewarm_s:
+        for c in cases:
+            run(c)
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.iters):
-            r = run()
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / args.iters
-        ok = int((r.status != 0).sum())
-        print(json.dumps({"mode": mode, "batch": Bn, "n": n, "m": m, "N": N, "ms": ms,
+    times = {c: [] for c in cases}
+    status = {}
+    for _ in range(args.rounds):
+        for c in cases:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                r = run(c)
+            e1.record()
+            torch.cuda.synchronize()
+            times[c].append(e0.elapsed_time(e1) / args.iters)
+            status[c] = int((r.status != 0).sum())
+    for c in cases:
+        ms = statistics.median(times[c])
+        print(json.dumps({"variant": int(c[0]), "generic": c[2], "mode": c[1], "batch": Bn,
+                          "n": n, "m": m, "N": N, "ms": ms, "ms_min": min(times[c]),
                           "problems_per_s": Bn / (ms * 1e-3),
                           "tflops_est": flop * Bn / (ms * 1e-3) / 1e12,
                           "frac_fp64": flop * Bn / (ms * 1e-3) / 1e12 / 78.6,
-                          "nonzero_status": ok}), flush=True)
+                          "nonzero_status": status[c]}), flush=True)
 
 
 if __name__ == "__main__":
