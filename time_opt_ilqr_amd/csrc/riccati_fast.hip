@@ -502,10 +502,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     static_for<S>([&](auto I) { LaneDot<S>::fma(VA[I], V[I], ab); });  // V [A|B]
     stamp(4);
     double Qxx[S];
-    copy(Qxx, qcol);
-    static_for<S>([&](auto R) {  // Q + A^T V A (lanes < n), (A^T V B on lanes n..)
-      ColChain<S>::template fmaq<R>(Qxx[R], ab, VA);
-    });
+    copy(Qxx, qcol);  // Q + A^T V A is accumulated under the Quu^-1 sweep below
     double QB[MM];
     zero(QB);
     static_for<MM>([&](auto R) {  // B^T V [A|B]
@@ -542,7 +539,9 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
         rj[r] = Qs[r] + ((c == r) ? lam1 + (1e-9 - 1.0) : 0.0);
       }
       double dj = 1.0;
-      SweepQ<MM>::run(rj, dj);
+      // the sweep fused with Qxx = Q + A^T V A (lanes < n; A^T V B on lanes n..):
+      // the 144 chain FMAs fill the pivots' rcp / Newton latency
+      SweepQColChain<MM, S>::run(rj, dj, Qxx, ab, VA);
       const bool okj = (dj > 0.0) && (bcast<0>(rj[0]) == bcast<0>(rj[0]));
 #pragma unroll
       for (int r = 0; r < MM; ++r) Qi[r] = ((c == r) ? 1.0 : 0.0) - rj[r];  // +(M+eps I)^-1
