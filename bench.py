@@ -79,9 +79,25 @@ def lft_bytes(N, s, m, w=8):
     return w * (N * (3 * s * s + s * m) + m * m + s + N)
 
 
-def riccati_flops(n, m, T):
-    """SURVEY.md 8(d) Riccati add-on: (4n^3 + 10n^2 m) per step."""
-    return (4 * n ** 3 + 10 * n * n * m) * T
+def riccati_flops(n, m, T, mode=0):
+    """SURVEY.md 8(d) Riccati add-on, (4n^3 + 10n^2 m + O(n^2 + nm^2 + m^3)) per step
+    (~1.49 MFLOP at n=12, m=4, T=100), with the lower-order terms counted term by
+    term as a competent implementation does them (solver.py:199-225 for mode 0,
+    horizon_selection.py:150-207 for mode 1): lx = Q e (2n^2), lu = R du (2m^2);
+    Qx, Qu (2n^2 + 2nm); V [A|B] (2n^2 (n+m)); Qxx = Q + A^T(VA) (2n^3 + n^2);
+    Qux (2n^2 m); Quu = R + B^T(VB) (2nm^2 + m^2); the m x m factor (m^3/3) and
+    the k, K solves (2m^2 + 2m^2 n).  Mode 0's value update Vx = Qx + K^T Qu +
+    Qux^T k + K^T Quu k (6nm + 2m^2) and Vxx = Qxx + K^T Qux + Qux^T K + K^T Quu K
+    (6n^2 m + 2nm^2); mode 1's Vxx = Qxx - Qux^T Quu^-1 Qux (2n^2 m), Vx (2nm) and
+    V0 with l0 (4n + 4m)."""
+    step = (2 * n * n + 2 * m * m + 2 * n * n + 2 * n * m + 2 * n * n * (n + m)
+            + 2 * n ** 3 + n * n + 2 * n * n * m + 2 * n * m * m + m * m + m ** 3 // 3
+            + 2 * m * m + 2 * m * m * n)
+    if mode == 0:
+        step += 6 * n * m + 2 * m * m + 6 * n * n * m + 2 * n * m * m
+    else:
+        step += 2 * n * n * m + 2 * n * m + 4 * n + 4 * m
+    return step * T
 
 
 # ---------------------------------------------------------------------------

@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
         for (int r = 0; r < MM; ++r) dg = (c == r) ? Qi[r] : dg;
         const double tr = row_sum_dpp(dg);
         const bool sure = okj && (tr < 1e6);
-        if (__any(!sure)) {  // the exact jitter-free check
+        if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
           double rc[MM];
 #pragma unroll
           for (int r = 0; r < MM; ++r) rc[r] = Qs[r] + ((c == r) ? lam1 - 1.0 : 0.0);
@@ -563,7 +563,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
         }
       }
       solved = okj && ok0;
-      if (__any(!okj && ok0)) {  // the jitter / lambda ladders for the rows that need them
+      if (__any(!okj && ok0 && act)) {  // the jitter / lambda ladders for the rows that need them
         const bool ladder = !okj && ok0;
         if constexpr (MODE == 0) {
           double Ql[MM];

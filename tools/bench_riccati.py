@@ -7,7 +7,7 @@ horizon = N.  The clocks are pre-warmed for --prewarm-s seconds, then every
 (variant, mode) is timed in interleaved rounds (same clock state for all; rule 24
 of cdna_hip_programming.md 5.4) and the median is reported: one JSON line per
 (variant, mode) with ms per launch, problems/s and the SURVEY.md 8(d) FLOP
-estimate (4n^3 + 10n^2 m) * T per problem.  Nonzero variants are developer-build
+count (bench.riccati_flops: 4n^3 + 10n^2 m + lower-order terms) * T per problem.  Nonzero variants are developer-build
 experiments (HOP_LIB=<libhop_amd_dev.so>).
 """
 import argparse
@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--prewarm-s", type=float, default=1.0)
     ap.add_argument("--variants", default="0", help="comma list; nonzero needs HOP_LIB=<dev build>")
     ap.add_argument("--generic", action="store_true", help="also time HOP_OPT_FORCE_GENERIC")
+    ap.add_argument("--libs", default="",
+                    help="comma list of library paths to A/B in this process (variant 0 of each)")
     args = ap.parse_args()
     import torch
     from time_opt_ilqr_amd import _lib, engine
@@ -49,13 +51,18 @@ def main():
     Q = M @ M.T / n + 0.5 * torch.eye(n, device=dev, dtype=torch.float64)
     R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
     Qf = 10.0 * torch.eye(n, device=dev, dtype=torch.float64)
-    flop = (4 * n ** 3 + 10 * n * n * m) * N
-    cases = [(v, md, False) for v in args.variants.split(",") for md in (0, 1)]
+    from bench import riccati_flops  # SURVEY.md 8(d) count, term by term
+    flop = {md: riccati_flops(n, m, N, md) for md in (0, 1)}
+    libs = {"": _lib.load()}
+    for p in filter(None, args.libs.split(",")):
+        libs[p] = _lib.load(p)
+    cases = [(v, md, False, lp) for lp in libs for v in args.variants.split(",") for md in (0, 1)]
     if args.generic:
-        cases += [("0", md, True) for md in (0, 1)]
+        cases += [("0", md, True, "") for md in (0, 1)]
 
     def run(case):
-        v, md, gen = case
+        v, md, gen, lp = case
+        _lib._lib = libs[lp]
         with _lib.options(variant=int(v), force_generic=gen):
             return engine.riccati(A, Bm, X, U, xg, ur, Q, R, Qf, N, 1e-3, mode=md)
 
@@ -78,11 +85,12 @@ def main():
             status[c] = int((r.status != 0).sum())
     for c in cases:
         ms = statistics.median(times[c])
-        print(json.dumps({"variant": int(c[0]), "generic": c[2], "mode": c[1], "batch": Bn,
+        print(json.dumps({"lib": os.path.basename(c[3]) or "default", "variant": int(c[0]),
+                          "generic": c[2], "mode": c[1], "batch": Bn,
                           "n": n, "m": m, "N": N, "ms": ms, "ms_min": min(times[c]),
                           "problems_per_s": Bn / (ms * 1e-3),
-                          "tflops_est": flop * Bn / (ms * 1e-3) / 1e12,
-                          "frac_fp64": flop * Bn / (ms * 1e-3) / 1e12 / 78.6,
+                          "tflops_est": flop[c[1]] * Bn / (ms * 1e-3) / 1e12,
+                          "frac_fp64": flop[c[1]] * Bn / (ms * 1e-3) / 1e12 / 78.6,
                           "nonzero_status": status[c]}), flush=True)
 
 
