@@ -13,7 +13,9 @@ Workloads (BASELINE.json configs):
   lft (default)  N=1: config 2 -- Quadrotor shape s=13, m=4, N=100, 4096 problems, fp64.
                  N>1: config 4 -- the same shape, 32768 problems per GPU (262144 on 8
                  GPUs), contiguous shards, weak scaling.
-  config3        Cartpole shape s=5, m=1, N=200, 65536 problems, fp32 (small-s kernel).
+  config3        Cartpole shape s=5, m=1, N=200, 65536 problems, fp32 (small-s kernel),
+                 blocks in the kernel's native tile64 layout (include/hop.h; --layout
+                 batch for batch-major blocks, which is also timed as a side figure).
   config5        mixed Segway / Cartpole / Quadrotor (i mod 3) padded to s=13, m=4,
                  N=128, 16384 problems per GPU (131072 on 8), fp32 blocks.
   select_gains   the select + backward of solver.py:581-597: trajectory-form select
@@ -181,16 +183,31 @@ def _lft_workload(args, world, lo, hi, dev):
     A, Bm, Q, Ri, z0, QT = synth.device_batch(hi - lo, s, m, N, seed=1234 + lo, device=dev,
                                               dtype=dtype)
     t_min, t_max = min(args.t_min, N), N
+    small = (s, m) in SMALL_SHAPES[args.dtype]
+    tiled = args.layout == "tile64" or (args.layout == "auto" and small and s == 5)
+    if tiled and not small:
+        raise SystemExit("--layout tile64: s <= 5 small-s shapes only")
 
-    def launch():
+    def launch_bm():
         return engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=t_max)
 
+    launch, host, alt = launch_bm, (A, Bm, Q, Ri, z0, QT), None
+    if tiled:  # the layout conversion is setup, outside the timed region
+        At, Bt, Qt, QTt = (engine.to_tile64(x) for x in (A, Bm, Q, QT))
+
+        def launch():
+            return engine.propagate(At, Bt, Qt, Ri, z0, QTt, t_min=t_min, t_max=t_max)
+
+        host, alt = (At.data, Bt.data, Qt.data, Ri, z0, QTt.data), launch_bm
+
     kname, bound = kernel_path(s, m, args.dtype)
+    if small:
+        kname = kname[:-1] + (",LY=2 tile64>" if tiled else ",LY=1 batch-major>")
     w = 8 if args.dtype == "f64" else 4
     info = dict(kernel=kname, bound=bound, flops=lft_flops(N, s, m), bytes=lft_bytes(N, s, m, w),
                 executed=cond_flops(N, s, m) if kname.startswith("lft_cond") else None,
-                t_min=t_min, t_max=t_max, s=s, m=m, N=N,
-                host=(A, Bm, Q, Ri, z0, QT))
+                t_min=t_min, t_max=t_max, s=s, m=m, N=N, host=host, alt=alt,
+                layout="tile64" if tiled else "batch-major")
     return launch, info
 
 
@@ -270,6 +287,9 @@ def main():
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="untimed launches before the warm-up steps (GPU clock ramp)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--layout", choices=["auto", "batch", "tile64"], default="auto",
+                    help="block layout of the lft/config3 workloads (auto: tile64 for the "
+                         "config-3 small-s shape, batch-major otherwise)")
     args = ap.parse_args()
 
     import torch
@@ -373,6 +393,19 @@ def main():
                "each step (PCIe-inclusive); not the headline value"}
         del pinned
 
+    # side figure: the same sweep on batch-major blocks (tile64 runs only)
+    alt_ms = None
+    if rank == 0 and info.get("alt") is not None:
+        ea = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(5)]
+        info["alt"]()
+        for a_, b_ in ea:
+            a_.record()
+            info["alt"]()
+            b_.record()
+        torch.cuda.synchronize()
+        alt_ms = sum(a_.elapsed_time(b_) for a_, b_ in ea) / len(ea)
+
     if rank == 0:
         total = Bn * world * K
         value = total / elapsed
@@ -388,7 +421,7 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            key = f"{wl}_s{s}_m{m}_N{N}_B{per_launch}_{args.dtype}"
+            key = f"{wl}_s{s}_m{m}_N{N}_B{per_launch}_{args.dtype}" + ("_tile64" if info.get("layout") == "tile64" else "")
             if key in tj:
                 traffic = tj[key]["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
@@ -410,6 +443,10 @@ def main():
             roof["arithmetic"] = "f64 (fp32 blocks in HBM/LDS)"
         if info["bound"] != "hbm":
             roof["hbm_gbs"] = info["bytes"] * per_launch / (kern_ms * 1e-3) / 1e9
+        if alt_ms is not None:
+            roof["batch_major_kernel_ms"] = alt_ms
+            roof["batch_major_frac"] = (info["bytes"] * per_launch / (alt_ms * 1e-3) / 1e9
+                                        / PEAK_HBM_GBS)
         names = {"lft": ("config 2: LFT sweep + fused argmin" if world == 1 else
                          "config 4 shard: LFT sweep + fused argmin"),
                  "config3": "config 3: LFT sweep + fused argmin (small-s kernel)",
@@ -434,6 +471,7 @@ def main():
             "config": {"workload": f"{names[wl]}, s={s} m={m} N={N}",
                        "batch_per_gpu": Bn, "global_batch": Bn * world, "s": s, "m": m,
                        "N": N, "t_min": info["t_min"], "t_max": info["t_max"],
+                       "layout": info.get("layout", "batch-major"),
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -119,6 +119,42 @@ int hop_lft_sweep_f32(const float* A_aug, const float* B_aug, const float* Q_aug
                       float* dbg_efg, float* dbg_prefix, void* stream);
 
 /*
+ * tile64 layout (the native layout of the s <= 5 one-problem-per-lane sweep)
+ *   A block tensor of `elems` elements per (problem, step) -- s*s for A/Q/QT,
+ *   s*m for B -- stored as [ceil(batch/64)][n_alloc][elems][64]: element e of
+ *   step k of problem b at ((b/64)*n_alloc + k)*elems*64 + e*64 + b%64.  A wave
+ *   of 64 problems then streams each block of a step as 64*elems contiguous
+ *   elements; batch-major blocks are 64 scattered spans of elems elements, and at
+ *   config 3 (s=5, fp32) that stream alone costs twice the tiled one.
+ * hop_tile64_elems: element count of a tile64 tensor (padding slots included).
+ * hop_tile64_f64/_f32: batch-major [batch][n_alloc][elems] -> tile64
+ *   (inverse=0; padding slots written 0), or tile64 -> batch-major (inverse=1).
+ *   A one-pass copy for callers holding batch-major blocks.
+ * hop_lft_sweep_tile64_f64/_f32: hop_lft_sweep_* (same reference function,
+ *   arguments and outputs) with A_aug, B_aug, Q_aug, QT_aug in tile64 layout;
+ *   R (no per-step stride), z0 and every output as hop_lft_sweep_*.  Shapes with
+ *   a small-s kernel only (fp32: s <= 5, m <= 2; fp64: s <= 4, m <= 2), else
+ *   HOP_E_SIZE; padding slots are read but never reported.
+ */
+int64_t hop_tile64_elems(int64_t batch, int32_t n_alloc, int32_t elems);
+int hop_tile64_f64(const double* src, double* dst, int64_t batch, int32_t n_alloc, int32_t elems,
+                   int32_t inverse, void* stream);
+int hop_tile64_f32(const float* src, float* dst, int64_t batch, int32_t n_alloc, int32_t elems,
+                   int32_t inverse, void* stream);
+int hop_lft_sweep_tile64_f64(const double* A_aug, const double* B_aug, const double* Q_aug,
+                             const double* R, int64_t r_batch_stride, int32_t r_is_inverse,
+                             const double* QT_aug, const double* z0, int64_t z0_batch_stride,
+                             int64_t batch, int32_t n_alloc, int32_t n_use, int32_t s, int32_t m,
+                             int32_t max_tries, int32_t t_min, int32_t t_max, double* J,
+                             int32_t* status, int32_t* t_star, double* j_star, void* stream);
+int hop_lft_sweep_tile64_f32(const float* A_aug, const float* B_aug, const float* Q_aug,
+                             const float* R, int64_t r_batch_stride, int32_t r_is_inverse,
+                             const float* QT_aug, const float* z0, int64_t z0_batch_stride,
+                             int64_t batch, int32_t n_alloc, int32_t n_use, int32_t s, int32_t m,
+                             int32_t max_tries, int32_t t_min, int32_t t_max, float* J,
+                             int32_t* status, int32_t* t_star, float* j_star, void* stream);
+
+/*
  * hop_select_horizon_f64 / _f32
  * Replaces T = int(np.argmin(J[T_min-1:T_max]) + T_min)
  *   /root/reference/solver.py:522, 590, 613 (legacy ilqr_propagator.py:496, 547).

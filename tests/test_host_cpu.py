@@ -30,7 +30,7 @@ def _header_functions():
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 24
+    assert len(names) == 29
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:
@@ -39,6 +39,24 @@ def test_header_symbols_exported(lib):
     for n in names:
         assert re.search(rf"\bT {n}\b", out), n
     assert lib.hop_abi_version() == 1
+
+
+def test_tile64_host_side_checks(lib):
+    """tile64 (include/hop.h): the element count covers whole tiles; shapes without a
+    small-s kernel and debug-free misuse are rejected before any launch."""
+    import ctypes as C
+    assert lib.hop_tile64_elems(70, 9, 25) == 128 * 9 * 25
+    assert lib.hop_tile64_elems(64, 3, 5) == 64 * 3 * 5
+    assert lib.hop_tile64_elems(0, 3, 5) == 0
+    assert lib.hop_tile64_elems(-1, 3, 5) == -1
+    d = C.c_void_p(16)  # never dereferenced: these calls are rejected on the host
+    args = lambda s, m, rbs=0: (d, d, d, d, rbs, 1, d, d, 0, 4, 10, 10, s, m, 8, 0, 0, d, d,  # noqa: E731
+                                None, None, None)
+    assert lib.hop_lft_sweep_tile64_f64(*args(13, 4)) == -2  # HOP_E_SIZE: s = 13
+    assert b"tile64" in lib.hop_last_error()
+    assert lib.hop_lft_sweep_tile64_f64(*args(5, 1)) == -2  # no fp64 kernel at s = 5
+    assert lib.hop_lft_sweep_tile64_f32(*args(6, 1)) == -2
+    assert lib.hop_tile64_f32(d, d, 5, 2, 0, 0, None) == -1  # elems < 1
 
 
 def test_options_are_explicit_and_product_build_has_no_ab_schedules(lib):

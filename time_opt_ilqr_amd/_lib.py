@@ -29,6 +29,9 @@ _U32 = C.c_uint32
 # (name, restype, argtypes) -- must match include/hop.h exactly
 _LFT = [_P, _P, _P, _P, _I64, _I64, _I32, _P, _P, _I64, _I64, _I32, _I32, _I32, _I32, _I32,
         _I32, _I32, _P, _P, _P, _P, _P, _P, _P]
+# tile64 sweep: A B Q R r_bs r_inv QT z0 z_bs batch n_alloc n_use s m tries t_min t_max J st ts js stream
+_LFT_T64 = [_P, _P, _P, _P, _I64, _I32, _P, _P, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32,
+            _I32, _P, _P, _P, _P, _P]
 _SEL = [_P, _I64, _I32, _I32, _I32, _P, _P, _P]
 _RIC64 = [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _P, _P,
           C.c_double, _U32, _I32, _I32, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]
@@ -52,6 +55,11 @@ SIGNATURES = {
     "hop_build_flags": (C.c_int, []),
     "hop_lft_sweep_f64": (C.c_int, _LFT),
     "hop_lft_sweep_f32": (C.c_int, _LFT),
+    "hop_lft_sweep_tile64_f64": (C.c_int, _LFT_T64),
+    "hop_lft_sweep_tile64_f32": (C.c_int, _LFT_T64),
+    "hop_tile64_elems": (C.c_int64, [_I64, _I32, _I32]),
+    "hop_tile64_f64": (C.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P]),
+    "hop_tile64_f32": (C.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P]),
     "hop_select_horizon_f64": (C.c_int, _SEL),
     "hop_select_horizon_f32": (C.c_int, _SEL),
     "hop_augment_f64": (C.c_int, _TRJ64 + _AUG_TAIL),

@@ -1,5 +1,6 @@
 // extern "C" boundary of libhop_amd.so (include/hop.h): argument validation,
 // kernel dispatch, the horizon argmin kernel.
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -59,7 +60,7 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
               int32_t n_alloc, int32_t n_use, int32_t s, int32_t m, int32_t max_tries,
               int32_t t_min, int32_t t_max, T* J, int32_t* status, int32_t* t_star, T* j_star,
               T* dbg_efg, T* dbg_pre, void* stream,
-              const hop::TrajArgs<T>* traj = nullptr) {
+              const hop::TrajArgs<T>* traj = nullptr, bool tile64 = false) {
   if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
   if (n_use <= 0 || batch == 0) return HOP_OK;  // reference: empty J
   if (s < 1 || s > HOP_MAX_DIM) return fail(HOP_E_SIZE, "s must be in [1, 16]");
@@ -82,6 +83,14 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
   a.t_min = t_min; a.t_max = t_max;
   a.J = J; a.status = status; a.t_star = t_star; a.j_star = j_star;
   a.dbg_efg = dbg_efg; a.dbg_pre = dbg_pre;
+  if (tile64) {  // the one-problem-per-lane kernels only (their native layout)
+    if (dbg_efg || dbg_pre) return fail(HOP_E_ARG, "tile64 layout: no debug outputs");
+    if (r_ks != 0) return fail(HOP_E_ARG, "tile64 layout: no per-step R");
+    a.tile64 = 1;
+    const hipError_t e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);
+    if (e != hipErrorNotSupported) return hip_status(e);
+    return fail(HOP_E_SIZE, "tile64 layout: no small-s kernel for this (s, m, dtype)");
+  }
   if (traj) {  // in-kernel augmentation: the s = 13 and the small-s kernels
     a.traj = 1;
     a.tr = *traj;
@@ -111,6 +120,41 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
     if (e != hipErrorNotSupported) return hip_status(e);
   }
   return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));
+}
+
+// tile64 <-> batch-major copy: dst element i of the tiled tensor
+// [ntiles][n_alloc][E][64] is src[(64 t + p) n_alloc E + k E + e] (0 past the
+// batch); inverse: the same map read the other way
+template <class T>
+__global__ __launch_bounds__(256) void tile64_kernel(const T* __restrict__ src, T* __restrict__ dst,
+                                                     long long batch, int n_alloc, int elems,
+                                                     int inverse, long long total) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+#pragma unroll 1
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int p = (int)(i & 63);
+    long long r = i >> 6;
+    const int e = (int)(r % elems);
+    r /= elems;
+    const int k = (int)(r % n_alloc);
+    const long long t = r / n_alloc, b = 64 * t + p;
+    const long long j = (b * n_alloc + k) * elems + e;
+    if (!inverse) dst[i] = b < batch ? src[j] : T(0);
+    else if (b < batch) dst[j] = src[i];
+  }
+}
+
+template <class T>
+int tile64_entry(const T* src, T* dst, int64_t batch, int32_t n_alloc, int32_t elems,
+                 int32_t inverse, void* stream) {
+  if (batch < 0 || n_alloc < 0 || elems < 1) return fail(HOP_E_ARG, "bad batch/n_alloc/elems");
+  if (batch == 0 || n_alloc == 0) return HOP_OK;
+  if (!src || !dst) return fail(HOP_E_ARG, "null pointer");
+  const long long total = (batch + 63) / 64 * 64 * (long long)n_alloc * elems;
+  const long long blocks = std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(tile64_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     src, dst, (long long)batch, n_alloc, elems, inverse ? 1 : 0, total);
+  return hip_status(hipGetLastError());
 }
 
 template <class T>
@@ -296,6 +340,39 @@ int hop_lft_sweep_f32(const float* A, const float* B, const float* Q, const floa
   return lft_entry<float>(A, B, Q, R, r_bs, r_ks, r_inv, QT, z0, z_bs, batch, n_alloc, n_use, s,
                           m, max_tries, t_min, t_max, J, status, t_star, j_star, dbg_efg,
                           dbg_prefix, stream);
+}
+
+int hop_lft_sweep_tile64_f64(const double* A, const double* B, const double* Q, const double* R,
+                             int64_t r_bs, int32_t r_inv, const double* QT, const double* z0,
+                             int64_t z_bs, int64_t batch, int32_t n_alloc, int32_t n_use,
+                             int32_t s, int32_t m, int32_t max_tries, int32_t t_min,
+                             int32_t t_max, double* J, int32_t* status, int32_t* t_star,
+                             double* j_star, void* stream) {
+  return lft_entry<double>(A, B, Q, R, r_bs, 0, r_inv, QT, z0, z_bs, batch, n_alloc, n_use, s, m,
+                           max_tries, t_min, t_max, J, status, t_star, j_star, nullptr, nullptr,
+                           stream, nullptr, true);
+}
+int hop_lft_sweep_tile64_f32(const float* A, const float* B, const float* Q, const float* R,
+                             int64_t r_bs, int32_t r_inv, const float* QT, const float* z0,
+                             int64_t z_bs, int64_t batch, int32_t n_alloc, int32_t n_use,
+                             int32_t s, int32_t m, int32_t max_tries, int32_t t_min,
+                             int32_t t_max, float* J, int32_t* status, int32_t* t_star,
+                             float* j_star, void* stream) {
+  return lft_entry<float>(A, B, Q, R, r_bs, 0, r_inv, QT, z0, z_bs, batch, n_alloc, n_use, s, m,
+                          max_tries, t_min, t_max, J, status, t_star, j_star, nullptr, nullptr,
+                          stream, nullptr, true);
+}
+int64_t hop_tile64_elems(int64_t batch, int32_t n_alloc, int32_t elems) {
+  if (batch < 0 || n_alloc < 0 || elems < 0) return -1;
+  return (batch + 63) / 64 * 64 * (int64_t)n_alloc * elems;
+}
+int hop_tile64_f64(const double* src, double* dst, int64_t batch, int32_t n_alloc, int32_t elems,
+                   int32_t inverse, void* stream) {
+  return tile64_entry<double>(src, dst, batch, n_alloc, elems, inverse, stream);
+}
+int hop_tile64_f32(const float* src, float* dst, int64_t batch, int32_t n_alloc, int32_t elems,
+                   int32_t inverse, void* stream) {
+  return tile64_entry<float>(src, dst, batch, n_alloc, elems, inverse, stream);
 }
 
 int hop_select_horizon_f64(const double* J, int64_t batch, int32_t ld, int32_t t_min,

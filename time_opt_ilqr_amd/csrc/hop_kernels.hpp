@@ -74,6 +74,7 @@ struct LftArgs {
   T* dbg_pre;        // [B][n][3][s][s] or null  (Ebar_k, Fbar_k, Gbar_k)
   int traj;          // 1: A/B/Q/QT unused, blocks built in-kernel from `tr`
   int cond;          // SchedCond: bit 0 rerun launch (only ST_RERUN problems), bit 1 flag all
+  int tile64;        // 1: A/B/Q/QT in the tile64 layout [B/64][nalloc][block elems][64]
   TrajArgs<T> tr;
 };
 

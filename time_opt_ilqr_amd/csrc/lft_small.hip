@@ -52,28 +52,51 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
       "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds), "s"(soff)
+      : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds)),
+        "s"(__builtin_amdgcn_readfirstlane(soff))
       : "memory");
 }
 
-template <class T, int S, int MM>
+// PW problems per wave: 64 (one per lane), or 32 (lanes 32..63 recompute lanes
+// 0..31's problems and store nothing) so that a batch of 64 problems per SIMD
+// runs as two waves per SIMD that hide each other's dependency stalls
+template <class T, int S, int MM, int PW = 64>
 struct Geo {
   static constexpr int CM = (S * S * (int)sizeof(T) + 15) / 16;   // chunks per s x s block
   static constexpr int CB = (S * MM * (int)sizeof(T) + 15) / 16;  // chunks per B block
   static constexpr int P_Q = 0, P_A = CM, P_B = 2 * CM, P_T = 2 * CM + CB;
   static constexpr int PIECES = 3 * CM + CB;
-  static constexpr int WAVE_BYTES = PIECES * 1024;
+  static constexpr int PIECE = 16 * PW;  // bytes per piece (one 16-B chunk per problem)
+  static constexpr int WAVE_BYTES = PIECES * PIECE;
   static constexpr int TPB = 256;  // 4 waves per block
+  static constexpr int PPB = 4 * PW;  // problems per block
+  // tile64 layout: a block's 64 problems are 64 S S (64 S MM) contiguous elements;
+  // lanes loading the last piece of a section (the rest would be the next step's)
+  static constexpr int LAST_M = (64 * S * S * (int)sizeof(T) - (CM - 1) * 1024) / 16;
+  static constexpr int LAST_B = (64 * S * MM * (int)sizeof(T) - (CB - 1) * 1024) / 16;
 };
 
-// read an (R x C) row-major block from the wave's chunk-major LDS image
-template <class T, int R, int C, int P0>
-__device__ __forceinline__ void read_block(const unsigned char* wimg, int lane, T (&out)[R][C]) {
+// read an (R x C) row-major block from the wave's LDS image.  LY 0: chunk-major
+// (piece r = the r-th 16-B chunk of every problem), LY 1: problem-major (the
+// problem's CH chunks contiguous at 16 CH slot), LY 2: element-major (element e of
+// problem p at TS (64 e + p): the image of the tiled HBM layout)
+template <class T, int R, int C, int P0, int PIECE = 1024, int LY = 0>
+__device__ __forceinline__ void read_block(const unsigned char* wimg, int slot, T (&out)[R][C]) {
   constexpr int NE = R * C, CH = (NE * (int)sizeof(T) + 15) / 16, PER = 16 / (int)sizeof(T);
+  if constexpr (LY == 2) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        out[i][j] = *reinterpret_cast<const T*>(wimg + P0 * 1024 +
+                                                 (int)sizeof(T) * (64 * (i * C + j) + slot));
+    return;
+  }
   T buf[CH * PER];
 #pragma unroll
   for (int r = 0; r < CH; ++r) {
-    const float4 v = *reinterpret_cast<const float4*>(wimg + (P0 + r) * 1024 + 16 * lane);
+    const float4 v = *reinterpret_cast<const float4*>(
+        LY == 1 ? wimg + P0 * 1024 + 16 * (CH * slot + r) : wimg + (P0 + r) * PIECE + 16 * slot);
     const T* e = reinterpret_cast<const T*>(&v);
 #pragma unroll
     for (int q = 0; q < PER; ++q) buf[r * PER + q] = e[q];
@@ -87,19 +110,27 @@ __device__ __forceinline__ void read_block(const unsigned char* wimg, int lane, 
 // COND: the conditioned-prefix association (small_math.hpp cond_*; DESIGN.md
 // 3.0) with first-attempt inverses; problems it cannot take get status 16 and
 // are recomputed by the LFT instantiation in rerun mode (a.cond & 1).
-template <class T, int S, int MM, bool COND = false>
-__global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
-  using G = Geo<T, S, MM>;
+// EXP (developer builds, timing experiments only -- results are wrong): 1 drops
+// the arithmetic (the LDS images are only summed), 2 streams step 0 only
+// PM: problem-major pieces (the wave's 64 CM chunks of a block in problem order,
+// so a wave-instruction reads ~64 / CM contiguous spans of 16 CM bytes instead of
+// 64 scattered 16-B chunks); only with PW = 64
+// LY 2 (timing experiment): the tiled HBM layout [B/64][nalloc][block elements][64]
+template <class T, int S, int MM, bool COND = false, int PW = 64, int EXP = 0, int LY = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 1 : 2))) void lft_small_kernel(LftArgs<T> a) {
+  using G = Geo<T, S, MM, PW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63, slot = lane & (PW - 1);
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned char* wimg = smem_raw + w * G::WAVE_BYTES;
   const unsigned wlds = (unsigned)(uintptr_t)wimg;
-  const long long wave_prob0 = (long long)blockIdx.x * G::TPB + w * 64;
-  const long long prob = wave_prob0 + lane;
-  bool valid = prob < a.batch;
-  const long long pb = valid ? prob : a.batch - 1;
-  const long long pb0 = wave_prob0 < a.batch ? wave_prob0 : a.batch - 1;
+  const long long wave_prob0 = (long long)blockIdx.x * G::PPB + w * PW;
+  const long long prob = wave_prob0 + slot;
+  const bool owner = PW == 64 || lane < PW;  // lanes past PW duplicate lane - PW
+  bool valid = owner && prob < a.batch;
+  const long long pb = prob < a.batch ? prob : a.batch - 1;
+  if (wave_prob0 >= a.batch) return;  // wave-uniform; no workgroup barrier in this kernel
+  const long long pb0 = wave_prob0;
   if (!COND && (a.cond & 1)) {  // rerun launch: only the problems the COND kernel handed over
     const bool need = valid && (a.status[prob] & 16);
     if (!__any(need)) return;  // wave-uniform; no workgroup barrier in this kernel
@@ -111,27 +142,57 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
   auto mk = [&](const T* base, long long pstr) {
     // exact bounds: range checking is per dword (tools/ubench_oob.hip), so a chunk
     // straddling the tensor end returns its valid dwords and zeros
-    const long long left = (a.batch - pb0) * pstr;
+    // (tile64: the tile is allocated whole, padding slots included)
+    const long long left = (LY == 2 ? 64 : a.batch - pb0) * pstr;
     const unsigned nrec = left > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)left;
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(base) + pb0 * (pstr / TS), (short)0,
                                              (int)nrec, 0x00020000);
   };
   const __amdgpu_buffer_rsrc_t rQ = mk(a.Q, pstrM), rA = mk(a.A, pstrM), rT = mk(a.QT, pstrM),
                                rB = mk(a.B, pstrB);
-  const unsigned vM = (unsigned)((pb - pb0) * pstrM), vB = (unsigned)((pb - pb0) * pstrB);
+  static_assert(LY == 0 || PW == 64, "layouts 1, 2 need 64 problems per wave");
+  constexpr bool PM = LY == 1;
+  unsigned vMr[G::CM], vBr[G::CB];  // per-piece lane source offsets (problem part)
+#pragma unroll
+  for (int r = 0; r < G::CM; ++r) {
+    const int q = 64 * r + lane, pp = PM ? q / G::CM : slot, cc = PM ? q % G::CM : r;
+    const long long pe = wave_prob0 + pp < a.batch ? wave_prob0 + pp : a.batch - 1;
+    vMr[r] = LY == 2 ? 1024u * r + 16u * lane : (unsigned)((pe - pb0) * pstrM) + 16u * cc;
+  }
+#pragma unroll
+  for (int r = 0; r < G::CB; ++r) {
+    const int q = 64 * r + lane, pp = PM ? q / G::CB : slot, cc = PM ? q % G::CB : r;
+    const long long pe = wave_prob0 + pp < a.batch ? wave_prob0 + pp : a.batch - 1;
+    vBr[r] = LY == 2 ? 1024u * r + 16u * lane : (unsigned)((pe - pb0) * pstrB) + 16u * cc;
+  }
+  // LDS-DMA writes lane l's 16 B at M0 + 16 l: with PW = 32 only the owner lanes
+  // load (the duplicates would write into the next piece)
   auto dma_stage = [&](int k) {  // Q, A, B of step k
-    const unsigned soM = (unsigned)(k * SS * TS), soB = (unsigned)(k * SM * TS);
+    const unsigned soM = (unsigned)(k * SS * TS * (LY == 2 ? 64 : 1)),
+                   soB = (unsigned)(k * SM * TS * (LY == 2 ? 64 : 1));
+    if (owner) {
 #pragma unroll
-    for (int r = 0; r < G::CM; ++r) dma16(vM + 16 * r, rQ, wlds + (G::P_Q + r) * 1024, soM);
+      for (int r = 0; r < G::CM; ++r)
+        if (LY != 2 || r + 1 < G::CM || lane < G::LAST_M)
+          dma16(vMr[r], rQ, wlds + (G::P_Q + r) * G::PIECE, soM);
 #pragma unroll
-    for (int r = 0; r < G::CM; ++r) dma16(vM + 16 * r, rA, wlds + (G::P_A + r) * 1024, soM);
+      for (int r = 0; r < G::CM; ++r)
+        if (LY != 2 || r + 1 < G::CM || lane < G::LAST_M)
+          dma16(vMr[r], rA, wlds + (G::P_A + r) * G::PIECE, soM);
 #pragma unroll
-    for (int r = 0; r < G::CB; ++r) dma16(vB + 16 * r, rB, wlds + (G::P_B + r) * 1024, soB);
+      for (int r = 0; r < G::CB; ++r)
+        if (LY != 2 || r + 1 < G::CB || lane < G::LAST_B)
+          dma16(vBr[r], rB, wlds + (G::P_B + r) * G::PIECE, soB);
+    }
   };
   auto dma_query = [&](int k) {  // QT of step k
-    const unsigned soM = (unsigned)(k * SS * TS);
+    const unsigned soM = (unsigned)(k * SS * TS * (LY == 2 ? 64 : 1));
+    if (owner) {
 #pragma unroll
-    for (int r = 0; r < G::CM; ++r) dma16(vM + 16 * r, rT, wlds + (G::P_T + r) * 1024, soM);
+      for (int r = 0; r < G::CM; ++r)
+        if (LY != 2 || r + 1 < G::CM || lane < G::LAST_M)
+          dma16(vMr[r], rT, wlds + (G::P_T + r) * G::PIECE, soM);
+    }
   };
   auto vm_wait = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
 
@@ -189,12 +250,22 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
     {
       Gen<T, S> Q, A;
       T Bk[S][MM];
-      read_block<T, S, S, G::P_Q>(wimg, lane, Q.a);
-      read_block<T, S, S, G::P_A>(wimg, lane, A.a);
-      read_block<T, S, MM, G::P_B>(wimg, lane, Bk);
+      read_block<T, S, S, G::P_Q, G::PIECE, LY>(wimg, slot, Q.a);
+      read_block<T, S, S, G::P_A, G::PIECE, LY>(wimg, slot, A.a);
+      read_block<T, S, MM, G::P_B, G::PIECE, LY>(wimg, slot, Bk);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (k + 1 < N) dma_stage(k + 1);
-      if constexpr (COND) {
+      if (k + 1 < N && EXP != 2) dma_stage(k + 1);
+      if constexpr (EXP == 1) {
+        T acc = T(0);
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+#pragma unroll
+          for (int j = 0; j < S; ++j) acc += Q.a[i][j] + A.a[i][j];
+#pragma unroll
+          for (int j = 0; j < MM; ++j) acc += Bk[i][j];
+        }
+        ps.best += acc;
+      } else if constexpr (COND) {
         Sym<T, S> E;
         sym_of(E, Q);
         cs.bad = cs.bad || !spd_inverse_once(E);
@@ -204,11 +275,17 @@ __global__ __launch_bounds__(256, 1) void lft_small_kernel(LftArgs<T> a) {
       }
     }
     Gen<T, S> QT;
-    read_block<T, S, S, G::P_T>(wimg, lane, QT.a);
+    read_block<T, S, S, G::P_T, G::PIECE, LY>(wimg, slot, QT.a);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (k + 1 < N) dma_query(k + 1);
+    if (k + 1 < N && EXP != 2) dma_query(k + 1);
     T jk;
-    if constexpr (COND) jk = cond_query<T, S, MM>(cs, QT);
+    if constexpr (EXP == 1) {
+      jk = ps.best;
+#pragma unroll
+      for (int i = 0; i < S; ++i)
+#pragma unroll
+        for (int j = 0; j < S; ++j) jk += QT.a[i][j];
+    } else if constexpr (COND) jk = cond_query<T, S, MM>(cs, QT);
     else jk = query<T, S, MM>(ps, QT, z, mt);
 #pragma unroll
     for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
@@ -487,22 +564,24 @@ template <class T>
 hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
   if (a.traj && (a.tr.n != a.s - 1 || a.tr.m != a.m || !a.r_is_inv)) return hipErrorNotSupported;
+  // Batch-major blocks stream as problem-major pieces (LY 1); tile64 blocks (LY 2)
+  // as contiguous 1-KiB pieces.  The batch-major stream is the bound at config 3:
+  // its DMA alone takes 1.54 ms, the tile64 one 0.80 ms (tools/exp_tiled.py).
   // Developer builds also carry the conditioned-prefix instantiation (variant 61:
   // it, then the LFT instantiation in rerun mode for the problems it flagged; 62:
-  // the COND kernel alone, A/B).  Off by default and absent from product builds:
-  // one problem per lane at one wave per SIMD is latency-bound, and the
-  // conditioned step measured slower here (config 3: 30.5 M vs 39.7 M sweeps/s)
-  // although it issues half the FLOPs
-  auto go1 = [&](auto kl, int bytes) {
-    const long long blocks = (a.batch + 255) / 256;
+  // the COND kernel alone, A/B) and the layout / occupancy experiments (72-78).
+  // The conditioned step issues half the FLOPs but its loop-carried chain is no
+  // shorter, and the stream, not the arithmetic, bounds this kernel
+  auto go1 = [&](auto kl, int bytes, int ppb = 256) {
+    const long long blocks = (a.batch + ppb - 1) / ppb;
     hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
     return hipGetLastError();
   };
 #ifdef HOP_DEV
-  const int cmode = g_opt_variant == 61 ? 1 : g_opt_variant == 62 ? 2 : 0;
-  auto go2 = [&](auto kc, auto kl, int bytes) {
-    if (cmode == 0) return go1(kl, bytes);
-    const long long blocks = (a.batch + 255) / 256;
+  const int cmode = (g_opt_variant == 61 || g_opt_variant == 73) ? 1 : g_opt_variant == 62 ? 2 : 0;
+  auto go2 = [&](auto kc, auto kl, int bytes, int ppb = 256) {
+    if (cmode == 0) return go1(kl, bytes, ppb);
+    const long long blocks = (a.batch + ppb - 1) / ppb;
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
     hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
@@ -512,21 +591,50 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
     hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
     return hipGetLastError();
   };
+  // variant 72: 32 problems per wave (two waves per SIMD), A/B against 64;
+  // 73: the conditioned association at 32 problems per wave + the rerun launch
 #define HOP_SMALL(S_, M_)                                                                 \
-  if (a.s == S_ && a.m == M_)                                                             \
+  if (a.s == S_ && a.m == M_) {                                                           \
+    if (a.tile64) {                                                                       \
+      if (g_opt_variant == 78)                                                            \
+        return go1(small::lft_small_kernel<T, S_, M_, false, 64, 1, 2>,                   \
+                   small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                \
+      return go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,                     \
+                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+    }                                                                                     \
+    if (!a.traj && g_opt_variant == 72)                                                   \
+      return go1(small::lft_small_kernel<T, S_, M_, false, 32>,                           \
+                 small::Geo<T, S_, M_, 32>::WAVE_BYTES * 4, small::Geo<T, S_, M_, 32>::PPB); \
+    if (!a.traj && (g_opt_variant == 74 || g_opt_variant == 75))                          \
+      return go1(g_opt_variant == 74 ? small::lft_small_kernel<T, S_, M_, false, 64, 1>     \
+                                     : small::lft_small_kernel<T, S_, M_, false, 64, 2>,    \
+                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+    if (!a.traj && g_opt_variant == 76)                                                   \
+      return go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 0>,                     \
+                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+    if (!a.traj && g_opt_variant == 77)                                                   \
+      return go1(small::lft_small_kernel<T, S_, M_, false, 64, 1, 1>,                     \
+                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+    if (!a.traj && g_opt_variant == 73)                                                   \
+      return go2(small::lft_small_kernel<T, S_, M_, true, 32>,                            \
+                 small::lft_small_kernel<T, S_, M_, false, 32>,                           \
+                 small::Geo<T, S_, M_, 32>::WAVE_BYTES * 4, small::Geo<T, S_, M_, 32>::PPB); \
     return a.traj ? go2(small::lft_small_traj_kernel<T, S_, M_, true>,                    \
                         small::lft_small_traj_kernel<T, S_, M_, false>,                   \
                         small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                          \
-                  : go2(small::lft_small_kernel<T, S_, M_, true>,                         \
-                        small::lft_small_kernel<T, S_, M_, false>,                        \
-                        small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+                  : go2(small::lft_small_kernel<T, S_, M_, true, 64, 0, 1>,               \
+                        small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,              \
+                        small::Geo<T, S_, M_>::WAVE_BYTES * 4);                          \
+  }
 #else
 #define HOP_SMALL(S_, M_)                                                                 \
   if (a.s == S_ && a.m == M_)                                                             \
-    return a.traj ? go1(small::lft_small_traj_kernel<T, S_, M_, false>,                   \
-                        small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                          \
-                  : go1(small::lft_small_kernel<T, S_, M_, false>,                        \
-                        small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+    return a.tile64 ? go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,            \
+                          small::Geo<T, S_, M_>::WAVE_BYTES * 4)                         \
+           : a.traj ? go1(small::lft_small_traj_kernel<T, S_, M_, false>,                 \
+                          small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                        \
+                    : go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,            \
+                          small::Geo<T, S_, M_>::WAVE_BYTES * 4);
 #endif
   if constexpr (sizeof(T) == 4) {
     HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)

@@ -53,6 +53,98 @@ class SweepResult:
     prefix: "object" = None  # [B, n_use, 3, s, s]  (Ebar_k, Fbar_k, Gbar_k)
 
 
+@dataclass
+class Tile64:
+    """A block tensor in the tile64 layout of include/hop.h: ``data`` is
+    [ceil(batch/64), N, rows*cols, 64] (element e of step k of problem b at
+    data[b // 64, k, e, b % 64]).  The native layout of the s <= 5 sweep: a wave
+    of 64 problems streams each block of a step as one contiguous span."""
+    data: "object"
+    batch: int
+    rows: int
+    cols: int
+
+    @property
+    def shape(self):
+        return (self.batch, int(self.data.shape[1]), self.rows, self.cols)
+
+    @property
+    def dtype(self):
+        return self.data.dtype
+
+    @property
+    def device(self):
+        return self.data.device
+
+
+def to_tile64(x) -> Tile64:
+    """[B, N, r, c] batch-major device blocks -> Tile64 (one hop_tile64 copy; padding
+    slots of the last tile are 0)."""
+    torch = _torch()
+    x = _dev(x, "x")
+    if x.dim() != 4:
+        raise ValueError(f"blocks must be [B, N, r, c], got {tuple(x.shape)}")
+    Bn, N, r, c = (int(v) for v in x.shape)
+    out = torch.empty(((Bn + 63) // 64, N, r * c, 64), dtype=x.dtype, device=x.device)
+    _lib.check(_fn("hop_tile64", x.dtype)(_lib.ptr(x), _lib.ptr(out), Bn, N, r * c, 0,
+                                          _lib.stream_handle(x.device)))
+    return Tile64(out, Bn, r, c)
+
+
+def from_tile64(t: Tile64):
+    """Tile64 -> [B, N, r, c] batch-major blocks (hop_tile64 inverse)."""
+    torch = _torch()
+    data = _dev(t.data, "tile64 data")
+    out = torch.empty(t.shape, dtype=data.dtype, device=data.device)
+    _lib.check(_fn("hop_tile64", data.dtype)(_lib.ptr(data), _lib.ptr(out), t.batch,
+                                             int(data.shape[1]), t.rows * t.cols, 1,
+                                             _lib.stream_handle(data.device)))
+    return out
+
+
+def _propagate_tile64(A, B, Q, R, z0, QT, n_use, r_is_inverse, max_tries, t_min, t_max, out):
+    torch = _torch()
+    for name, t in (("A", A), ("B", B), ("Q", Q), ("QT", QT)):
+        if not isinstance(t, Tile64):
+            raise TypeError(f"{name}: tile64 sweep needs every block tensor as Tile64")
+    Bn, N, s, _ = A.shape
+    m = B.cols
+    dt, dev = A.dtype, A.device
+    for name, t, cols in (("B", B, m), ("Q", Q, s), ("QT", QT, s), ("A", A, s)):
+        if t.shape != (Bn, N, s, cols) or t.dtype != dt or t.device != dev:
+            raise ValueError(f"{name}: tile64 blocks {t.shape} do not match A {A.shape}")
+        _dev(t.data, name, dt, dev)
+    R = _dev(R, "R", dt, dev)
+    z0 = _dev(z0, "z0", dt, dev)
+    n_use = N if n_use is None else int(n_use)
+    if n_use > N:
+        raise IndexError(f"T_use={n_use} exceeds the {N} stages supplied")
+    if R.dim() == 2:
+        r_bs = 0
+    elif R.dim() == 3:
+        r_bs = 0 if R.shape[0] == 1 else m * m
+    else:
+        raise ValueError("tile64 sweep: R must be [m, m] or [B or 1, m, m] (no per-step R)")
+    if tuple(R.shape[-2:]) != (m, m):
+        raise ValueError(f"R blocks must be {m}x{m}")
+    if z0.shape[-1] != s or (z0.dim() == 2 and z0.shape[0] not in (1, Bn)):
+        raise ValueError("z0 must be [s] or [B, s]")
+    z_bs = 0 if z0.dim() == 1 or z0.shape[0] == 1 else s
+    n_eff = max(n_use, 0)
+    J = torch.empty((Bn, n_eff), dtype=dt, device=dev) if out is None else out
+    status = (torch.empty if n_eff > 0 else torch.zeros)((Bn,), dtype=torch.int32, device=dev)
+    fuse = t_max is not None
+    ts = torch.empty((Bn,), dtype=torch.int32, device=dev) if fuse else None
+    js = torch.empty((Bn,), dtype=dt, device=dev) if fuse else None
+    rc = _fn("hop_lft_sweep_tile64", dt)(
+        _lib.ptr(A.data), _lib.ptr(B.data), _lib.ptr(Q.data), _lib.ptr(R), r_bs,
+        1 if r_is_inverse else 0, _lib.ptr(QT.data), _lib.ptr(z0), z_bs, Bn, N, n_use, s, m,
+        int(max_tries), int(t_min) if fuse else 0, int(t_max) if fuse else 0, _lib.ptr(J),
+        _lib.ptr(status), _lib.ptr(ts), _lib.ptr(js), _lib.stream_handle(dev))
+    _lib.check(rc)
+    return SweepResult(J, status, ts, js)
+
+
 def propagate(A, B, Q, R, z0, QT, *, n_use: Optional[int] = None, r_is_inverse: bool = True,
               max_tries: int = 8, t_min: Optional[int] = None, t_max: Optional[int] = None,
               return_efg: bool = False, return_prefix: bool = False, out=None) -> SweepResult:
@@ -62,8 +154,14 @@ def propagate(A, B, Q, R, z0, QT, *, n_use: Optional[int] = None, r_is_inverse: 
     R        : R^-1 if r_is_inverse (R_inv_cached) else raw R_k, shaped
                [m, m] | [Bn or 1, m, m] | [Bn or 1, N, m, m] (per step)
     n_use    : T_use (default N).  t_min/t_max: fuse the argmin (solver.py:522).
+    A, B, Q, QT may instead all be ``Tile64`` (s <= 5 shapes; see to_tile64).
     """
     torch = _torch()
+    if isinstance(A, Tile64):
+        if return_efg or return_prefix:
+            raise ValueError("tile64 sweep: no debug outputs")
+        return _propagate_tile64(A, B, Q, R, z0, QT, n_use, r_is_inverse, max_tries, t_min,
+                                 t_max, out)
     dt = A.dtype
     A = _dev(A, "A", dt)
     dev = A.device
