@@ -215,17 +215,41 @@ def _config5_workload(args, world, lo, hi, dev):
     import torch
     from time_opt_ilqr_amd import engine, synth
     N = args.N
-    mb, _ = synth.config5_batch(hi - lo, N, seed=77 + lo, device=dev, dtype=torch.float32)
+    Bn = hi - lo
+    mb, groups = synth.config5_batch(Bn, N, seed=77 + lo, device=dev, dtype=torch.float32)
     t_min = min(args.t_min, N)
 
-    def launch():
+    def launch_padded():
         return engine.propagate(mb.A, mb.B, mb.Q, mb.R_inv, mb.z0, mb.QT, t_min=t_min, t_max=N)
 
+    if args.layout in ("auto", "bucketed"):
+        # shape buckets: the Quadrotor third on the s=13 fp32-block kernel, the
+        # Segway / Cartpole members at their true s=5 on the small-s kernel (tile64
+        # blocks, side stream); J as the padded launch (block-decoupled embedding)
+        from time_opt_ilqr_amd.packing import merge_by_shape
+        sgroups, sorder = merge_by_shape(groups, torch.arange(Bn) % 3)  # s=5 kinds: one launch
+        plan = engine.mixed_plan(sorder, len(sgroups), dev)
+        tg = []
+        for A, B, Q, Ri, z0, QT in sgroups:
+            if A.shape[-1] <= 5:
+                A, B, Q, QT = (engine.to_tile64(x) for x in (A, B, Q, QT))
+            tg.append((A, B, Q, Ri, z0, QT))
+
+        def launch():
+            return engine.propagate_groups(tg, plan, t_min=t_min, t_max=N)
+
+        kname = ("lft_cond_kernel<SchedCond,13,4,float> (Quadrotor third) + "
+                 "lft_small_kernel<float,5,1,LY=2 tile64> (Segway/Cartpole, side stream)")
+        alg_bytes = (lft_bytes(N, 13, 4, 4) + 2 * lft_bytes(N, 5, 1, 4)) // 3
+        info = dict(kernel=kname, bound="fp64", flops=CONFIG5_ALG_FLOPS, bytes=alg_bytes,
+                    executed=None, t_min=t_min, t_max=N, s=13, m=4, N=N, host=None,
+                    alt=launch_padded, layout="shape-bucketed (true s; padded s=13 timed beside)")
+        return launch, info
     info = dict(kernel="lft_cond_kernel<SchedCond,13,4,float>", bound="fp64",
                 flops=CONFIG5_ALG_FLOPS, bytes=lft_bytes(N, 13, 4, 4),
                 executed=cond_flops(N, 13, 4), t_min=t_min, t_max=N, s=13, m=4, N=N,
-                host=(mb.A, mb.B, mb.Q, mb.R_inv, mb.z0, mb.QT))
-    return launch, info
+                host=(mb.A, mb.B, mb.Q, mb.R_inv, mb.z0, mb.QT), layout="padded to s=13")
+    return launch_padded, info
 
 
 def _select_gains_workload(args, world, lo, hi, dev):
@@ -287,9 +311,11 @@ def main():
     ap.add_argument("--prewarm-s", type=float, default=0.5,
                     help="untimed launches before the warm-up steps (GPU clock ramp)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
-    ap.add_argument("--layout", choices=["auto", "batch", "tile64"], default="auto",
-                    help="block layout of the lft/config3 workloads (auto: tile64 for the "
-                         "config-3 small-s shape, batch-major otherwise)")
+    ap.add_argument("--layout", choices=["auto", "batch", "tile64", "bucketed", "padded"],
+                    default="auto",
+                    help="lft/config3: block layout (auto: tile64 for the config-3 small-s "
+                         "shape, batch-major otherwise); config5: shape-bucketed (auto) or "
+                         "padded to s=13")
     args = ap.parse_args()
 
     import torch
@@ -443,14 +469,18 @@ def main():
             roof["arithmetic"] = "f64 (fp32 blocks in HBM/LDS)"
         if info["bound"] != "hbm":
             roof["hbm_gbs"] = info["bytes"] * per_launch / (kern_ms * 1e-3) / 1e9
-        if alt_ms is not None:
+        if alt_ms is not None and wl == "config5":
+            roof["padded_s13_ms"] = alt_ms
+            roof["padded_s13_frac"] = (info["flops"] * per_launch / (alt_ms * 1e-3) / 1e12
+                                       / peak)
+        elif alt_ms is not None:
             roof["batch_major_kernel_ms"] = alt_ms
             roof["batch_major_frac"] = (info["bytes"] * per_launch / (alt_ms * 1e-3) / 1e9
                                         / PEAK_HBM_GBS)
         names = {"lft": ("config 2: LFT sweep + fused argmin" if world == 1 else
                          "config 4 shard: LFT sweep + fused argmin"),
                  "config3": "config 3: LFT sweep + fused argmin (small-s kernel)",
-                 "config5": "config 5: mixed Segway/Cartpole/Quadrotor padded to s=13 m=4, "
+                 "config5": "config 5: mixed Segway/Cartpole/Quadrotor (i mod 3), "
                             "LFT sweep + fused argmin",
                  "select_gains": "select (in-kernel augmentation + LFT + argmin) + truncated "
                                  "Riccati gains at each T* (solver.py:581-597)"}

@@ -574,3 +574,27 @@ def test_block_decoupled_packing_matches_oracle_embedding():
         assert np.max(np.abs(J1 - J0) / J0) <= 1e-12
     assert mb.true_s.tolist() == [5, 5, 13, 5, 5, 13, 5]
     assert mb.true_m.tolist() == [1, 1, 4, 1, 1, 4, 1]
+
+
+def test_merge_by_shape_regroups_kinds_in_slot_order():
+    """packing.merge_by_shape (config 5 by shape bucket): kinds sharing (s, m) merge
+    into one group whose members follow the batch slots; other kinds pass through."""
+    import torch
+    from time_opt_ilqr_amd.packing import merge_by_shape
+    N = 3
+
+    def kind(b, s, m, base):
+        A = base + torch.arange(b, dtype=torch.float64).reshape(b, 1, 1, 1).expand(b, N, s, s)
+        return (A.clone(), torch.zeros(b, N, s, m), A.clone(), torch.eye(m),
+                torch.full((s,), base), A.clone())
+
+    groups = [kind(4, 5, 1, 100.0), kind(4, 5, 1, 200.0), kind(3, 13, 4, 300.0)]
+    order = torch.tensor([0, 1, 2, 0, 1, 2, 0, 1, 2, 0, 1])
+    sg, so = merge_by_shape(groups, order)
+    assert so.tolist() == [0, 0, 1, 0, 0, 1, 0, 0, 1, 0, 0]
+    assert len(sg) == 2 and sg[1][0] is groups[2][0]
+    A5 = sg[0][0][:, 0, 0, 0].tolist()
+    assert A5 == [100.0, 200.0, 101.0, 201.0, 102.0, 202.0, 103.0, 203.0]
+    assert sg[0][3].shape == (1, 1)  # equal shared R_inv stays shared
+    assert sg[0][4].shape == (8, 5)  # different shared z0 expanded per member
+    assert sg[0][4][:, 0].tolist() == [100.0, 200.0] * 4

@@ -34,7 +34,9 @@ constexpr int CH_U = MU * 8 / 16;       // 2 of u_k
 constexpr int OFF_A = 0, OFF_B = 5 * 1024, OFF_X = 7 * 1024, OFF_U = 8 * 1024;
 constexpr int BUF = 9 * 1024;               // second image at +BUF
 constexpr int OFF_T = 2 * BUF;              // transpose tiles
-constexpr int WAVE_BYTES = OFF_T + kProbPerWave * kLdsTile * 8;
+constexpr int OFF_Q = OFF_T + kProbPerWave * kLdsTile * 8;  // Q rows: problem g, row r, lane c
+constexpr int Q_PROB = NX * 16 * 8;                         // at OFF_Q + 1536 g + 128 r + 8 c
+constexpr int WAVE_BYTES = OFF_Q + kProbPerWave * Q_PROB;
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
@@ -112,6 +114,28 @@ __device__ __forceinline__ void read_step(const unsigned (&ad)[NX], unsigned xa,
         "i"(IMG)
       : "memory");
 }
+// ... and (Q) the step's Qxx accumulator start, Q row r on lane c, from the Q image
+template <int IMG>
+__device__ __forceinline__ void read_q12(unsigned qa, double (&q)[NX]) {
+  asm volatile(
+      "ds_read_b64 %0, %12 offset:0\n\t"
+      "ds_read_b64 %1, %12 offset:128\n\t"
+      "ds_read_b64 %2, %12 offset:256\n\t"
+      "ds_read_b64 %3, %12 offset:384\n\t"
+      "ds_read_b64 %4, %12 offset:512\n\t"
+      "ds_read_b64 %5, %12 offset:640\n\t"
+      "ds_read_b64 %6, %12 offset:768\n\t"
+      "ds_read_b64 %7, %12 offset:896\n\t"
+      "ds_read_b64 %8, %12 offset:1024\n\t"
+      "ds_read_b64 %9, %12 offset:1152\n\t"
+      "ds_read_b64 %10, %12 offset:1280\n\t"
+      "ds_read_b64 %11, %12 offset:1408\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]),
+        "=&v"(q[6]), "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11])
+      : "v"(qa)
+      : "memory");
+}
 template <int IMG>
 __device__ __forceinline__ void read_step_vt(const unsigned (&ad)[NX], unsigned xa, unsigned ua,
                                              unsigned ra, double (&ab)[NX], double& x, double& u,
@@ -152,6 +176,89 @@ __device__ __forceinline__ void read_step_vt(const unsigned (&ad)[NX], unsigned 
       : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]),
         "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(xa), "v"(ua),
         "v"(ra), "i"(IMG)
+      : "memory");
+}
+
+// read_step / read_step_vt plus the step's Qxx accumulator start (Q row r on lane c,
+// from the per-wave Q image) under the same wait
+template <int IMG>
+__device__ __forceinline__ void read_step_q(const unsigned (&ad)[NX], unsigned xa, unsigned ua, unsigned qa, double (&ab)[NX], double& x, double& u, double (&q)[NX]) {
+  asm volatile(
+      "ds_read_b64 %0, %26 offset:%c41\n\t"
+      "ds_read_b64 %1, %27 offset:%c41\n\t"
+      "ds_read_b64 %2, %28 offset:%c41\n\t"
+      "ds_read_b64 %3, %29 offset:%c41\n\t"
+      "ds_read_b64 %4, %30 offset:%c41\n\t"
+      "ds_read_b64 %5, %31 offset:%c41\n\t"
+      "ds_read_b64 %6, %32 offset:%c41\n\t"
+      "ds_read_b64 %7, %33 offset:%c41\n\t"
+      "ds_read_b64 %8, %34 offset:%c41\n\t"
+      "ds_read_b64 %9, %35 offset:%c41\n\t"
+      "ds_read_b64 %10, %36 offset:%c41\n\t"
+      "ds_read_b64 %11, %37 offset:%c41\n\t"
+      "ds_read_b64 %12, %38 offset:%c41\n\t"
+      "ds_read_b64 %13, %39 offset:%c41\n\t"
+      "ds_read_b64 %14, %40 offset:0\n\t"
+      "ds_read_b64 %15, %40 offset:128\n\t"
+      "ds_read_b64 %16, %40 offset:256\n\t"
+      "ds_read_b64 %17, %40 offset:384\n\t"
+      "ds_read_b64 %18, %40 offset:512\n\t"
+      "ds_read_b64 %19, %40 offset:640\n\t"
+      "ds_read_b64 %20, %40 offset:768\n\t"
+      "ds_read_b64 %21, %40 offset:896\n\t"
+      "ds_read_b64 %22, %40 offset:1024\n\t"
+      "ds_read_b64 %23, %40 offset:1152\n\t"
+      "ds_read_b64 %24, %40 offset:1280\n\t"
+      "ds_read_b64 %25, %40 offset:1408\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]), "=&v"(ab[7]), "=&v"(ab[8]), "=&v"(ab[9]), "=&v"(ab[10]), "=&v"(ab[11]), "=&v"(x), "=&v"(u), "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(xa), "v"(ua), "v"(qa), "i"(IMG)
+      : "memory");
+}
+template <int IMG>
+__device__ __forceinline__ void read_step_vt_q(const unsigned (&ad)[NX], unsigned xa, unsigned ua, unsigned ra, unsigned qa, double (&ab)[NX], double& x, double& u, double (&t)[NX], double (&q)[NX]) {
+  asm volatile(
+      "ds_read_b64 %0, %38 offset:%c54\n\t"
+      "ds_read_b64 %1, %39 offset:%c54\n\t"
+      "ds_read_b64 %2, %40 offset:%c54\n\t"
+      "ds_read_b64 %3, %41 offset:%c54\n\t"
+      "ds_read_b64 %4, %42 offset:%c54\n\t"
+      "ds_read_b64 %5, %43 offset:%c54\n\t"
+      "ds_read_b64 %6, %44 offset:%c54\n\t"
+      "ds_read_b64 %7, %45 offset:%c54\n\t"
+      "ds_read_b64 %8, %46 offset:%c54\n\t"
+      "ds_read_b64 %9, %47 offset:%c54\n\t"
+      "ds_read_b64 %10, %48 offset:%c54\n\t"
+      "ds_read_b64 %11, %49 offset:%c54\n\t"
+      "ds_read_b64 %12, %50 offset:%c54\n\t"
+      "ds_read_b64 %13, %51 offset:%c54\n\t"
+      "ds_read_b64 %14, %52 offset:0\n\t"
+      "ds_read_b64 %15, %52 offset:8\n\t"
+      "ds_read_b64 %16, %52 offset:16\n\t"
+      "ds_read_b64 %17, %52 offset:24\n\t"
+      "ds_read_b64 %18, %52 offset:32\n\t"
+      "ds_read_b64 %19, %52 offset:40\n\t"
+      "ds_read_b64 %20, %52 offset:48\n\t"
+      "ds_read_b64 %21, %52 offset:56\n\t"
+      "ds_read_b64 %22, %52 offset:64\n\t"
+      "ds_read_b64 %23, %52 offset:72\n\t"
+      "ds_read_b64 %24, %52 offset:80\n\t"
+      "ds_read_b64 %25, %52 offset:88\n\t"
+      "ds_read_b64 %26, %53 offset:0\n\t"
+      "ds_read_b64 %27, %53 offset:128\n\t"
+      "ds_read_b64 %28, %53 offset:256\n\t"
+      "ds_read_b64 %29, %53 offset:384\n\t"
+      "ds_read_b64 %30, %53 offset:512\n\t"
+      "ds_read_b64 %31, %53 offset:640\n\t"
+      "ds_read_b64 %32, %53 offset:768\n\t"
+      "ds_read_b64 %33, %53 offset:896\n\t"
+      "ds_read_b64 %34, %53 offset:1024\n\t"
+      "ds_read_b64 %35, %53 offset:1152\n\t"
+      "ds_read_b64 %36, %53 offset:1280\n\t"
+      "ds_read_b64 %37, %53 offset:1408\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]), "=&v"(ab[7]), "=&v"(ab[8]), "=&v"(ab[9]), "=&v"(ab[10]), "=&v"(ab[11]), "=&v"(x), "=&v"(u), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]), "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(xa), "v"(ua), "v"(ra), "v"(qa), "i"(IMG)
       : "memory");
 }
 
@@ -330,7 +437,9 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
                   pV0 = (long long)(NA + 1) * 8;
   constexpr bool wantv = WANTV;
   // stores per step, all issued unconditionally (non-committing lanes write out of
-  // range): K 4, k 1 [+ Vxx 12 (of the step before), Vx 1, V0 1]
+  // range): K 4, k 1 [+ Vxx 12 (of the step before), Vx 1, V0 1].  (Row c of the
+  // exactly symmetric V is also lane c's 12 registers, but 6 16-B stores of those
+  // rows scatter 48 16-B pieces per instruction and measured 5 % slower in mode 1.)
   constexpr int NST = 5 + (WANTV ? 14 : 0);
   unsigned va[5], vb[2], vx_, vu_;
 #pragma unroll
@@ -367,10 +476,14 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
 
   // loop-invariant cost blocks in registers: Q column c / row c, R column / row
   const int cq = c < S ? c : 0, cr = c < MM ? c : 0;
-  double qcol[S], qrow[S], rcol[MM], rrow[MM];
+  // Q row r on lane c (the Qxx accumulator start) lives in the wave's Q image and
+  // is re-read each step with the step's [A|B]; only Q's rows (for lx) stay in VGPRs
+  double qrow[S], rcol[MM], rrow[MM];
+  const unsigned qa = wlds + OFF_Q + Q_PROB * g + 8 * c;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    qcol[i] = c < S ? Qp[i * S + cq] : 0.0;
+    const double qv = c < S ? Qp[i * S + cq] : 0.0;
+    asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(qa), "v"(qv), "i"(128 * i) : "memory");
     qrow[i] = c < S ? Qp[cq * S + i] : 0.0;
   }
 #pragma unroll
@@ -455,24 +568,24 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
                  (unsigned)(i - 1) * (MM * 8));
     stamp(1);
     double ab[S], xi, ui;
+    double Qxx[S];  // Q (the accumulator start of Qxx = Q + A^T V A)
     if constexpr (FIRST) {
-      read_step<IMG>(ad, xa, ua, ab, xi, ui);
+      read_step_q<IMG>(ad, xa, ua, qa, ab, xi, ui, Qxx);
     } else {
       double t[S];
-      read_step_vt<IMG>(ad, xa, ua, tra, ab, xi, ui, t);
+      read_step_vt_q<IMG>(ad, xa, ua, tra, qa, ab, xi, ui, t, Qxx);
+      // _sym of step i+1's Vxx; a row that did not commit carried (and parked) its
+      // old, exactly symmetric V, for which this is V itself
 #pragma unroll
-      for (int r = 0; r < S; ++r) {
-        const double vs = 0.5 * (Vp[r] + t[r]);  // _sym of step i+1's Vxx
-        V[r] = cprev ? vs : V[r];
-      }
+      for (int r = 0; r < S; ++r) V[r] = 0.5 * (Vp[r] + t[r]);
     }
     // Vxx of step i+1 (mode 1 / requested): NST counts 12 stores here every step
     // (the first step's are out of range) so vm_wait_n stays exact
     if constexpr (WANTV && EXP != 1) {
       const bool wr = !FIRST && cprev && c < S;
-      const unsigned sv = (unsigned)(i + 1) * (S * S * 8);
+      const unsigned sv = (unsigned)(i + 1) * (S * S * 8), vo = wr ? voVxx : OOB;
 #pragma unroll
-      for (int r = 0; r < S; ++r) st64(V[r], rVxx, wr ? voVxx + 8u * S * r : OOB, sv);
+      for (int r = 0; r < S; ++r) st64(V[r], rVxx, vo + 8u * S * r, sv);
     }
     stamp(2);
     const bool act = alive && (i < L);
@@ -501,8 +614,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     zero(VA);
     static_for<S>([&](auto I) { LaneDot<S>::fma(VA[I], V[I], ab); });  // V [A|B]
     stamp(4);
-    double Qxx[S];
-    copy(Qxx, qcol);  // Q + A^T V A is accumulated under the Quu^-1 sweep below
+    // Q + A^T V A is accumulated into Qxx under the Quu^-1 sweep below
     double QB[MM];
     zero(QB);
     static_for<MM>([&](auto R) {  // B^T V [A|B]
@@ -642,8 +754,15 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
       if (bad || vfail) st |= ST_NONFINITE;
       alive = false;
     }
+    if (__any(!commit)) {  // a row keeps its V: carry and park that instead (rare but
+                           // for rows waiting for their horizon to start)
 #pragma unroll
-    for (int r = 0; r < S; ++r) Vp[r] = Vn[r];
+      for (int r = 0; r < S; ++r) Vp[r] = commit ? Vn[r] : V[r];
+      lds_park12(Vp, twa);
+    } else {
+#pragma unroll
+      for (int r = 0; r < S; ++r) Vp[r] = Vn[r];
+    }
     cprev = commit;
     vx = commit ? vxn : vx;
     v0 = commit ? v0n : v0;
@@ -652,9 +771,9 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     // not commit address out of range (dropped by the descriptor's range check)
     if constexpr (EXP != 1) {
       const bool wr = commit && c < S;
-      const unsigned so = (unsigned)i * (MM * S * 8);
+      const unsigned so = (unsigned)i * (MM * S * 8), vo = wr ? voK : OOB;
 #pragma unroll
-      for (int r = 0; r < MM; ++r) st64(K[r], rK, wr ? voK + 8u * S * r : OOB, so);
+      for (int r = 0; r < MM; ++r) st64(K[r], rK, vo + 8u * S * r, so);
       st64(kv, rk, (commit && c < MM) ? vok : OOB, (unsigned)i * (MM * 8));
       if constexpr (WANTV) {
         st64(vxn, rVx, wr ? voVx : OOB, (unsigned)i * (S * 8));

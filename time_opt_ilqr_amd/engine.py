@@ -219,6 +219,79 @@ def propagate(A, B, Q, R, z0, QT, *, n_use: Optional[int] = None, r_is_inverse: 
     return SweepResult(J, status, ts, js, efg, pre)
 
 
+@dataclass
+class MixedPlan:
+    """Batch slots of each shape group of a mixed batch (see propagate_groups)."""
+    slots: list          # per group: int64 device tensor of batch slots
+    batch: int
+
+
+def mixed_plan(order, n_groups: int, device) -> MixedPlan:
+    """order[i] = group of batch slot i; slot i takes the next unused member of
+    its group (the convention of packing.pack_mixed)."""
+    torch = _torch()
+    order = torch.as_tensor(order, dtype=torch.int64).cpu()
+    slots = [torch.nonzero(order == g).reshape(-1).to(device) for g in range(n_groups)]
+    return MixedPlan(slots, int(order.numel()))
+
+
+_SIDE = {}
+
+
+def _side_stream(device):
+    torch = _torch()
+    if device not in _SIDE:
+        _SIDE[device] = torch.cuda.Stream(device=device)
+    return _SIDE[device]
+
+
+def propagate_groups(groups, plan: MixedPlan, *, t_min: Optional[int] = None,
+                     t_max: Optional[int] = None, max_tries: int = 8) -> SweepResult:
+    """A mixed batch swept by shape bucket: config 5 without the
+    padding to s = 13.  groups[g] = (A, B, Q, R_inv, z0, QT) of group g's members
+    at their TRUE shape, in member order (A/B/Q/QT may be Tile64 for s <= 5);
+    plan.slots[g] = their batch slots.  Each group runs its own kernel -- the
+    s <= 5 groups on a side stream, beside the s = 13 launch -- and J [B, N],
+    status, T*, J* come back in batch order.  J equals that of the padded launch
+    (packing.pack_mixed: the block-decoupled embedding leaves it unchanged) up to
+    rounding; every group needs the same N."""
+    torch = _torch()
+    if len(groups) != len(plan.slots):
+        raise ValueError("one slot list per group")
+    first = groups[0][0]
+    dev, dt = first.device, first.dtype
+    N = int(first.shape[1])
+    fuse = t_max is not None
+    Bn = plan.batch
+    J = torch.empty((Bn, N), dtype=dt, device=dev)
+    status = torch.empty((Bn,), dtype=torch.int32, device=dev)
+    ts = torch.empty((Bn,), dtype=torch.int32, device=dev) if fuse else None
+    js = torch.empty((Bn,), dtype=dt, device=dev) if fuse else None
+    main = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(main)
+    for grp, slots in zip(groups, plan.slots):
+        A = grp[0]
+        if int(A.shape[1]) != N or A.dtype != dt:
+            raise ValueError("every group needs the same N and dtype")
+        if int(A.shape[0]) < int(slots.numel()):
+            raise ValueError("a group has fewer members than batch slots")
+        s = int(A.shape[2])
+        with torch.cuda.stream(side if s <= 5 else main):
+            r = propagate(*grp, t_min=t_min, t_max=t_max, max_tries=max_tries)
+            cnt = int(slots.numel())
+            J.index_copy_(0, slots, r.J[:cnt])
+            status.index_copy_(0, slots, r.status[:cnt])
+            if fuse:
+                ts.index_copy_(0, slots, r.t_star[:cnt])
+                js.index_copy_(0, slots, r.j_star[:cnt])
+    main.wait_stream(side)
+    for t in (J, status, ts, js):
+        if t is not None:
+            t.record_stream(side)
+    return SweepResult(J, status, ts, js)
+
+
 def select_horizon(J, t_min: int, t_max: int):
     """First minimiser over J[..., t_min-1 : t_max] (+t_min) -- solver.py:522."""
     torch = _torch()

@@ -128,3 +128,54 @@ def pack_mixed(groups: Sequence[tuple], order, s_out: int, m_out: int) -> MixedB
         out.true_s[slots] = A.shape[-1]
         out.true_m[slots] = B.shape[-1]
     return out
+
+
+def merge_by_shape(groups: Sequence[tuple], order):
+    """Regroup a mixed batch by block shape for engine.propagate_groups: kinds
+    that share (s, m) -- Segway and Cartpole in config 5 -- become one group (one
+    launch), its members in batch-slot order.  groups / order as pack_mixed
+    (R_inv and z0 may be shared per kind: [m, m] / [s]).  Returns (shape_groups,
+    shape_order) with shape_order[i] = shape group of slot i.  A setup-time
+    gather: one copy of the merged members."""
+    torch = _torch()
+    order = torch.as_tensor(order, dtype=torch.int64).cpu()
+    shapes, kind_to_shape = [], []
+    for grp in groups:
+        key = (int(grp[0].shape[-1]), int(grp[1].shape[-1]))
+        if key not in shapes:
+            shapes.append(key)
+        kind_to_shape.append(shapes.index(key))
+    shape_order = torch.as_tensor(kind_to_shape, dtype=torch.int64)[order]
+    rank = torch.empty_like(order)  # slot i is the rank[i]-th member of its kind
+    for g in range(len(groups)):
+        sl = torch.nonzero(order == g).reshape(-1)
+        rank[sl] = torch.arange(sl.numel())
+    out = []
+    for h in range(len(shapes)):
+        kinds = [g for g in range(len(groups)) if kind_to_shape[g] == h]
+        if len(kinds) == 1:
+            out.append(tuple(groups[kinds[0]]))
+            continue
+        sl = torch.nonzero(shape_order == h).reshape(-1)
+        kind_of, rank_of = order[sl], rank[sl]
+        parts = []
+        for j in range(6):
+            ts = [groups[g][j] for g in kinds]
+            full_dim = 3 if j == 3 else 2 if j == 4 else None
+            if full_dim is not None and all(t.dim() == full_dim - 1 for t in ts) and \
+                    all(torch.equal(t, ts[0]) for t in ts):
+                parts.append(ts[0])  # one shared block for the merged group
+                continue
+            if full_dim is not None:  # expand shared per-kind blocks to per member
+                ts = [t if t.dim() == full_dim else t.expand((groups[g][0].shape[0],) +
+                                                               tuple(t.shape)).contiguous()
+                      for g, t in zip(kinds, ts)]
+            ref = ts[0]
+            rows = torch.empty((sl.numel(),) + tuple(ref.shape[1:]), dtype=ref.dtype,
+                               device=ref.device)
+            for g, t in zip(kinds, ts):
+                m = torch.nonzero(kind_of == g).reshape(-1)
+                rows[m.to(ref.device)] = t[rank_of[m].to(ref.device)]
+            parts.append(rows)
+        out.append(tuple(parts))
+    return out, shape_order
