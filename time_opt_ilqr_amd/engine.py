@@ -6,6 +6,7 @@ All compute happens in libhop_amd.so; torch only owns memory and streams.
 """
 from __future__ import annotations
 
+import numbers
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -339,6 +340,17 @@ def _bstride(t, per, name, Bn):
     raise ValueError(f"{name} has unexpected shape {tuple(t.shape)}")
 
 
+def _per_problem(v, Bn, dtype, dev, name):
+    """[Bn] device tensor from a scalar (a device fill: no host-device copy that
+    would stall the launch queue), a tensor, or an array."""
+    torch = _torch()
+    if isinstance(v, numbers.Real) and not isinstance(v, bool):
+        return torch.full((Bn,), float(v) if dtype.is_floating_point else int(v), dtype=dtype,
+                          device=dev)
+    t = v if isinstance(v, torch.Tensor) else torch.as_tensor(v)
+    return _dev(t.to(device=dev, dtype=dtype).reshape(-1).expand(Bn), name)
+
+
 def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
             w_stage: float = 0.0, wrap_idx=None, qxx_extra=None, qx_extra=None, c_extra=None,
             reg_max_tries: int = 12, want_v: bool = False) -> RiccatiResult:
@@ -364,18 +376,21 @@ def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
     Q = _dev(Q, "Q", dt, dev)
     R = _dev(R, "R", dt, dev)
     Qf = _dev(Qf, "Qf", dt, dev)
-    horizon = _dev(torch.as_tensor(horizon, device=dev).to(torch.int32).reshape(-1)
-                   .expand(Bn), "horizon")
-    lm = _dev(torch.as_tensor(lm, device=dev, dtype=dt).reshape(-1).expand(Bn), "lm")
+    horizon = _per_problem(horizon, Bn, torch.int32, dev, "horizon")
+    lm = _per_problem(lm, Bn, dt, dev, "lm")
     ex = [None if t is None else _dev(t, nm, dt, dev)
           for t, nm in ((qxx_extra, "qxx_extra"), (qx_extra, "qx_extra"), (c_extra, "c_extra"))]
-    K = torch.zeros((Bn, N, m, n), dtype=dt, device=dev)
-    k = torch.zeros((Bn, N, m), dtype=dt, device=dev)
-    status = torch.zeros((Bn,), dtype=torch.int32, device=dev)
+    # outputs are written for steps < horizon[b] (Vxx/Vx/V0 up to horizon[b]) of
+    # problems that do not fail; the rest is left unwritten (the reference returns
+    # lists of length T*), so no fill kernel runs -- in mode 1 a zero fill of Vxx
+    # alone costs about a third of the pass
+    K = torch.empty((Bn, N, m, n), dtype=dt, device=dev)
+    k = torch.empty((Bn, N, m), dtype=dt, device=dev)
+    status = torch.empty((Bn,), dtype=torch.int32, device=dev)
     want = want_v or mode == 1
-    Vxx = torch.zeros((Bn, N + 1, n, n), dtype=dt, device=dev) if want else None
-    Vx = torch.zeros((Bn, N + 1, n), dtype=dt, device=dev) if want else None
-    V0 = torch.zeros((Bn, N + 1), dtype=dt, device=dev) if want else None
+    Vxx = torch.empty((Bn, N + 1, n, n), dtype=dt, device=dev) if want else None
+    Vx = torch.empty((Bn, N + 1, n), dtype=dt, device=dev) if want else None
+    V0 = torch.empty((Bn, N + 1), dtype=dt, device=dev) if want else None
     rc = _fn("hop_riccati", dt)(
         _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(X), _lib.ptr(U),
         _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref), _bstride(u_ref, 1, "u_ref", Bn),
@@ -501,7 +516,8 @@ def propagate_traj(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, *, wrap_idx=No
         raise IndexError(f"T_use={n_use} exceeds the {N} stages supplied")
     n_eff = max(n_use, 0)
     J = torch.empty((Bn, n_eff), dtype=dt, device=dev)
-    status = torch.zeros((Bn,), dtype=torch.int32, device=dev)
+    # every sweep kernel writes the status of each problem it runs
+    status = (torch.empty if n_eff > 0 else torch.zeros)((Bn,), dtype=torch.int32, device=dev)
     fuse = t_max is not None
     ts = torch.empty((Bn,), dtype=torch.int32, device=dev) if fuse else None
     js = torch.empty((Bn,), dtype=dt, device=dev) if fuse else None
