@@ -578,7 +578,10 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
     return hipGetLastError();
   };
 #ifdef HOP_DEV
-  const int cmode = (g_opt_variant == 61 || g_opt_variant == 73) ? 1 : g_opt_variant == 62 ? 2 : 0;
+  const int cmode = (g_opt_variant == 61 || g_opt_variant == 73 ||
+                     (a.tile64 && sizeof(T) == 4 && g_opt_variant == 0))
+                        ? 1
+                        : g_opt_variant == 62 ? 2 : 0;
   auto go2 = [&](auto kc, auto kl, int bytes, int ppb = 256) {
     if (cmode == 0) return go1(kl, bytes, ppb);
     const long long blocks = (a.batch + ppb - 1) / ppb;
@@ -596,6 +599,10 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
 #define HOP_SMALL(S_, M_)                                                                 \
   if (a.s == S_ && a.m == M_) {                                                           \
     if (a.tile64) {                                                                       \
+      if (cmode != 0 || (sizeof(T) == 4 && g_opt_variant == 0))                           \
+        return go2(small::lft_small_kernel<T, S_, M_, true, 64, 0, 2>,                    \
+                   small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,                   \
+                   small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                \
       if (g_opt_variant == 78)                                                            \
         return go1(small::lft_small_kernel<T, S_, M_, false, 64, 1, 2>,                   \
                    small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                \
@@ -627,14 +634,33 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
                         small::Geo<T, S_, M_>::WAVE_BYTES * 4);                          \
   }
 #else
+  // tile64 fp32: the conditioned association (half the FLOPs; its stream, not its
+  // arithmetic, is then the bound: config 3 0.83 ms against 0.91 for the LFT and
+  // 0.81 for the stream alone), then the LFT kernel in rerun mode for the problems
+  // it handed over (chol_inv ladders, status bits: the reference's semantics)
+  auto gocond = [&](auto kc, auto kl, int bytes) {
+    const long long blocks = (a.batch + 255) / 256;
+    LftArgs<T> c = a;
+    c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
+    hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
+    LftArgs<T> r = a;
+    r.cond = 1;
+    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
+    return hipGetLastError();
+  };
 #define HOP_SMALL(S_, M_)                                                                 \
-  if (a.s == S_ && a.m == M_)                                                             \
+  if (a.s == S_ && a.m == M_) {                                                           \
+    if (a.tile64 && sizeof(T) == 4)                                                       \
+      return gocond(small::lft_small_kernel<T, S_, M_, true, 64, 0, 2>,                   \
+                    small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,                  \
+                    small::Geo<T, S_, M_>::WAVE_BYTES * 4);                               \
     return a.tile64 ? go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,            \
                           small::Geo<T, S_, M_>::WAVE_BYTES * 4)                         \
            : a.traj ? go1(small::lft_small_traj_kernel<T, S_, M_, false>,                 \
                           small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                        \
                     : go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,            \
-                          small::Geo<T, S_, M_>::WAVE_BYTES * 4);
+                          small::Geo<T, S_, M_>::WAVE_BYTES * 4);                        \
+  }
 #endif
   if constexpr (sizeof(T) == 4) {
     HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)

@@ -351,6 +351,15 @@ def _per_problem(v, Bn, dtype, dev, name):
     return _dev(t.to(device=dev, dtype=dtype).reshape(-1).expand(Bn), name)
 
 
+def _scalar_or_vec(v, dtype, dev, name):
+    """[1] (a device fill) or [n] device tensor."""
+    torch = _torch()
+    if isinstance(v, numbers.Real) and not isinstance(v, bool):
+        return torch.full((1,), float(v), dtype=dtype, device=dev)
+    t = v if isinstance(v, torch.Tensor) else torch.as_tensor(v)
+    return _dev(t.to(device=dev, dtype=dtype).reshape(-1), name)
+
+
 def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
             w_stage: float = 0.0, wrap_idx=None, qxx_extra=None, qx_extra=None, c_extra=None,
             reg_max_tries: int = 12, want_v: bool = False) -> RiccatiResult:
@@ -441,7 +450,7 @@ def _traj_args(A, Bm, a_res, X, U, xg, u_ref, Q, P, w, wrap_idx, q_reg, rho_reg,
     u_ref = _dev(u_ref, "u_ref", dt, dev)
     Q = _dev(Q, "Q", dt, dev)
     P = _dev(P, "P", dt, dev)
-    w = _dev(torch.as_tensor(w, dtype=dt, device=dev).reshape(-1), "w", dt, dev)
+    w = _scalar_or_vec(w, dt, dev, "w")
     if w.numel() not in (1, Bn):
         raise ValueError("w must be a scalar or [B]")
     ex = [None if t is None else _dev(t, nm, dt, dev)
@@ -653,7 +662,7 @@ class CostParams:
         Q = _dev(self.Q, "Q", dt, dev)
         R = _dev(self.R, "R", dt, dev)
         Qf = _dev(self.Qf, "Qf", dt, dev)
-        w = _dev(torch.as_tensor(self.w, dtype=dt, device=dev).reshape(-1), "w", dt, dev)
+        w = _scalar_or_vec(self.w, dt, dev, "w")
         for t, nm, shp in ((xg, "xg", (n,)), (u_ref, "u_ref", (m,)), (Q, "Q", (n, n)),
                            (R, "R", (m, m)), (Qf, "Qf", (n, n))):
             if tuple(t.shape[-len(shp):]) != shp:

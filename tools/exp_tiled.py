@@ -1,6 +1,6 @@
-"""Timing experiment (developer build): the small-s kernel on a tiled HBM layout
-[B/64][N][block elements][64] (variant 79; 78 = its LDS-DMA alone) against the
-batch-major layout (variant 0).  Same problems, permuted into tiles; J compared.
+"""Timing experiment (developer build): the small-s sweep on tile64 blocks (include/hop.h)
+with the LFT association (variant 0), the conditioned association + rerun (61) and
+the stream alone (78), against batch-major blocks (variant 0).  J compared.
 
     HOP_LIB=<libhop_amd_dev.so> python tools/exp_tiled.py [--batch 65536] [--N 200] [--s 5] [--m 1]
 """
@@ -11,12 +11,6 @@ import statistics
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-
-
-def tile(x):
-    B, N = x.shape[:2]
-    E = x[0, 0].numel()
-    return x.reshape(B // 64, 64, N, E).permute(0, 2, 3, 1).contiguous().reshape(x.shape)
 
 
 def main():
@@ -35,32 +29,32 @@ def main():
     dt = torch.float32 if args.dtype == "f32" else torch.float64
     A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, args.s, args.m, args.N, seed=5,
                                               device=dev, dtype=dt)
-    At, Bt, Qt, QTt = tile(A), tile(Bm), tile(Q), tile(QT)
-    cases = {"0": (A, Bm, Q, QT), "76": (A, Bm, Q, QT), "79": (At, Bt, Qt, QTt),
-             "78": (At, Bt, Qt, QTt), "77": (A, Bm, Q, QT)}
+    tiled = [engine.to_tile64(x) for x in (A, Bm, Q, QT)]
+    cases = {"batch:0": ((A, Bm, Q, QT), 0), "tile:0": (tiled, 0), "tile:61": (tiled, 61),
+             "tile:78": (tiled, 78)}
     lib = _lib.load()
 
-    def run(v):
-        a, b, q, qt = cases[v]
-        _lib.check(lib.hop_set_options(0, int(v)))
-        return engine.propagate(a, b, q, Ri, z0, qt)
+    def run(c):
+        (a, b, q, qt), v = cases[c]
+        _lib.check(lib.hop_set_options(0, v))
+        return engine.propagate(a, b, q, Ri, z0, qt, t_min=20, t_max=args.N)
 
-    J0 = run("0").J
-    for v in ("76", "79"):
-        J = run(v).J
+    J0 = run("batch:0").J
+    for c in ("tile:0", "tile:61"):
+        J = run(c).J
         torch.cuda.synchronize()
-        print(v, "max rel vs 0:", float(((J - J0).abs() / J0.abs()).max()), flush=True)
-    times = {v: [] for v in cases}
+        print(c, "max rel vs batch-major:", float(((J - J0).abs() / J0.abs()).max()), flush=True)
+    times = {c: [] for c in cases}
     for _ in range(args.rounds):
-        for v in cases:
+        for c in cases:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(args.iters):
-                run(v)
+                run(c)
             e1.record()
             torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) / args.iters)
-    print(json.dumps({v: statistics.median(t) for v, t in times.items()}))
+            times[c].append(e0.elapsed_time(e1) / args.iters)
+    print(json.dumps({c: statistics.median(t) for c, t in times.items()}))
 
 
 if __name__ == "__main__":
