@@ -282,7 +282,7 @@ def _select_gains_workload(args, world, lo, hi, dev):
         sel.riccati_status = ric.status
         return sel
 
-    info = dict(kernel="lft_cond_cf_kernel<SchedCondTraj,13,4> + riccati_kernel<double,12,4>",
+    info = dict(kernel="lft_cond_cf_kernel<SchedCondTraj,13,4> + riccati_fast_kernel<0>",
                 bound="fp64", flops=lft_flops(N, n + 1, m) + riccati_flops(n, m, N),
                 bytes=8 * (N * (n * n + n * m + 2 * n + m) + n), executed=None,
                 t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
