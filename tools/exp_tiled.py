@@ -30,7 +30,7 @@ def main():
     A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, args.s, args.m, args.N, seed=5,
                                               device=dev, dtype=dt)
     tiled = [engine.to_tile64(x) for x in (A, Bm, Q, QT)]
-    cases = {"batch:0": ((A, Bm, Q, QT), 0), "tile:0": (tiled, 0), "tile:61": (tiled, 61),
+    cases = {"batch:0": ((A, Bm, Q, QT), 0), "tile:0": (tiled, 0), "tile:80": (tiled, 80),
              "tile:78": (tiled, 78)}
     lib = _lib.load()
 
@@ -40,7 +40,7 @@ def main():
         return engine.propagate(a, b, q, Ri, z0, qt, t_min=20, t_max=args.N)
 
     J0 = run("batch:0").J
-    for c in ("tile:0", "tile:61"):
+    for c in ("tile:0", "tile:80"):
         J = run(c).J
         torch.cuda.synchronize()
         print(c, "max rel vs batch-major:", float(((J - J0).abs() / J0.abs()).max()), flush=True)
