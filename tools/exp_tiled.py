@@ -1,6 +1,7 @@
-"""Timing experiment (developer build): the small-s sweep on tile64 blocks (include/hop.h)
-with the LFT association (variant 0), the conditioned association + rerun (61) and
-the stream alone (78), against batch-major blocks (variant 0).  J compared.
+"""Timing experiment (developer build): the small-s sweep on tile64 blocks (include/hop.h):
+the default (fp32: conditioned association + rerun), every problem handed over to the
+LFT kernel (HOP_OPT_FORCE_HANDOVER: the LFT association's time plus one conditioned
+pass) and the stream alone (variant 78), against batch-major blocks.  J compared.
 
     HOP_LIB=<libhop_amd_dev.so> python tools/exp_tiled.py [--batch 65536] [--N 200] [--s 5] [--m 1]
 """
@@ -30,17 +31,17 @@ def main():
     A, Bm, Q, Ri, z0, QT = synth.device_batch(args.batch, args.s, args.m, args.N, seed=5,
                                               device=dev, dtype=dt)
     tiled = [engine.to_tile64(x) for x in (A, Bm, Q, QT)]
-    cases = {"batch:0": ((A, Bm, Q, QT), 0), "tile:0": (tiled, 0), "tile:80": (tiled, 80),
-             "tile:78": (tiled, 78)}
+    cases = {"batch:0": ((A, Bm, Q, QT), 0, 0), "tile:0": (tiled, 0, 0),
+             "tile:handover": (tiled, 0, _lib.OPT_FORCE_HANDOVER), "tile:78": (tiled, 78, 0)}
     lib = _lib.load()
 
     def run(c):
-        (a, b, q, qt), v = cases[c]
-        _lib.check(lib.hop_set_options(0, v))
+        (a, b, q, qt), v, flags = cases[c]
+        _lib.check(lib.hop_set_options(flags, v))
         return engine.propagate(a, b, q, Ri, z0, qt, t_min=20, t_max=args.N)
 
     J0 = run("batch:0").J
-    for c in ("tile:0", "tile:80"):
+    for c in ("tile:0", "tile:handover"):
         J = run(c).J
         torch.cuda.synchronize()
         print(c, "max rel vs batch-major:", float(((J - J0).abs() / J0.abs()).max()), flush=True)
