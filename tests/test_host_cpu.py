@@ -598,3 +598,15 @@ def test_merge_by_shape_regroups_kinds_in_slot_order():
     assert sg[0][3].shape == (1, 1)  # equal shared R_inv stays shared
     assert sg[0][4].shape == (8, 5)  # different shared z0 expanded per member
     assert sg[0][4][:, 0].tolist() == [100.0, 200.0] * 4
+
+
+def test_tile64_descriptor_checks_shape():
+    """engine.Tile64.check: the kernels read whole tiles, so a data tensor that is not
+    exactly [ceil(batch/64), N, rows*cols, 64] is rejected before any launch."""
+    import torch
+    from time_opt_ilqr_amd.engine import Tile64
+    assert Tile64(torch.zeros(2, 3, 25, 64), 70, 5, 5).check().shape == (70, 3, 5, 5)
+    for bad in (torch.zeros(1, 3, 25, 64), torch.zeros(2, 3, 24, 64), torch.zeros(2, 3, 25, 32),
+                torch.zeros(2, 3, 25, 64).transpose(0, 1)):
+        with pytest.raises(ValueError):
+            Tile64(bad, 70, 5, 5).check()

@@ -69,6 +69,17 @@ class Tile64:
     def shape(self):
         return (self.batch, int(self.data.shape[1]), self.rows, self.cols)
 
+    def check(self, name="tile64"):
+        """The data tensor must be exactly [ceil(batch/64), N, rows*cols, 64]: the
+        kernels read whole tiles."""
+        d = self.data
+        want = ((self.batch + 63) // 64, int(d.shape[1]) if d.dim() == 4 else -1,
+                self.rows * self.cols, 64)
+        if d.dim() != 4 or tuple(d.shape) != want or not d.is_contiguous():
+            raise ValueError(f"{name}: tile64 data must be a contiguous {want} tensor, got "
+                             f"{tuple(d.shape)}")
+        return self
+
     @property
     def dtype(self):
         return self.data.dtype
@@ -95,7 +106,7 @@ def to_tile64(x) -> Tile64:
 def from_tile64(t: Tile64):
     """Tile64 -> [B, N, r, c] batch-major blocks (hop_tile64 inverse)."""
     torch = _torch()
-    data = _dev(t.data, "tile64 data")
+    data = _dev(t.check().data, "tile64 data")
     out = torch.empty(t.shape, dtype=data.dtype, device=data.device)
     _lib.check(_fn("hop_tile64", data.dtype)(_lib.ptr(data), _lib.ptr(out), t.batch,
                                              int(data.shape[1]), t.rows * t.cols, 1,
@@ -111,7 +122,8 @@ def _propagate_tile64(A, B, Q, R, z0, QT, n_use, r_is_inverse, max_tries, t_min,
     Bn, N, s, _ = A.shape
     m = B.cols
     dt, dev = A.dtype, A.device
-    for name, t, cols in (("B", B, m), ("Q", Q, s), ("QT", QT, s), ("A", A, s)):
+    for name, t, cols in (("A", A, s), ("B", B, m), ("Q", Q, s), ("QT", QT, s)):
+        t.check(name)
         if t.shape != (Bn, N, s, cols) or t.dtype != dt or t.device != dev:
             raise ValueError(f"{name}: tile64 blocks {t.shape} do not match A {A.shape}")
         _dev(t.data, name, dt, dev)
