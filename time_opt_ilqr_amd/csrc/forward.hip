@@ -193,7 +193,8 @@ __global__ __launch_bounds__(TPB) void cost_kernel(CostArgs c, const double* X, 
 }
 
 // ---------------------------------------------------------------- line search
-// pass 1: lane q = b * S + slot, S = n_alpha + 1; slot n_alpha computes J_old.
+// pass 1: lane q = b * n_alpha + slot rolls out step size `slot`; lane
+// batch * n_alpha + b computes problem b's J_old.
 // Step k+1's rows of X, U, K, k are loaded at the top of step k (register double
 // buffer), so their latency hides under step k's dynamics and cost.
 template <int SYS, bool SH, int WM>
@@ -235,11 +236,15 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
     cl.u_ref = sc + 2 * NQ + NR + n;
     cl.w = sc + 2 * NQ + NR + n + m;
   }
+  // lanes [0, batch * n_alpha): (problem, step size) rollouts; the J_old lanes of
+  // every problem come after them, so no wave mixes the two loops (a mixed wave
+  // runs both, one after the other)
   const int S = a.n_alpha + 1;
   const long long q = (long long)blockIdx.x * TPB + threadIdx.x;
   if (q >= a.batch * S) return;
-  const long long b = q / S;
-  const int slot = (int)(q - b * S);
+  const long long nr = a.batch * a.n_alpha;
+  const long long b = q < nr ? q / a.n_alpha : q - nr;
+  const int slot = q < nr ? (int)(q - b * a.n_alpha) : a.n_alpha;
   const int N = a.N;
   const double* X = a.X + b * (long long)(N + 1) * n;
   const double* U = a.U + b * (long long)N * m;
