@@ -528,3 +528,34 @@ def test_cond_nonfinite_short_horizons_and_tails(dev):
     assert int(one.status.abs().sum()) == 0
     empty = engine.propagate(*args, n_use=0)
     assert empty.J.shape == (Bn, 0) and int(empty.status.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("s,m", [(13, 4), (8, 2), (5, 1), (3, 1)])
+def test_nonfinite_inputs_status_and_curve_match_oracle(dev, s, m):
+    """chol_inv's _assert_finite (utils.py:77): a non-finite block raises in the
+    reference; the oracle reports its inverse as NaN with ST_NONFINITE alone (no
+    jitter ladder).  Every kernel family (s=13 default + rerun, generic s=8, small
+    s=5/3) gives the oracle's exact status word and NaN pattern, the finite
+    horizons to 1e-9: NaN in Q_k (every later horizon NaN), in QT_k (one horizon),
+    inf in A_k, NaN in z0, and an indefinite block beside them (jitter bits kept)."""
+    from time_opt_ilqr_amd import engine
+    Bn, N = 6, 14
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(7070 + s, Bn, s, m, N)
+    A, Q, QT, z0 = A.copy(), Q.copy(), QT.copy(), z0.copy()
+    Q[0, 4, 1, 2] = np.nan
+    QT[1, 6, 0, 0] = np.nan
+    A[2, 3, 0, 1] = np.inf
+    z0[3, 1] = np.nan
+    Q[4, 2] = Q[4, 2] - np.eye(s) * (np.linalg.eigvalsh(Q[4, 2]).min() + 5e-8)  # jitter
+    Q[5, 9, s - 1, 0] = -np.inf
+    res = engine.propagate(_t(A, dev), _t(Bm, dev), _t(Q, dev), _t(Ri, dev), _t(z0, dev),
+                           _t(QT, dev))
+    st = res.status.cpu().numpy()
+    J = res.J.cpu().numpy()
+    for b in range(Bn):
+        o = orc.lft_sweep(A[b], Bm[b], Q[b], Ri[b], z0[b], QT[b])
+        assert int(st[b]) == int(o["status"]), (b, int(st[b]), int(o["status"]))
+        nan = np.isnan(o["J"])
+        assert np.array_equal(np.isnan(J[b]), nan), (b, J[b], o["J"])
+        if b != 4 and not nan.all():  # b=4: the escalated block amplifies rounding
+            assert _elem_rel(J[b][~nan], o["J"][~nan]) <= 1e-9, b

@@ -252,7 +252,11 @@ def _traj_nonfinite_and_tiny_horizons(dev):
     args = (*_dev_args(st2, dev), _t(st["R_inv"], dev), _t(st["P"], dev), _t(st["w"], dev))
     res = engine.propagate_traj(*args, wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=5, t_max=5)
     status = res.status.cpu().numpy()
-    assert status[2] & 4
+    p2 = dict(ps[2])
+    p2["X"] = X[2]
+    _, o2 = _oracle(p2, 1.0)  # the oracle's status word and NaN pattern, exactly
+    assert int(status[2]) == int(o2["status"]) == 4
+    assert np.array_equal(np.isnan(res.J[2].cpu().numpy()), np.isnan(o2["J"]))
     assert (np.delete(status, 2) == 0).all()
     assert (np.delete(res.t_star.cpu().numpy(), 2) == 5).all()
     J = res.J.cpu().numpy()

@@ -213,14 +213,26 @@ __device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int m
   }
   T eps = T(1e-9);
   int tries = 0;
-  bool done = false;
+  bool done = false, nf = false;
 #pragma unroll 1
   while (true) {
     bool ok = true;
     sweep_neg_inverse(r, eps, c, ok);
+    if (tries == 0 && __any(!ok)) {
+      // chol_inv's _assert_finite (utils.py:77): a non-finite input never
+      // factors; no ladder for its row, the result is NaN with ST_NONFINITE
+      T z = T(0);
+      if (c < S) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) z = z + tile[i * kLdsRow + c] * T(0);
+      }
+      const unsigned long long m = __ballot(!(z == z));
+      nf = !ok && ((m >> (16 * ((threadIdx.x & 63) >> 4))) & 0xffffull) != 0ull;
+      if (nf) st |= ST_NONFINITE;
+    }
     const bool last = tries >= max_tries;
-    if (!done && !ok && last) st |= ST_LU;
-    done = ok || last;
+    if (!done && !ok && !nf && last) st |= ST_LU;
+    done = ok || last || nf;
     if (!__any(!done)) break;
     if (!done) {
       eps *= T(10);
@@ -234,7 +246,7 @@ __device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int m
   }
   wave_sync();
 #pragma unroll
-  for (int i = 0; i < S; ++i) r[i] = -r[i];
+  for (int i = 0; i < S; ++i) r[i] = nf ? T(__builtin_nan("")) : -r[i];
 }
 
 // Same, without the LU slot (utils.py:96-120 chol_solve): returns false when

@@ -273,6 +273,23 @@ __device__ __forceinline__ void diag_add(const double* img, int c, double delta)
   }
 }
 
+// chol_inv's _assert_finite (utils.py:77): a non-finite input raises in the
+// reference and can never factor, so its row runs no jitter ladder; the
+// inverse (or quadratic form) is NaN and the row gets ST_NONFINITE alone, as
+// the oracle's spd_inverse.  Checked only after a failed first attempt (rare
+// path): the input image at img (row-major, row stride LD: S rows, NC columns,
+// NC = S + 1 with the bordered column z0 of the query), one ballot.
+template <int S, int LD, int NC = S>
+__device__ __forceinline__ bool row_input_nonfinite(const double* img, int c) {
+  double z = 0.0;
+  if (c < NC) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) z = __builtin_fma(img[i * LD + c], 0.0, z);
+  }
+  const unsigned long long m = __ballot(!(z == z));
+  return ((m >> (16 * ((threadIdx.x & 63) >> 4))) & 0xffffull) != 0ull;
+}
+
 // Retry ladder shared by all inverses (utils.py:69-93 semantics): rows that
 // failed re-form their input with eps x 10; after max_tries the last sweep is
 // kept (LU slot) and flagged.  Rows that already succeeded recompute bitwise
@@ -283,10 +300,11 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
   double eps = ok0 ? 1e-9 : 1e-8;  // rows that succeeded keep their jitter
   double cur = 1e-9;               // offset form: jitter currently in the LDS diagonal
   int tries = ok0 ? 0 : 1;
-  bool done = ok0;
-  if (!ok0) st |= ST_JITTER;
+  const bool nf = !ok0 && row_input_nonfinite<S, LD>(img, c);
+  bool done = ok0 || nf;
+  if (!ok0) st |= nf ? ST_NONFINITE : ST_JITTER;
 #pragma unroll 1
-  while (true) {
+  while (__any(!done)) {
     if constexpr (offset_form<C>()) {
       diag_add<S, LD>(img, c, eps - cur);  // +0 for rows that keep their jitter
       cur = eps;
@@ -302,6 +320,10 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
       eps *= 10.0;
       ++tries;
     }
+  }
+  if (nf) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = __builtin_nan("");
   }
 }
 
@@ -375,10 +397,11 @@ __device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c
   {
     double eps = ok0 ? 1e-9 : 1e-8;
     int tries = ok0 ? 0 : 1;
-    bool done = ok0;
-    if (!ok0) st |= ST_JITTER;
+    const bool nf = !ok0 && row_input_nonfinite<S, kLdsRow, S + 1>(tile, c);
+    bool done = ok0 || nf;
+    if (!ok0) st |= nf ? ST_NONFINITE : ST_JITTER;
 #pragma unroll 1
-    while (true) {
+    while (__any(!done)) {
       sym_from<C, S, kLdsRow>(tile, c, r);
       bool ok2 = true;
       q = elim_quad<C, S>(r, eps, ok2);
@@ -391,6 +414,7 @@ __device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c
         ++tries;
       }
     }
+    if (nf) q = __builtin_nan("");
   }
   return q;
 }
@@ -417,10 +441,19 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
   if (__any(!ok0)) {
     double eps = ok0 ? 1e-9 : 1e-8, cur = 1e-9;
     int tries = ok0 ? 0 : 1;
-    bool done = ok0;
-    if (!ok0) st |= ST_JITTER;
+    // Xt + Gbar non-finite (or H, Ebar: X0 = Ebar - Fbar Wt Fbar^T is then NaN too)
+    bool nf = !ok0 && row_input_nonfinite<S, kLdsRow>(tile, c);
+    {
+      double z = 0.0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) z = __builtin_fma(H[i], 0.0, __builtin_fma(Eb[i], 0.0, z));
+      const unsigned long long m = __ballot(c < S && !(z == z));
+      nf = nf || (!ok0 && ((m >> (16 * ((threadIdx.x & 63) >> 4))) & 0xffffull) != 0ull);
+    }
+    bool done = ok0 || nf;
+    if (!ok0) st |= nf ? ST_NONFINITE : ST_JITTER;
 #pragma unroll 1
-    while (true) {
+    while (__any(!done)) {
       diag_add<S, kLdsRow>(tile, c, eps - cur);
       cur = eps;
       sym_from<C, S, kLdsRow>(tile, c, r);
@@ -437,6 +470,10 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
         eps *= 10.0;
         ++tries;
       }
+    }
+    if (nf) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) X0[i] = __builtin_nan("");
     }
   }
   wave_sync();

@@ -78,6 +78,15 @@ HOP_HD inline bool sweep_neg_inverse(Sym<T, S>& x, T eps) {
   return ok;
 }
 
+// every packed entry finite (x * 0 is 0 for finite x, NaN otherwise)
+template <class T, int S>
+HOP_HD inline bool all_finite(const Sym<T, S>& m) {
+  T z = T(0);
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) z = z + m.v[k] * T(0);
+  return z == z;
+}
+
 // chol_inv (utils.py:69-93) on an already symmetric input: jitter 1e-9, x10 per
 // failure; after max_tries the last attempt is kept (LU slot) and flagged.
 template <class T, int S>
@@ -85,6 +94,14 @@ HOP_HD inline void spd_inverse(Sym<T, S>& m, int max_tries, unsigned& st) {
   const Sym<T, S> in = m;
   T eps = T(1e-9);
   bool ok = sweep_neg_inverse(m, eps);
+  if (!ok && !all_finite(in)) {
+    // chol_inv's _assert_finite (utils.py:77): a non-finite input never factors;
+    // no ladder, the result is NaN with the non-finite bit (oracle spd_inverse)
+    st |= kStNonfinite;
+#pragma unroll
+    for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = T(__builtin_nan(""));
+    return;
+  }
   if (!ok) {
     st |= kStJitter;
     for (int tries = 1;; ++tries) {
@@ -128,7 +145,16 @@ HOP_HD inline T quad_inverse(const Sym<T, S>& x0, const T (&z)[S], int max_tries
       }
     }
     if (ok) return acc;
-    if (tries == 0) st |= kStJitter;
+    if (tries == 0) {  // a non-finite input runs no ladder (chol_inv's _assert_finite)
+      T zz = T(0);
+#pragma unroll
+      for (int i = 0; i < S; ++i) zz = zz + z[i] * T(0);
+      if (!all_finite(x0) || !(zz == zz)) {
+        st |= kStNonfinite;
+        return T(__builtin_nan(""));
+      }
+      st |= kStJitter;
+    }
     if (tries >= max_tries) {
       st |= kStLu;
       return acc;
