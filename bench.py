@@ -102,6 +102,19 @@ def riccati_flops(n, m, T, mode=0):
     return step * T
 
 
+def riccati_bytes(n, m, T, mode=0, want_v=None):
+    """Algorithmic HBM bytes per problem of one Riccati pass (fp64): per step A_k,
+    B_k, x_k, u_k read and K_k, k_k written; with the value expansions (mode 1, or
+    mode 0 when Vxx is requested) Vxx, Vx, V0 written at every step and the
+    terminal one; plus x_T and the terminal reads.  Mode 1 moves 3,336 B per step
+    at n = 12, m = 4 against ~1.2e4 FLOP: its bound is HBM, not fp64."""
+    want_v = (mode == 1) if want_v is None else want_v
+    step = n * n + n * m + n + m + m * n + m
+    if want_v:
+        step += n * n + n + 1
+    return 8 * (step * T + n + ((n * n + n + 1) if want_v else 0))
+
+
 # ---------------------------------------------------------------------------
 # CPU baseline: the oracle's NumPy restatement on the host cores (rank 0 only)
 # ---------------------------------------------------------------------------

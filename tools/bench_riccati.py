@@ -51,8 +51,9 @@ def main():
     Q = M @ M.T / n + 0.5 * torch.eye(n, device=dev, dtype=torch.float64)
     R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
     Qf = 10.0 * torch.eye(n, device=dev, dtype=torch.float64)
-    from bench import riccati_flops  # SURVEY.md 8(d) count, term by term
+    from bench import riccati_bytes, riccati_flops  # SURVEY.md 8(d) count, term by term
     flop = {md: riccati_flops(n, m, N, md) for md in (0, 1)}
+    byts = {md: riccati_bytes(n, m, N, md) for md in (0, 1)}
     libs = {"": _lib.load()}
     for p in filter(None, args.libs.split(",")):
         libs[p] = _lib.load(p)
@@ -91,6 +92,8 @@ def main():
                           "problems_per_s": Bn / (ms * 1e-3),
                           "tflops_est": flop[c[1]] * Bn / (ms * 1e-3) / 1e12,
                           "frac_fp64": flop[c[1]] * Bn / (ms * 1e-3) / 1e12 / 78.6,
+                          "hbm_tbs": byts[c[1]] * Bn / (ms * 1e-3) / 1e12,
+                          "frac_hbm": byts[c[1]] * Bn / (ms * 1e-3) / 1e12 / 8.0,
                           "nonzero_status": status[c]}), flush=True)
 
 
