@@ -29,6 +29,11 @@ using namespace hop::dyn;
 
 constexpr int TPB = 256;
 constexpr int TILE = 64;
+// A_k, B_k (and a_k, F(x_k, u_k)) are written once and read by the next stage
+// from HBM (629 MB at B = 4096, N = 100, far past the MALL): non-temporal
+// stores, 0.213 -> 0.158 ms (forward) and 0.239 -> 0.196 ms (central) for the
+// quadrotor at B = 4096, N = 100 (tools/ab_libs.py, same process, bitwise equal)
+#define HOP_LIN_STORE(v, p) __builtin_nontemporal_store((v), (p))
 
 template <int SYS, bool CEN>
 __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
@@ -94,8 +99,8 @@ __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
       const int ls = e / n, i = e - ls * n;
       const long long r = srow[ls];
       if (r < 0) continue;
-      if (a.a_res) a.a_res[r * n + i] = sf[e] - a.X[(sxrow[ls] + 1) * n + i];
-      if (a.Fx) a.Fx[r * n + i] = sf[e];
+      if (a.a_res) HOP_LIN_STORE(sf[e] - a.X[(sxrow[ls] + 1) * n + i], a.a_res + r * n + i);
+      if (a.Fx) HOP_LIN_STORE(sf[e], a.Fx + r * n + i);
     }
   }
   // phase 3: one (step, column) per thread
@@ -113,11 +118,11 @@ __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
     if (j < n) {
       double* Ak = a.A + r * (n * n) + j;
 #pragma unroll
-      for (int i = 0; i < n; ++i) Ak[i * n] = col[i];
+      for (int i = 0; i < n; ++i) HOP_LIN_STORE(col[i], Ak + i * n);
     } else {
       double* Bk = a.B + r * (n * m) + (j - n);
 #pragma unroll
-      for (int i = 0; i < n; ++i) Bk[i * m] = col[i];
+      for (int i = 0; i < n; ++i) HOP_LIN_STORE(col[i], Bk + i * m);
     }
   }
 }
