@@ -314,3 +314,33 @@ def test_dropin_input_shapes_like_the_reference(dev):
     short = solver.cost_timeopt_true(X[:T + 1], U[:T], xg, u_ref, Q, R, alpha, w, T)
     assert full == short
     del torch
+
+
+def test_ilqr_batch_nonfinite_initial_trajectories_crash_up_front(dev):
+    """Problems whose initial rollout is not finite on the rows the select reads raise
+    in the reference's first select (chol_inv's _assert_finite, utils.py:77): they
+    are reported crashed with nothing recorded, their J curve NaN and their select
+    status non-finite, and the other problems' runs are bitwise those of the batch
+    without them."""
+    import torch
+    from time_opt_ilqr_amd import solver, systems
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap_idx, _ = systems.make_quadrotor(N=40)
+    rng = np.random.default_rng(5)
+    Bn = 7
+    X0 = x0 + 0.2 * rng.standard_normal((Bn, 12))
+    X0[2, 9] = 2e3    # |omega| > 1e3: the quadrotor's guard makes X[1:] NaN
+    X0[5, 7] = np.nan
+    Qf = np.asarray(io.orc.terminal_weight(alpha, 12))
+    kw = dict(dt=F.dt, max_iter=4, wrap_idx=wrap_idx, use_central_diff=False)
+    res = solver.ilqr_timeopt_batch(2, X0, xg, u_ref, Q, R, Qf, w, 40, 8, 40, **kw)
+    keep = [0, 1, 3, 4, 6]
+    ref = solver.ilqr_timeopt_batch(2, X0[keep], xg, u_ref, Q, R, Qf, w, 40, 8, 40, **kw)
+    assert _np(res["crashed"]).tolist() == [0, 0, 1, 0, 0, 1, 0]
+    assert _np(res["n_hist"])[[2, 5]].tolist() == [0, 0]
+    assert bool(torch.isnan(res["J_curve"][[2, 5]]).all())
+    st0 = _np(res["select_status"][:, 0])
+    assert (st0[[2, 5]] & 4).all() and (st0[keep] == _np(ref["select_status"][:, 0])).all()
+    for f in ("n_hist", "T_hist", "J_hist", "T_star", "X", "U", "J_curve"):
+        a, b = res[f][keep], ref[f]
+        assert torch.equal(a.nan_to_num(7.0) if a.is_floating_point() else a,
+                           b.nan_to_num(7.0) if b.is_floating_point() else b), f

@@ -147,6 +147,16 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     bad = _lib.ST_FAIL | _lib.ST_NONFINITE
     # the last select's J curve of every problem (solver.py:751-762 returns it)
     J_curve = torch.full((Bn, T_max), float("nan"), dtype=f64, device=dev)
+    # A problem whose initial trajectory is not finite on the rows the select block
+    # reads (X[:T_max+1], U[:T_max]) raises in the reference's first select: its
+    # augmented blocks are NaN and chol_inv's _assert_finite (utils.py:77) refuses
+    # them.  Such problems are marked crashed here and never enter the batch, so
+    # they cannot cost the select block's rerun launch (one reference-association
+    # sweep of latency, 0.83 ms at N = 100, for a handful of problems).  The
+    # line search only ever accepts finite rollouts, so later trajectories stay
+    # finite and the check is needed once.
+    pre_bad = ~(torch.isfinite(X[:, :T_max + 1]).flatten(1).all(1)
+                & torch.isfinite(U[:, :T_max]).flatten(1).all(1))
 
     def iterate(s, warm):
         """one update (solver.py:541-553 when warm, else 578-752) of the problems in s"""
@@ -192,28 +202,40 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     # launch every iteration).  Needs the cost blocks shared by the batch.
     compact = all(t.dim() == d for t, d in ((xg_t, 1), (ur_t, 1), (Q_t, 2), (Qf_t, 2)))
     fields = ("X", "U", "lm", "T_bar", "J_hist", "T_hist", "n_hist", "done", "crashed")
-    stat, J_sel = iterate(st, True)
-    J_curve.copy_(J_sel)
-    status_log = [stat]
-    iters = 0
-    for _ in range(int(max_iter)):
+    pre = pre_bad.to(torch.int32)
+    st.crashed |= pre
+    st.done |= pre
+    pre_status = torch.where(pre_bad, bad, 0).to(torch.int32)
+
+    def step(warm):
+        """one iteration over the live problems; False when none is left"""
         live = st.done == 0
         n_live = int(live.sum().item())
         if n_live == 0:
-            break
+            return False
         if n_live == Bn or not compact:
-            stat, J_sel = iterate(st, False)
+            stat, J_sel = iterate(st, warm)
             J_curve[live] = J_sel[live]  # problems that had stopped ran no select
-            status_log.append(stat)
+            status_log.append(stat if warm is False or n_live == Bn
+                              else torch.where(live, stat, pre_status))
         else:
             idx = live.nonzero()[:, 0]
             sub = IlqrState(*[getattr(st, f).index_select(0, idx) for f in fields])
-            stat, J_sel = iterate(sub, False)
+            stat, J_sel = iterate(sub, warm)
             for f in fields:
                 getattr(st, f).index_copy_(0, idx, getattr(sub, f))
             J_curve.index_copy_(0, idx, J_sel)
-            status_log.append(torch.zeros((Bn,), dtype=stat.dtype, device=dev)
-                              .index_copy_(0, idx, stat))
+            status_log.append((pre_status if warm else torch.zeros_like(pre_status))
+                              .index_copy(0, idx, stat))
+        return True
+
+    status_log = []
+    if not step(True):
+        status_log.append(pre_status)
+    iters = 0
+    for _ in range(int(max_iter)):
+        if not step(False):
+            break
         iters += 1
     nh = st.n_hist
     last = (nh - 1).clamp(min=0).long()
