@@ -197,36 +197,54 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         return sel.status, sel.J
 
     # Problems that met the stop rule (or whose select raised) leave the batch: the
-    # remaining ones are gathered into a compact batch, so finished problems cost
-    # nothing (a crashed problem would otherwise force the select block's rerun
-    # launch every iteration).  Needs the cost blocks shared by the batch.
+    # remaining ones run as a compact batch, so finished problems cost nothing (a
+    # crashed problem would otherwise force the select block's rerun launch every
+    # iteration).  The compact state persists across iterations and is gathered
+    # again only when the live set shrinks (no per-iteration gather / scatter of
+    # the nine per-problem fields).  Needs the cost blocks shared by the batch.
     compact = all(t.dim() == d for t, d in ((xg_t, 1), (ur_t, 1), (Q_t, 2), (Qf_t, 2)))
     fields = ("X", "U", "lm", "T_bar", "J_hist", "T_hist", "n_hist", "done", "crashed")
     pre = pre_bad.to(torch.int32)
     st.crashed |= pre
     st.done |= pre
     pre_status = torch.where(pre_bad, bad, 0).to(torch.int32)
+    cur, idx = st, None  # idx: the rows of st that cur holds (None: cur is st)
+
+    def sync_back():
+        if idx is not None:
+            for f in fields:
+                getattr(st, f).index_copy_(0, idx, getattr(cur, f))
 
     def step(warm):
         """one iteration over the live problems; False when none is left"""
-        live = st.done == 0
+        nonlocal cur, idx
+        live = cur.done == 0
         n_live = int(live.sum().item())
         if n_live == 0:
             return False
-        if n_live == Bn or not compact:
+        base = pre_status if warm else torch.zeros_like(pre_status)
+        if not compact:  # per-problem cost blocks: the whole batch, stopped rows masked
             stat, J_sel = iterate(st, warm)
-            J_curve[live] = J_sel[live]  # problems that had stopped ran no select
-            status_log.append(stat if warm is False or n_live == Bn
-                              else torch.where(live, stat, pre_status))
+            full = live if n_live < Bn else None
+            if full is None:
+                J_curve.copy_(J_sel)
+                status_log.append(stat)
+            else:
+                J_curve[full] = J_sel[full]  # problems that had stopped ran no select
+                status_log.append(torch.where(full, stat, base))
+            return True
+        if n_live < live.numel():  # the live set shrank: gather it again
+            loc = live.nonzero()[:, 0]
+            sync_back()
+            cur = IlqrState(*[getattr(cur, f).index_select(0, loc) for f in fields])
+            idx = loc if idx is None else idx.index_select(0, loc)
+        stat, J_sel = iterate(cur, warm)
+        if idx is None:
+            J_curve.copy_(J_sel)
+            status_log.append(stat)
         else:
-            idx = live.nonzero()[:, 0]
-            sub = IlqrState(*[getattr(st, f).index_select(0, idx) for f in fields])
-            stat, J_sel = iterate(sub, warm)
-            for f in fields:
-                getattr(st, f).index_copy_(0, idx, getattr(sub, f))
             J_curve.index_copy_(0, idx, J_sel)
-            status_log.append((pre_status if warm else torch.zeros_like(pre_status))
-                              .index_copy(0, idx, stat))
+            status_log.append(base.index_copy(0, idx, stat))
         return True
 
     status_log = []
@@ -237,6 +255,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         if not step(False):
             break
         iters += 1
+    sync_back()
     nh = st.n_hist
     last = (nh - 1).clamp(min=0).long()
     T_out = torch.where(nh > 0, st.T_hist.gather(1, last[:, None])[:, 0], st.T_bar)
