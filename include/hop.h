@@ -425,6 +425,18 @@ int hop_ilqr_accept_f64(int64_t batch, int32_t warm, const double* J, const int3
                         int32_t* T_hist, int32_t* n_hist, int32_t hist_cap, int32_t* done,
                         void* stream);
 
+/*
+ * hop_ilqr_select_mask
+ * The per-iteration masks of the device outer loop (solver.py:514-525, 581-597):
+ * a problem whose select block raised (sel_status has ST_FAIL or ST_NONFINITE:
+ * the reference's FloatingPointError / LinAlgError out of propagator_all_Jt_aug)
+ * and is not done yet is marked crashed and done; active = the problem is not
+ * done and its truncated Riccati pass succeeded (ric_status has no ST_FAIL), the
+ * line search's mask.  One launch instead of a chain of elementwise ops.
+ */
+int hop_ilqr_select_mask(int64_t batch, const int32_t* sel_status, const int32_t* ric_status,
+                         int32_t* done, int32_t* crashed, int32_t* active, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

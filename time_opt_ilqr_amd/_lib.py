@@ -84,6 +84,7 @@ SIGNATURES = {
     "hop_obstacle_cost_f64": (C.c_int, [_P, _I64, _I64, _I32, _P, _I32, _P, _P, _P, _P]),
     "hop_ilqr_accept_f64": (C.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _P,
                                       _P]),
+    "hop_ilqr_select_mask": (C.c_int, [_I64, _P, _P, _P, _P, _P, _P]),
 }
 
 _lock = threading.Lock()

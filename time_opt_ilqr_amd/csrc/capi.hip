@@ -635,4 +635,14 @@ int hop_ilqr_accept_f64(int64_t batch, int32_t warm, const double* J, const int3
   return hip_status(hop::dispatch_accept(a, (hipStream_t)stream));
 }
 
+int hop_ilqr_select_mask(int64_t batch, const int32_t* sel_status, const int32_t* ric_status,
+                         int32_t* done, int32_t* crashed, int32_t* active, void* stream) {
+  if (batch < 0) return fail(HOP_E_ARG, "bad size");
+  if (batch == 0) return HOP_OK;
+  if (!sel_status || !ric_status || !done || !crashed || !active)
+    return fail(HOP_E_ARG, "null pointer");
+  hop::MaskArgs a{batch, sel_status, ric_status, done, crashed, active};
+  return hip_status(hop::dispatch_select_mask(a, (hipStream_t)stream));
+}
+
 }  // extern "C"

@@ -431,6 +431,19 @@ __global__ __launch_bounds__(256) void accept_kernel(AcceptArgs a) {
   }
 }
 
+// the outer loop's per-iteration masks (hop_ilqr_select_mask): crash marking from the
+// select block's status, then the line search's active mask from the Riccati status
+__global__ __launch_bounds__(256) void select_mask_kernel(MaskArgs a) {
+  const long long b = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (b >= a.batch) return;
+  int done = a.done[b];
+  if (!done && (a.sel_status[b] & (int)(ST_FAIL | ST_NONFINITE))) {
+    a.crashed[b] = 1;
+    a.done[b] = done = 1;
+  }
+  a.active[b] = !done && !(a.ric_status[b] & (int)ST_FAIL);
+}
+
 template <int SYS>
 hipError_t launch_all(int which, const void* args, hipStream_t st) {
   switch (which) {
@@ -486,6 +499,12 @@ hipError_t dispatch_forward(int sys, int which, const void* args, hipStream_t st
 hipError_t dispatch_obstacle(const ObstacleArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL(fwd::obstacle_kernel, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0,
                      stream, a);
+  return hipGetLastError();
+}
+
+hipError_t dispatch_select_mask(const MaskArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(fwd::select_mask_kernel, dim3((unsigned)((a.batch + 255) / 256)), dim3(256),
+                     0, stream, a);
   return hipGetLastError();
 }
 

@@ -183,6 +183,11 @@ struct AcceptArgs {
 hipError_t dispatch_forward(int sys, int which, const void* args, hipStream_t stream);
 hipError_t dispatch_obstacle(const ObstacleArgs& a, hipStream_t stream);
 hipError_t dispatch_accept(const AcceptArgs& a, hipStream_t stream);
+struct MaskArgs {
+  long long batch;
+  const int* sel_status; const int* ric_status; int* done; int* crashed; int* active;
+};
+hipError_t dispatch_select_mask(const MaskArgs& a, hipStream_t stream);
 hipError_t dispatch_linearize(const LinArgs& a, hipStream_t stream);
 hipError_t dispatch_dynamics(const DynArgs& a, hipStream_t stream);
 

@@ -827,3 +827,21 @@ def ilqr_accept(state, J, accepted, T_star, *, warm: bool = False):
         _lib.ptr(state.n_hist), state.J_hist.shape[1], _lib.ptr(state.done),
         _lib.stream_handle(dev))
     _lib.check(rc)
+
+
+def ilqr_select_mask(state, sel_status, ric_status):
+    """Crash marking after the select block and the line search's active mask
+    (solver.py:514-525, 581-597) in one launch: problems whose select raised
+    (ST_FAIL / ST_NONFINITE) and are not done become crashed and done; returns
+    active [B] int32 = not done and the Riccati pass succeeded."""
+    torch = _torch()
+    Bn = state.done.shape[0]
+    dev = state.done.device
+    sel = _dev(sel_status, "sel_status", torch.int32, dev)
+    ric = _dev(ric_status, "ric_status", torch.int32, dev)
+    active = torch.empty((Bn,), dtype=torch.int32, device=dev)
+    rc = _lib.load().hop_ilqr_select_mask(Bn, _lib.ptr(sel), _lib.ptr(ric), _lib.ptr(state.done),
+                                          _lib.ptr(state.crashed), _lib.ptr(active),
+                                          _lib.stream_handle(dev))
+    _lib.check(rc)
+    return active

@@ -171,10 +171,6 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, s.X, s.U, xg_t, ur_t, Q_t, R_inv,
                                     P, float(w), wrap_idx=wrap_idx, n_use=T_max, t_min=T_min,
                                     t_max=T_max, **ex)
-        # the reference raises out of ilqr_timeopt here (FloatingPointError / LinAlgError)
-        crash = ((sel.status & bad) != 0) & (s.done == 0)
-        s.crashed |= crash.to(torch.int32)
-        s.done |= crash.to(torch.int32)
         T_star = sel.t_star
         clock("select", t0)
         t0 = time.perf_counter()
@@ -185,7 +181,10 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
                                                             c_extra=ex["c_extra"])))
         clock("backward", t0)
         t0 = time.perf_counter()
-        active = ((ric.status & _lib.ST_FAIL) == 0) & (s.done == 0)
+        # the reference raises out of ilqr_timeopt at the select (FloatingPointError /
+        # LinAlgError): such problems become crashed and done; the line search runs
+        # the others whose Riccati pass succeeded (one launch for both masks)
+        active = engine.ilqr_select_mask(s, sel.status, ric.status)
         fw = engine.forward_linesearch(sid, s.X, s.U, T_star, ric.K, ric.k, cost, dt,
                                        alphas=alphas, active=active)
         engine.ilqr_accept(s, fw.J, fw.accepted, T_star, warm=warm)
