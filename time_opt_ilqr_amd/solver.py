@@ -103,7 +103,9 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
                          "(as_terminal_weight(alpha))")
     P = 0.5 * (Qf_t + Qf_t.transpose(-1, -2))  # _sym on the device
     obs = None if obstacles is None or len(obstacles) == 0 else tt(obstacles)
-    cost = engine.CostParams(xg_t, ur_t, Q_t, R_t, Qf_t, float(w), obs, wrap_idx)
+    # w as a device scalar made once (a Python float would cost a fill launch per call)
+    w_t = torch.full((1,), float(w), dtype=f64, device=dev)
+    cost = engine.CostParams(xg_t, ur_t, Q_t, R_t, Qf_t, w_t, obs, wrap_idx)
     if U_init is None:
         U = ur_t.reshape(-1, m).expand(Bn, m)[:, None, :].expand(Bn, N, m).contiguous()
     else:
@@ -169,7 +171,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
             c, cx, cxx = engine.obstacle_cost(s.X[:, :N], obs)
             ex = dict(qxx_extra=cxx, qx_extra=cx, c_extra=c)
         sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, s.X, s.U, xg_t, ur_t, Q_t, R_inv,
-                                    P, float(w), wrap_idx=wrap_idx, n_use=T_max, t_min=T_min,
+                                    P, w_t, wrap_idx=wrap_idx, n_use=T_max, t_min=T_min,
                                     t_max=T_max, **ex)
         T_star = sel.t_star
         clock("select", t0)
