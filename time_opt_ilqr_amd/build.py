@@ -17,14 +17,14 @@ REPO = os.path.dirname(HERE)
 LIB = os.path.join(HERE, "libhop_amd.so")
 SOURCES = ["capi.hip", "augment.hip", "lft_sweep.hip", "lft_sweep_v2.hip", "lft_small.hip",
            "riccati.hip", "riccati_fast.hip", "linearize.hip", "forward.hip"]
-# developer builds (HOP_DEV_BUILD=1 or --dev): the A/B schedules, stamped
-# instantiations and the s <= 5 build without SLP vectorisation, selected at run
-# time by hop_set_options' variant number; product builds compile none of them
+# developer builds (HOP_DEV_BUILD=1 or --dev): the A/B schedules and stamped
+# instantiations, selected at run time by hop_set_options' variant number;
+# product builds compile none of them
 DEV = os.environ.get("HOP_DEV_BUILD", "0") not in ("", "0") or "--dev" in sys.argv
-DEV_SOURCES = ["lft_small_noslp.hip"]
+DEV_SOURCES = []
 if DEV:  # a separate library (load it with HOP_LIB=<path>): the product .so stays product
     LIB = os.path.join(HERE, "libhop_amd_dev.so")
-EXTRA = {"lft_small_noslp.hip": ["-fno-slp-vectorize"]}
+EXTRA = {}
 HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp", "wrap.hpp", "dynamics.hpp"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",

@@ -110,13 +110,7 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
       const hipError_t e = hop::dispatch_lft_v2_f32(a, (hipStream_t)stream);
       if (e != hipErrorNotSupported) return hip_status(e);
     }
-    hipError_t e;
-#ifdef HOP_DEV
-    if (hop::g_opt_variant == 71)  // A/B: the s <= 5 build without SLP vectorisation
-      e = hop::dispatch_lft_small_noslp<T>(a, (hipStream_t)stream);
-    else
-#endif
-      e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
+    const hipError_t e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);  // s <= 5
     if (e != hipErrorNotSupported) return hip_status(e);
   }
   return hip_status(hop::dispatch_lft<T>(a, (hipStream_t)stream));

@@ -198,8 +198,6 @@ hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream);
 template <class T>
-hipError_t dispatch_lft_small_noslp(const LftArgs<T>& a, hipStream_t stream);
-template <class T>
 hipError_t dispatch_augment(const AugArgs<T>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream);

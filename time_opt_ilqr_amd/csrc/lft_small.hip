@@ -15,13 +15,6 @@
 #include "hop_device.hpp"
 #include "hop_kernels.hpp"
 
-// lft_small_noslp.hip re-compiles this file under another namespace with
-// -fno-slp-vectorize (developer builds: same-process A/B, variant 71)
-#ifndef HOP_SMALL_NS
-#define HOP_SMALL_NS small
-#define HOP_SMALL_DISPATCH dispatch_lft_small
-#endif
-#define small HOP_SMALL_NS
 
 namespace hop {
 namespace small {
@@ -565,7 +558,7 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
 
 // small-s path: returns hipErrorNotSupported when the shape has no instantiation
 template <class T>
-hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
+hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0) return hipErrorNotSupported;
   if (a.traj && (a.tr.n != a.s - 1 || a.tr.m != a.m || !a.r_is_inv)) return hipErrorNotSupported;
   // Batch-major blocks stream as problem-major pieces (LY 1); tile64 blocks (LY 2)
@@ -676,7 +669,7 @@ hipError_t HOP_SMALL_DISPATCH(const LftArgs<T>& a, hipStream_t stream) {
   return hipErrorNotSupported;
 }
 
-template hipError_t HOP_SMALL_DISPATCH<float>(const LftArgs<float>&, hipStream_t);
-template hipError_t HOP_SMALL_DISPATCH<double>(const LftArgs<double>&, hipStream_t);
+template hipError_t dispatch_lft_small<float>(const LftArgs<float>&, hipStream_t);
+template hipError_t dispatch_lft_small<double>(const LftArgs<double>&, hipStream_t);
 
 }  // namespace hop
