@@ -202,7 +202,9 @@ int traj_check(const hop::TrajArgs<T>& t, int64_t batch, int32_t n_alloc, int32_
   if (t.n < 1 || t.n + 1 > HOP_MAX_DIM) return fail(HOP_E_SIZE, "n must be in [1, 15]");
   if (t.m < 1 || t.m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
   if (n_build > n_alloc) return fail(HOP_E_ARG, "n_use > n_alloc (reference IndexError)");
-  if (!t.A || !t.Bm || !t.ares || !t.X || !t.U || !t.xg || !t.u_ref || !t.Q || !t.P || !t.w)
+  // an empty batch (an empty shard) passes NULL data pointers: nothing is read
+  if (batch > 0 && (!t.A || !t.Bm || !t.ares || !t.X || !t.U || !t.xg || !t.u_ref || !t.Q ||
+                    !t.P || !t.w))
     return fail(HOP_E_ARG, "null input pointer");
   if (t.xg_bs < 0 || t.ur_bs < 0 || t.q_bs < 0 || t.p_bs < 0 || t.w_bs < 0)
     return fail(HOP_E_ARG, "negative stride");
