@@ -559,3 +559,38 @@ def test_nonfinite_inputs_status_and_curve_match_oracle(dev, s, m):
         assert np.array_equal(np.isnan(J[b]), nan), (b, J[b], o["J"])
         if b != 4 and not nan.all():  # b=4: the escalated block amplifies rounding
             assert _elem_rel(J[b][~nan], o["J"][~nan]) <= 1e-9, b
+
+
+def test_random_shapes_every_path_vs_oracle(dev):
+    """Seeded random shapes (s 2..16, m 1..min(s, 6), N 1..24, B 1..9, fp64/fp32,
+    batch-major and tile64 where the small-s path takes them, random t_min/t_max):
+    J against the oracle (fp64 1e-9 elementwise, fp32 2e-3), T* equal in fp64, and
+    the status word equal on these well-conditioned inputs."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    rng = np.random.default_rng(20261016)
+    for case in range(14):
+        s = int(rng.integers(2, 17))
+        m = int(rng.integers(1, min(s, 6) + 1))
+        N = int(rng.integers(1, 25))
+        Bn = int(rng.integers(1, 10))
+        f32 = bool(rng.integers(0, 2)) and s <= 13
+        t_min = int(rng.integers(1, N + 1))
+        t_max = int(rng.integers(t_min, N + 1))
+        A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(500 + 37 * case, Bn, s, m, N)
+        dt = torch.float32 if f32 else torch.float64
+        args = [_t(x, dev, dt) for x in (A, Bm, Q, Ri, z0[0], QT)]
+        r = engine.propagate(*args, t_min=t_min, t_max=t_max)
+        Jo, st = orc.lft_sweep_batch(A, Bm, Q, Ri, z0[0], QT)
+        tag = (case, s, m, N, Bn, "f32" if f32 else "f64", t_min, t_max)
+        J = r.J.double().cpu().numpy()
+        assert _elem_rel(J, Jo) <= (2e-3 if f32 else 1e-9), tag
+        Ts, _ = orc.select_horizon(Jo, t_min, t_max)
+        if not f32:
+            assert r.t_star.cpu().numpy().tolist() == Ts.tolist(), tag
+            assert r.status.cpu().numpy().tolist() == st.tolist(), tag
+        tiled = {(2, 1), (3, 1), (4, 1), (4, 2)} | ({(5, 1), (5, 2)} if f32 else set())
+        if (s, m) in tiled:  # the same problems on tile64 blocks (small-s instantiations)
+            tl = engine.propagate(*(engine.to_tile64(x) for x in args[:3]), args[3], args[4],
+                                  engine.to_tile64(args[5]), t_min=t_min, t_max=t_max)
+            assert _elem_rel(tl.J.double().cpu().numpy(), Jo) <= (2e-3 if f32 else 1e-9), tag
