@@ -553,7 +553,8 @@ def test_nonfinite_inputs_status_and_curve_match_oracle(dev, s, m):
     st = res.status.cpu().numpy()
     J = res.J.cpu().numpy()
     for b in range(Bn):
-        o = orc.lft_sweep(A[b], Bm[b], Q[b], Ri[b], z0[b], QT[b])
+        with np.errstate(invalid="ignore", over="ignore"):  # NaN / inf blocks by design
+            o = orc.lft_sweep(A[b], Bm[b], Q[b], Ri[b], z0[b], QT[b])
         assert int(st[b]) == int(o["status"]), (b, int(st[b]), int(o["status"]))
         nan = np.isnan(o["J"])
         assert np.array_equal(np.isnan(J[b]), nan), (b, J[b], o["J"])
