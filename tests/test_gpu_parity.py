@@ -328,7 +328,8 @@ def test_real_DI_dropins(dev, golden_dir):
     assert _rel(bf, d["bf_J"]) <= RTOL64
 
 
-@pytest.mark.parametrize("schedule", ["2", "8", "10", "12", "14", "30", "40"])
+@pytest.mark.parametrize("schedule", [pytest.param(v, marks=pytest.mark.devbuild)
+                                      for v in ("2", "8", "10", "12", "14")] + ["30", "40"])
 def test_lft_fast_path_matches_generic_kernel(dev, schedule):
     """Every schedule of the exact-size fp64 kernel (LDS-DMA streamed, s=13/m=4)
     and the generic kernel agree, including the jitter / LU retry paths and batch
@@ -441,6 +442,7 @@ def test_cond_forced_handover_is_the_lft_kernel(dev):
     assert int(r.status[4]) & orc.ST_LU
 
 
+@pytest.mark.devbuild
 @pytest.mark.parametrize("s,m,dt", [(5, 1, "f32"), (3, 1, "f64"), (4, 2, "f64")])
 def test_small_cond_kernel(dev, s, m, dt):
     """Small-s COND kernels (developer builds, opt-in): alone (variant 62) no

@@ -60,7 +60,7 @@ def _oracle(p, rho, n_use=None, extra=None):
     return (Aa, Ba, Qa, Ri, z0, QT), orc.lft_sweep(Aa, Ba, Qa, Ri, z0, QT, n_use)
 
 
-@pytest.fixture(params=["40", "53"])
+@pytest.fixture(params=[pytest.param("40", marks=pytest.mark.devbuild), "53"])
 def traj_variant(request):
     """Fused s=13 trajectory kernels: 53 (default) closed-form stage inverses, 40 stage
     inverses by Gauss-Jordan sweeps on the built images (both + the rerun launch;
