@@ -32,15 +32,19 @@ def _worker(rank, world, port, total, out_dir):
             if hi > lo else [np.zeros((0,))] * 7
         ts = torch.zeros(hi - lo, dtype=torch.int32)
         js = torch.zeros(hi - lo, dtype=torch.float64)
+        Jc = torch.zeros((hi - lo, 12), dtype=torch.float64)
         for i in range(hi - lo):
             # problem index lo+i uses seed 100+lo+i in both paths
             A1, B1, Q1, R1, Ri1, z1, QT1 = orc.synth_lft_problem(100 + lo + i, 4, 1, 12)
             o = orc.lft_sweep(A1, B1, Q1, Ri1, z1, QT1)
             t, j = orc.select_horizon(o["J"], 3, 12)
             ts[i], js[i] = int(t), float(j)
+            Jc[i] = torch.as_tensor(o["J"])
         T, J = hd.gather_selection(ts, js, total)
+        curves = hd.gather_curves(Jc, total)
         if rank == 0:
-            np.savez(os.path.join(out_dir, "gathered.npz"), T=T.numpy(), J=J.numpy())
+            np.savez(os.path.join(out_dir, "gathered.npz"), T=T.numpy(), J=J.numpy(),
+                     curves=curves.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -52,12 +56,14 @@ def test_gloo_shards_and_gather(tmp_path, world, total):
     mp.spawn(_worker, args=(world, _free_port(), total, str(tmp_path)), nprocs=world, join=True)
     got = np.load(tmp_path / "gathered.npz")
     from oracle import hop_oracle as orc
-    T_ref, J_ref = [], []
+    T_ref, J_ref, C_ref = [], [], []
     for b in range(total):
         A1, B1, Q1, R1, Ri1, z1, QT1 = orc.synth_lft_problem(100 + b, 4, 1, 12)
         o = orc.lft_sweep(A1, B1, Q1, Ri1, z1, QT1)
         t, j = orc.select_horizon(o["J"], 3, 12)
         T_ref.append(int(t))
         J_ref.append(float(j))
+        C_ref.append(o["J"])
     assert got["T"].tolist() == T_ref
     assert np.array_equal(got["J"], np.array(J_ref))
+    assert np.array_equal(got["curves"], np.array(C_ref).reshape(total, 12))

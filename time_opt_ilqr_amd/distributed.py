@@ -49,3 +49,23 @@ def gather_selection(t_star, j_star, total: int, group=None):
     parts = [out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)]
     full = torch.cat(parts, 0)
     return full[:, 0].to(torch.int32), full[:, 1].to(j_star.dtype)
+
+
+def gather_curves(J, total: int, group=None):
+    """All-gather every rank's J curves [shard, N] into [total, N] (the optional
+    full-curve collection of SURVEY.md 2: the reference's driver plots and writes
+    the last J curve, ilqr_propagator.py:825/860).  N * 8 bytes per problem, so
+    callers gather curves only when they need them; the bench gathers (T*, J*)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if world == 1:
+        return J
+    N = J.shape[1] if J.dim() == 2 else 0
+    sizes = [shard_bounds(total, r, world) for r in range(world)]
+    cap = max(hi - lo for lo, hi in sizes)
+    packed = torch.full((cap, N), float("nan"), dtype=J.dtype, device=J.device)
+    packed[: J.shape[0]] = J
+    out = torch.empty((world * cap, N), dtype=J.dtype, device=J.device)
+    dist.all_gather_into_tensor(out, packed, group=group)
+    return torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
