@@ -293,6 +293,39 @@ int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float
                     float* Vxx, float* Vx, float* V0, int32_t* status, void* stream);
 
 /*
+ * hop_bruteforce_jcurve_f64 / _f32
+ * replaces bruteforce_all_Jt_backward_expansion(A_list, B_list, X, U, xg, u_ref, Q,
+ *          R, alpha, w, T_max, lm_lambda, wrap_idx, extra_stage_cost)
+ *          /root/reference/solver.py:293-358 (the select step of
+ *          ilqr_timeopt(method="bruteforce"), solver.py:525-532 / 607-614)
+ *   J[b][T-1] = V_0 of the length-T value-expansion sweep (mode 1 arithmetic with
+ *   the fixed lm_lambda and chol_solve's jitter ladder) for T = 1..t_max: all
+ *   t_max sweeps of every problem in ONE launch (grid y = T).  Inputs as
+ *   hop_riccati_*; t_max <= n_alloc.
+ *   Outputs: J [batch][t_max]; status [batch][t_max] per horizon (HOP_ST_FAIL /
+ *   HOP_ST_NONFINITE where the reference raises LinAlgError / FloatingPointError;
+ *   J is NaN there).
+ */
+int hop_bruteforce_jcurve_f64(const double* A, const double* Bm, const double* X,
+                              const double* U, const double* xg, int64_t xg_batch_stride,
+                              const double* u_ref, int64_t u_ref_batch_stride, const double* Q,
+                              int64_t q_batch_stride, const double* R, int64_t r_batch_stride,
+                              const double* Qf, int64_t qf_batch_stride, const double* qxx_extra,
+                              const double* qx_extra, const double* c_extra, double lm_lambda,
+                              double w_stage, uint32_t wrap_mask, int64_t batch, int32_t n_alloc,
+                              int32_t n, int32_t m, int32_t t_max, double* J, int32_t* status,
+                              void* stream);
+int hop_bruteforce_jcurve_f32(const float* A, const float* Bm, const float* X, const float* U,
+                              const float* xg, int64_t xg_batch_stride, const float* u_ref,
+                              int64_t u_ref_batch_stride, const float* Q, int64_t q_batch_stride,
+                              const float* R, int64_t r_batch_stride, const float* Qf,
+                              int64_t qf_batch_stride, const float* qxx_extra,
+                              const float* qx_extra, const float* c_extra, float lm_lambda,
+                              float w_stage, uint32_t wrap_mask, int64_t batch, int32_t n_alloc,
+                              int32_t n, int32_t m, int32_t t_max, float* J, int32_t* status,
+                              void* stream);
+
+/*
  * Batched dynamics and finite-difference linearisation.
  * System ids (the reference's systems.py makers, F discretised with the given dt):
  *   0 double integrator  make_double_integrator     systems.py:28-50    n=2,  m=1

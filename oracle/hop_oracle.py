@@ -425,13 +425,13 @@ def riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
 
 
 def bruteforce_J(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, w, T_max,
-                 lm_lambda=1e-6, wrap_idx=None):
+                 lm_lambda=1e-6, wrap_idx=None, extra=None):
     """solver.py:293-358: J[T-1] = V0 of a fresh Riccati sweep of length T."""
     J = np.zeros(int(T_max))
     for T in range(1, int(T_max) + 1):
         _, _, V0, _, _ = riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R,
                                          alpha, T, 0, lm_lambda=lm_lambda,
-                                         w_stage=w, wrap_idx=wrap_idx,
+                                         w_stage=w, wrap_idx=wrap_idx, extra=extra,
                                          reg_max_tries=1)
         J[T - 1] = V0[0]
     return J

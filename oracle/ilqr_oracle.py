@@ -122,11 +122,13 @@ def forward_linesearch(sys_id, dt, X, U, xg, u_ref, Q, R, Qf, w, T_star, k_list,
 
 def ilqr_timeopt(sys_id, dt, x0, xg, u_ref, Q, R, Qf, w, N, T_min, T_max, max_iter=15,
                  lm_init=1e-3, wrap_idx=None, central=True, obstacles=None,
-                 alphas=ALPHAS, U_init=None):
+                 alphas=ALPHAS, U_init=None, method="propagator"):
     """solver.py:449-765, method="propagator" (augmentation with the default
-    q_reg 1e-9 / rho_reg 1e-12, the propagator J curve at T_use = T_max).
+    q_reg 1e-9 / rho_reg 1e-12, the propagator J curve at T_use = T_max) or
+    method="bruteforce" (the J curve of solver.py:293-358 at lm_lambda = 1e-6).
     U_init as solver.py:480-490 (1-D = one control per step, padded with its
     last row, truncated to N)."""
+    assert method in ("propagator", "bruteforce")
     extra = _extra_fn(obstacles)
     if U_init is None:
         U = np.tile(np.asarray(u_ref, dtype=float).reshape(1, -1), (N, 1))
@@ -147,6 +149,10 @@ def ilqr_timeopt(sys_id, dt, x0, xg, u_ref, Q, R, Qf, w, N, T_min, T_max, max_it
 
     def select(X, U):
         A, B, a_res = dyn.linearize(sys_id, X, U, dt, central=central)
+        if method == "bruteforce":
+            J = orc.bruteforce_J(list(A), list(B), X, U, xg, u_ref, Q, R, alpha, w, T_max,
+                                 wrap_idx=wrap_idx, extra=extra)
+            return A, B, int(np.argmin(J[T_min - 1:T_max]) + T_min)
         Aa, Ba, Qa, _, z0, R_inv = orc.augment_stage(A, B, a_res, X, U, xg, u_ref, Q, R, w,
                                                      wrap_idx=wrap_idx, extra=extra)
         QT = orc.augment_terminal(X, xg, alpha, wrap_idx)

@@ -410,6 +410,41 @@ def ilqr_capture(tag, maker, maker_kwargs, T_min, T_max, max_iter, central, keep
           f"fwd captured={len(calls)}")
 
 
+ILQR_BF_CASES = [  # (tag, maker, maker kwargs, T_min, T_max, max_iter, central)
+    ("di", "make_double_integrator", dict(N=50), 10, 50, 8, False),
+    ("cartpole", "make_cartpole_swingup", dict(N=80), 20, 70, 3, False),
+    ("segway", "make_segway_balance", dict(N=60), 10, 60, 3, False),
+    ("quadrotor", "make_quadrotor", dict(N=60), 20, 55, 3, False),
+    ("pointmass", "make_pointmass_navigation", dict(N=60), 20, 55, 3, True),
+]
+
+
+def ilqr_bruteforce_capture(tag, maker, maker_kwargs, T_min, T_max, max_iter, central):
+    """ilqr_timeopt(method="bruteforce") end to end (solver.py:449-765 with the
+    brute-force J curve of solver.py:293-358 as the select step)."""
+    F, x0, xg, u_ref, Q, R, alpha, w, N, _, _, wrap_idx, extra = \
+        getattr(ref_systems, maker)(**maker_kwargs)
+    esc = extra["extra_stage_cost"] if extra else None
+    sol = ref_solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max,
+                                  method="bruteforce", max_iter=max_iter, wrap_idx=wrap_idx,
+                                  use_central_diff=central, extra_stage_cost=esc)
+    d = dict(N=N, T_min=T_min, T_max=T_max, max_iter=max_iter, central=int(central),
+             dt=float(F.dt), x0=x0, xg=xg, u_ref=u_ref, Q=Q, R=R,
+             Qf=ref_utils.as_terminal_weight(alpha, len(x0)), w=w,
+             wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64),
+             X=sol["X"], U=sol["U"], J_hist=np.array(sol["J_hist"]),
+             T_hist=np.array(sol["T_hist"]), T_star=int(sol["T_star"]),
+             J_curve=np.array(sol["J_curve"]))
+    np.savez_compressed(os.path.join(HERE, f"ilqr_bf_{tag}.npz"), **d)
+    print(f"ilqr_bf_{tag}: T*={sol['T_star']} J_hist={sol['J_hist']} T_hist={sol['T_hist']}")
+
+
+def main_ilqr_bruteforce():
+    np.seterr(all="ignore")
+    for case in ILQR_BF_CASES:
+        ilqr_bruteforce_capture(*case)
+
+
 def main_ilqr():
     np.seterr(all="ignore")
     for case in ILQR_CASES:
@@ -625,6 +660,8 @@ if __name__ == "__main__":
         main_traj()
     elif "--lin" in sys.argv:  # only the dynamics / linearisation fixtures
         main_lin()
+    elif "--ilqr-bf" in sys.argv:  # ilqr_timeopt(method="bruteforce") end to end
+        main_ilqr_bruteforce()
     elif "--ilqr" in sys.argv:  # only the forward line search / outer loop fixtures
         main_ilqr()
     else:

@@ -30,7 +30,7 @@ def _header_functions():
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 30
+    assert len(names) == 32
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:
@@ -100,6 +100,14 @@ def test_argument_validation_without_gpu(lib):
     rc = lib.hop_riccati_f64(*([nul] * 4), nul, 0, nul, 0, nul, 0, nul, 0, nul, 0, nul, nul, nul,
                              nul, nul, 0.0, 0, 2, 12, 4, 10, 12, 4, *([nul] * 6), nul)
     assert rc == -1 and b"mode" in lib.hop_last_error()
+    # the brute-force J curve: t_max > n_alloc is the reference's IndexError
+    jc = lambda t_max, n_alloc, wrap=0: lib.hop_bruteforce_jcurve_f64(  # noqa: E731
+        *([nul] * 4), nul, 0, nul, 0, nul, 0, nul, 0, nul, 0, nul, nul, nul, 1e-6, 0.0, wrap,
+        3, n_alloc, 12, 4, t_max, nul, nul, nul)
+    assert jc(11, 10) == -1 and b"t_max > n_alloc" in lib.hop_last_error()
+    assert jc(0, 10) == -1 and b"t_max < 1" in lib.hop_last_error()
+    assert jc(10, 10, 1 << 12) == -1 and b"wrap_mask" in lib.hop_last_error()
+    assert jc(10, 10) == -1 and b"null pointer" in lib.hop_last_error()
 
 
 def test_product_path_has_no_cpu_fallback():

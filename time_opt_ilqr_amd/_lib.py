@@ -37,6 +37,9 @@ _RIC64 = [_P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, 
           C.c_double, _U32, _I32, _I32, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P]
 _RIC32 = list(_RIC64)
 _RIC32[19] = C.c_float
+# J-curve form: the 17 Riccati inputs, lm w wrap batch n_alloc n m t_max J status stream
+_JC64 = _RIC64[:17] + [C.c_double, C.c_double, _U32, _I64, _I32, _I32, _I32, _I32, _P, _P, _P]
+_JC32 = _RIC64[:17] + [C.c_float, C.c_float, _U32, _I64, _I32, _I32, _I32, _I32, _P, _P, _P]
 # trajectory-form inputs shared by hop_augment_* and hop_lft_sweep_traj_*:
 # A Bm a_res X U xg xg_bs u_ref ur_bs Q q_bs P p_bs w w_bs qxx qx c wrap q_reg rho_reg
 _TRJ64 = [_P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _U32,
@@ -69,6 +72,8 @@ SIGNATURES = {
     "hop_lft_sweep_traj_f32": (C.c_int, _TRJ32 + _TRAJ_TAIL),
     "hop_riccati_f64": (C.c_int, _RIC64),
     "hop_riccati_f32": (C.c_int, _RIC32),
+    "hop_bruteforce_jcurve_f64": (C.c_int, _JC64),
+    "hop_bruteforce_jcurve_f32": (C.c_int, _JC32),
     "hop_system_dims": (C.c_int, [_I32, _P, _P]),
     "hop_linearize_f64": (C.c_int, [_I32, C.c_double, _P, _P, _I64, _I32, _I32, _I32,
                                     C.c_double, C.c_double, C.c_double, C.c_double, _P, _P, _P,
@@ -105,6 +110,11 @@ def load(path: str | None = None):
         if not os.path.exists(p):
             raise HopError(f"{p} not built: run `python -m time_opt_ilqr_amd.build` "
                            "(the HIP engine has no CPU fallback)")
+        # torch's HIP runtime must be the process's one: the library resolves
+        # libamdhip64.so.7 against what is already loaded, and loaded first it would
+        # pull in /opt/rocm's copy beside torch's bundled one -- two runtimes, and
+        # the library's launches then see no device (measured: HIP error 100)
+        import torch  # noqa: F401
         lib = C.CDLL(p)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

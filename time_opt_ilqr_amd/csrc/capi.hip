@@ -195,6 +195,39 @@ int riccati_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, 
   return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
 }
 
+// J-curve form: V_0 of the length-T sweep for every T in 1..t_max in one launch
+template <class T>
+int jcurve_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, int64_t xg_bs,
+                 const T* u_ref, int64_t ur_bs, const T* Q, int64_t q_bs, const T* R,
+                 int64_t r_bs, const T* Qf, int64_t qf_bs, const T* qxx_extra,
+                 const T* qx_extra, const T* c_extra, T lm_lambda, T w_stage, uint32_t wrap_mask,
+                 int64_t batch, int32_t n_alloc, int32_t n, int32_t m, int32_t t_max, T* J,
+                 int32_t* status, void* stream) {
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (n < 1 || n > HOP_MAX_DIM) return fail(HOP_E_SIZE, "n must be in [1, 16]");
+  if (m < 1 || m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
+  if (t_max < 1) return fail(HOP_E_ARG, "t_max < 1");
+  // the reference slices A_list[:T] for T <= T_max (an IndexError past N)
+  if (t_max > n_alloc) return fail(HOP_E_ARG, "t_max > n_alloc (reference IndexError)");
+  if (t_max > 65535) return fail(HOP_E_SIZE, "t_max > 65535");
+  if ((wrap_mask >> n) != 0u) return fail(HOP_E_ARG, "wrap_mask names a state >= n");
+  if (batch == 0) return HOP_OK;
+  if (!A || !Bm || !X || !U || !xg || !u_ref || !Q || !R || !Qf || !J || !status)
+    return fail(HOP_E_ARG, "null pointer");
+  hop::RiccatiArgs<T> a;
+  a.A = A; a.Bm = Bm; a.X = X; a.U = U; a.xg = xg; a.u_ref = u_ref; a.Q = Q; a.R = R; a.Qf = Qf;
+  a.qxx_extra = qxx_extra; a.qx_extra = qx_extra; a.c_extra = c_extra;
+  a.horizon = nullptr; a.lm = nullptr;
+  a.xg_bstride = xg_bs; a.uref_bstride = ur_bs; a.q_bstride = q_bs; a.r_bstride = r_bs;
+  a.qf_bstride = qf_bs;
+  a.batch = batch; a.nalloc = n_alloc; a.n = n; a.m = m; a.mode = 1;
+  a.reg_max_tries = 1; a.max_tries = 8; a.wrap_mask = wrap_mask; a.w_stage = w_stage;
+  a.K = nullptr; a.k = nullptr; a.Vxx = nullptr; a.Vx = nullptr; a.V0 = nullptr;
+  a.status = nullptr;
+  a.jc_J = J; a.jc_status = status; a.jc_tmax = t_max; a.lm_value = lm_lambda;
+  return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
+}
+
 // ---- trajectory form (augmented.py:10-87 on the device) -------------------
 template <class T>
 int traj_check(const hop::TrajArgs<T>& t, int64_t batch, int32_t n_alloc, int32_t n_build) {
@@ -406,6 +439,32 @@ int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float
                               qxx_extra, qx_extra, c_extra, horizon, lm, w_stage, wrap_mask,
                               mode, reg_max_tries, batch, n_alloc, n, m, K, k, Vxx, Vx, V0,
                               status, stream);
+}
+
+int hop_bruteforce_jcurve_f64(const double* A, const double* Bm, const double* X,
+                              const double* U, const double* xg, int64_t xg_bs,
+                              const double* u_ref, int64_t ur_bs, const double* Q, int64_t q_bs,
+                              const double* R, int64_t r_bs, const double* Qf, int64_t qf_bs,
+                              const double* qxx_extra, const double* qx_extra,
+                              const double* c_extra, double lm_lambda, double w_stage,
+                              uint32_t wrap_mask, int64_t batch, int32_t n_alloc, int32_t n,
+                              int32_t m, int32_t t_max, double* J, int32_t* status,
+                              void* stream) {
+  return jcurve_entry<double>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
+                              qxx_extra, qx_extra, c_extra, lm_lambda, w_stage, wrap_mask, batch,
+                              n_alloc, n, m, t_max, J, status, stream);
+}
+int hop_bruteforce_jcurve_f32(const float* A, const float* Bm, const float* X, const float* U,
+                              const float* xg, int64_t xg_bs, const float* u_ref, int64_t ur_bs,
+                              const float* Q, int64_t q_bs, const float* R, int64_t r_bs,
+                              const float* Qf, int64_t qf_bs, const float* qxx_extra,
+                              const float* qx_extra, const float* c_extra, float lm_lambda,
+                              float w_stage, uint32_t wrap_mask, int64_t batch, int32_t n_alloc,
+                              int32_t n, int32_t m, int32_t t_max, float* J, int32_t* status,
+                              void* stream) {
+  return jcurve_entry<float>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
+                             qxx_extra, qx_extra, c_extra, lm_lambda, w_stage, wrap_mask, batch,
+                             n_alloc, n, m, t_max, J, status, stream);
 }
 
 int hop_augment_f64(const double* A, const double* Bm, const double* a_res, const double* X,

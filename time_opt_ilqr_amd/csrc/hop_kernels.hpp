@@ -105,6 +105,14 @@ struct RiccatiArgs {
   T* Vx;   // [B][nalloc+1][n] or null
   T* V0;   // [B][nalloc+1] or null
   int* status;  // [B]
+  // J-curve form (hop_bruteforce_jcurve_*, solver.py:293-358): when jc_J is set the
+  // grid's y index is the horizon (L = blockIdx.y + 1, the same for a whole wave),
+  // lm is the scalar lm_value, no K / k / V is stored and each (problem, horizon)
+  // writes J[b][L-1] = V_0 and its status to jc_status[b][L-1]
+  T* jc_J = nullptr;          // [B][jc_tmax]
+  int* jc_status = nullptr;   // [B][jc_tmax]
+  int jc_tmax = 0;
+  T lm_value = T(0);
 };
 
 // batched finite-difference linearisation (linearize.hip, dynamics.hpp)

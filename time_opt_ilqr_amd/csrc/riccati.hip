@@ -75,12 +75,13 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   const T* Qp = a.Q + pb * a.q_bstride;
   const T* Rp = a.R + pb * a.r_bstride;
   const T* Qfp = a.Qf + pb * a.qf_bstride;
-  const int L = valid ? a.horizon[pb] : 0;
+  const bool JC = a.jc_J != nullptr;  // J-curve form: the grid's y index is the horizon
+  const int L = valid ? (JC ? (int)blockIdx.y + 1 : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
   Lw = __builtin_amdgcn_readfirstlane(Lw);
-  const T lam0 = a.lm[pb];
+  const T lam0 = JC ? a.lm_value : a.lm[pb];
   unsigned long long sec[10] = {};
   unsigned long long tprev = 0;
   auto stamp = [&](int j) {
@@ -331,11 +332,13 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       for (int r = 0; r < S; ++r) Vxx[r] = Vn[r];
       vx = vxn;
       v0 = v0n;
-      T* Ko = a.K + (pb * NA + i) * (long long)m * n;
+      if (!JC) {
+        T* Ko = a.K + (pb * NA + i) * (long long)m * n;
 #pragma unroll
-      for (int r = 0; r < MM; ++r)
-        if (r < m && c < n) Ko[r * n + c] = K[r];
-      if (c < m) a.k[(pb * NA + i) * m + c] = kv;
+        for (int r = 0; r < MM; ++r)
+          if (r < m && c < n) Ko[r * n + c] = K[r];
+        if (c < m) a.k[(pb * NA + i) * m + c] = kv;
+      }
       if (a.Vxx) {
         T* o = a.Vxx + (pb * (NA + 1) + i) * nn;
 #pragma unroll
@@ -353,22 +356,29 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
       atomicAdd(&g_ric_stamp[15], 1ull);
     }
   }
-  if (valid && c == 0) a.status[prob] = (int)st;
+  if (valid && c == 0) {
+    if (JC) {  // V_0 of this horizon's sweep (the reference raises on failure: NaN)
+      const long long o = prob * a.jc_tmax + (L - 1);
+      a.jc_J[o] = alive ? v0 : T(NAN);
+      a.jc_status[o] = (int)st;
+    } else {
+      a.status[prob] = (int)st;
+    }
+  }
 }
 
 template <class T, int S, int MM>
 hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   const size_t lds = (size_t)2 * kProbPerBlock * kLdsTile * sizeof(T);
+  const dim3 grid((unsigned)blocks, a.jc_J ? (unsigned)a.jc_tmax : 1u);
 #ifdef HOP_DEV
   if (opt(HOP_OPT_STAMPS)) {  // diagnostic: section stamps (tools/stamps_riccati.py)
-    hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), dim3((unsigned)blocks), dim3(256), lds,
-                       stream, a);
+    hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), grid, dim3(256), lds, stream, a);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL((riccati_kernel<T, S, MM>), dim3((unsigned)blocks), dim3(256), lds, stream,
-                     a);
+  hipLaunchKernelGGL((riccati_kernel<T, S, MM>), grid, dim3(256), lds, stream, a);
   return hipGetLastError();
 }
 

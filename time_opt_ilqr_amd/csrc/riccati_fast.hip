@@ -386,8 +386,9 @@ __device__ __forceinline__ void st64(double v, __amdgpu_buffer_rsrc_t r, unsigne
 __device__ unsigned long long g_ricf_stamp[16];
 
 // EXP (developer builds, timing experiments only -- results are wrong): 1 drops
-// the stores, 2 the per-step LDS-DMA
-template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0>
+// the stores, 2 the per-step LDS-DMA.  JC: the J-curve form (mode 1, the grid's y
+// index is the horizon, no K / k / V stores; RiccatiArgs::jc_J)
+template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool JC = false>
 __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
   constexpr int S = NX, MM = MU;
   unsigned long long sec[12] = {};
@@ -431,8 +432,8 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
                                rX = rsrc(a.X + pb0 * (pX / 8), left * pX),
                                rU = rsrc(a.U + pb0 * (pU / 8), left * pU);
   const long long pK = (long long)NA * MM * S * 8, pk = (long long)NA * MM * 8;
-  const __amdgpu_buffer_rsrc_t rK = rsrc(a.K + pb0 * (pK / 8), left * pK),
-                               rk = rsrc(a.k + pb0 * (pk / 8), left * pk);
+  const __amdgpu_buffer_rsrc_t rK = rsrc(JC ? a.X : a.K + pb0 * (pK / 8), JC ? 0 : left * pK),
+                               rk = rsrc(JC ? a.X : a.k + pb0 * (pk / 8), JC ? 0 : left * pk);
   const long long pVxx = (long long)(NA + 1) * S * S * 8, pVx = (long long)(NA + 1) * S * 8,
                   pV0 = (long long)(NA + 1) * 8;
   constexpr bool wantv = WANTV;
@@ -440,7 +441,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   // range): K 4, k 1 [+ Vxx 12 (of the step before), Vx 1, V0 1].  (Row c of the
   // exactly symmetric V is also lane c's 12 registers, but 6 16-B stores of those
   // rows scatter 48 16-B pieces per instruction and measured 5 % slower in mode 1.)
-  constexpr int NST = 5 + (WANTV ? 14 : 0);
+  constexpr int NST = JC ? 0 : 5 + (WANTV ? 14 : 0);
   unsigned va[5], vb[2], vx_, vu_;
 #pragma unroll
   for (int j = 0; j < 5; ++j) va[j] = voff<CH_A>(j, lane, wave_prob0, pb0, a.batch, pA);
@@ -466,13 +467,13 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   const double* Qp = a.Q + pb * a.q_bstride;
   const double* Rp = a.R + pb * a.r_bstride;
   const double* Qfp = a.Qf + pb * a.qf_bstride;
-  const int L = valid ? a.horizon[pb] : 0;
+  const int L = valid ? (JC ? (int)blockIdx.y + 1 : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
   Lw = __builtin_amdgcn_readfirstlane(Lw);
   Lw = Lw < NA ? Lw : NA;
-  const double lam0 = a.lm[pb];
+  const double lam0 = JC ? a.lm_value : a.lm[pb];
 
   // loop-invariant cost blocks in registers: Q column c / row c, R column / row
   const int cq = c < S ? c : 0, cr = c < MM ? c : 0;
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
     stamp(11);
     // stores: every lane issues them (fixed count for vm_wait_n), lanes that do
     // not commit address out of range (dropped by the descriptor's range check)
-    if constexpr (EXP != 1) {
+    if constexpr (EXP != 1 && !JC) {
       const bool wr = commit && c < S;
       const unsigned so = (unsigned)i * (MM * S * 8), vo = wr ? voK : OOB;
 #pragma unroll
@@ -815,7 +816,15 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
       atomicAdd(&g_ricf_stamp[15], 1ull);
     }
   }
-  if (valid && c == 0) a.status[prob] = (int)st;
+  if (valid && c == 0) {
+    if constexpr (JC) {  // V_0 of this horizon's sweep (the reference raises on failure: NaN)
+      const long long o = prob * a.jc_tmax + (L - 1);
+      a.jc_J[o] = alive ? v0 : NAN;
+      a.jc_status[o] = (int)st;
+    } else {
+      a.status[prob] = (int)st;
+    }
+  }
 }
 
 template <int MODE, bool WANTV>
@@ -855,6 +864,13 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
   // (out-of-range store offsets start at 2 GiB)
   const long long NA = a.nalloc;
   if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0x7FFF0000ll) return hipErrorNotSupported;
+  if (a.jc_J) {  // the J-curve form: one launch, grid y = horizon 1..jc_tmax
+    const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+    hipLaunchKernelGGL((ricf::riccati_fast_kernel<1, false, false, 0, true>),
+                       dim3((unsigned)blocks, (unsigned)a.jc_tmax), dim3(256),
+                       (size_t)kWavesPerBlock * ricf::WAVE_BYTES, stream, a);
+    return hipGetLastError();
+  }
   if (a.mode == 1) return ricf::launch<1, true>(a, stream);
   return a.Vxx ? ricf::launch<0, true>(a, stream) : ricf::launch<0, false>(a, stream);
 }

@@ -425,6 +425,50 @@ def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
     return RiccatiResult(K, k, status, Vxx, Vx, V0)
 
 
+def bruteforce_jcurve(A, Bm, X, U, xg, u_ref, Q, R, Qf, t_max: int, *, lm_lambda: float = 1e-6,
+                      w_stage: float = 0.0, wrap_idx=None, qxx_extra=None, qx_extra=None,
+                      c_extra=None):
+    """bruteforce_all_Jt_backward_expansion (solver.py:293-358) for a batch: J [B, t_max]
+    with J[:, T-1] = V_0 of the length-T sweep, and the per-horizon status [B, t_max]
+    (ST_FAIL / ST_NONFINITE where the reference raises).  All t_max sweeps of every
+    problem run in one launch (hop_bruteforce_jcurve_*).  Inputs as riccati()."""
+    torch = _torch()
+    dt = A.dtype
+    A = _dev(A, "A", dt)
+    dev = A.device
+    Bn, N, n, _ = A.shape
+    Bm = _dev(Bm, "Bm", dt, dev)
+    m = Bm.shape[-1]
+    X = _dev(X, "X", dt, dev)
+    U = _dev(U, "U", dt, dev)
+    if (tuple(Bm.shape) != (Bn, N, n, m) or tuple(X.shape) != (Bn, N + 1, n)
+            or tuple(U.shape) != (Bn, N, m)):
+        raise ValueError("need A [B, N, n, n], Bm [B, N, n, m], X [B, N+1, n], U [B, N, m]")
+    xg = _dev(xg, "xg", dt, dev)
+    u_ref = _dev(u_ref, "u_ref", dt, dev)
+    Q = _dev(Q, "Q", dt, dev)
+    R = _dev(R, "R", dt, dev)
+    Qf = _dev(Qf, "Qf", dt, dev)
+    ex = [None if t is None else _dev(t, nm, dt, dev)
+          for t, nm in ((qxx_extra, "qxx_extra"), (qx_extra, "qx_extra"), (c_extra, "c_extra"))]
+    for t, shp in zip(ex, ((Bn, N, n, n), (Bn, N, n), (Bn, N))):
+        if t is not None and tuple(t.shape) != shp:
+            raise ValueError(f"extra stage-cost term must be {list(shp)}")
+    t_max = int(t_max)
+    J = torch.empty((Bn, t_max), dtype=dt, device=dev)
+    status = torch.empty((Bn, t_max), dtype=torch.int32, device=dev)
+    rc = _fn("hop_bruteforce_jcurve", dt)(
+        _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(X), _lib.ptr(U),
+        _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref), _bstride(u_ref, 1, "u_ref", Bn),
+        _lib.ptr(Q), _bstride(Q, 2, "Q", Bn), _lib.ptr(R), _bstride(R, 2, "R", Bn),
+        _lib.ptr(Qf), _bstride(Qf, 2, "Qf", Bn),
+        _lib.ptr(ex[0]), _lib.ptr(ex[1]), _lib.ptr(ex[2]), float(lm_lambda), float(w_stage),
+        wrap_mask(wrap_idx, n), Bn, N, n, m, t_max, _lib.ptr(J), _lib.ptr(status),
+        _lib.stream_handle(dev))
+    _lib.check(rc)
+    return J, status
+
+
 # ---------------------------------------------------------------------------
 # trajectory form: augmented.py:10-87 on the device (+ the fused sweep)
 # ---------------------------------------------------------------------------

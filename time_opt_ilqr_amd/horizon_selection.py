@@ -228,28 +228,25 @@ def bruteforce_all_Jt_backward_expansion(A_list, B_list, X, U, xg, u_ref, Q, R, 
                                          T_max: int, *, lm_lambda: float = 1e-6, wrap_idx=None,
                                          extra_stage_cost=None) -> np.ndarray:
     """Exact quadratic-model J(T) curve: T_max independent Riccati sweeps of
-    lengths 1..T_max, run as ONE batched launch (J[T-1] = V0 at t = 0)."""
-    torch = _torch()
+    lengths 1..T_max, run as ONE launch (hop_bruteforce_jcurve, grid y = T)."""
     T_max = int(T_max)
     X = np.asarray(X, dtype=float)
     U = np.asarray(U, dtype=float)
     if U.ndim == 1:
         U = U.reshape(-1, 1)
-    n, m = X.shape[1], U.shape[1]
-    A = _to_dev(np.stack([np.asarray(a, dtype=float) for a in A_list[:T_max]]))
-    Bm = _to_dev(np.stack([np.asarray(b, dtype=float) for b in B_list[:T_max]]))
-    Xd = _to_dev(X[:T_max + 1])
-    Ud = _to_dev(U[:T_max])
-    rep = lambda t: t.unsqueeze(0).expand(T_max, *t.shape).contiguous()  # noqa: E731
+    if T_max > len(A_list) or T_max > len(B_list) or T_max > len(U) or T_max + 1 > len(X):
+        raise IndexError("list index out of range")
+    n = X.shape[1]
+    A = _to_dev(np.stack([np.asarray(a, dtype=float) for a in A_list[:T_max]])[None])
+    Bm = _to_dev(np.stack([np.asarray(b, dtype=float) for b in B_list[:T_max]])[None])
     qxx, qx, c0 = _extra_arrays(extra_stage_cost, X, U, T_max)
-    rr = lambda a: None if a is None else rep(_to_dev(a[0]))  # noqa: E731
-    r = engine.riccati(rep(A), rep(Bm), rep(Xd), rep(Ud), _to_dev(np.asarray(xg, float)),
-                       _to_dev(np.atleast_1d(np.asarray(u_ref, float))), _to_dev(Q), _to_dev(R),
-                       _to_dev(as_terminal_weight(alpha, n)),
-                       torch.arange(1, T_max + 1, dtype=torch.int32), float(lm_lambda), mode=1,
-                       w_stage=float(w), wrap_idx=wrap_idx, qxx_extra=rr(qxx), qx_extra=rr(qx),
-                       c_extra=rr(c0), reg_max_tries=1)
-    st = r.status.cpu().numpy()
-    if (st & (_lib.ST_FAIL | _lib.ST_NONFINITE)).any():
+    dv = lambda a: None if a is None else _to_dev(a)  # noqa: E731
+    J, st = engine.bruteforce_jcurve(
+        A, Bm, _to_dev(X[None, :T_max + 1]), _to_dev(U[None, :T_max]),
+        _to_dev(np.asarray(xg, float)), _to_dev(np.atleast_1d(np.asarray(u_ref, float))),
+        _to_dev(Q), _to_dev(np.atleast_2d(R)), _to_dev(as_terminal_weight(alpha, n)), T_max,
+        lm_lambda=float(lm_lambda), w_stage=float(w), wrap_idx=wrap_idx, qxx_extra=dv(qxx),
+        qx_extra=dv(qx), c_extra=dv(c0))
+    if (st.cpu().numpy() & (_lib.ST_FAIL | _lib.ST_NONFINITE)).any():
         raise np.linalg.LinAlgError("chol_solve failed: matrix not PD after jitter")
-    return r.V0[:, 0].cpu().numpy()
+    return J[0].cpu().numpy()

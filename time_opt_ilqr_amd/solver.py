@@ -70,8 +70,12 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
                        dt: float, U_init=None, max_iter: int = 15, lm_init: float = 1e-3,
                        wrap_idx: Optional[Sequence[int]] = None, use_central_diff: bool = True,
                        obstacles=None, alphas=ALPHAS, device=None,
-                       stage_timers: bool = True) -> Dict[str, Any]:
-    """Batched ilqr_timeopt(method="propagator") (solver.py:449-765).
+                       stage_timers: bool = True, method: str = "propagator") -> Dict[str, Any]:
+    """Batched ilqr_timeopt(method="propagator" | "bruteforce") (solver.py:449-765).
+
+    The select step is the LFT sweep of the augmented system (propagator) or the
+    brute-force J curve of T_max value-expansion sweeps (bruteforce, solver.py:293-358,
+    one hop_bruteforce_jcurve launch); everything after it is shared.
 
     x0 [n] or [B, n] (torch or NumPy); U_init [B, N, m] or None (u_ref tiled);
     xg/u_ref/Q/R shared or per problem; Qf = as_terminal_weight(alpha) [n, n];
@@ -81,6 +85,9 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     leaves the host waiting only on the once-per-iteration "all done" flag).
     """
     torch = _torch()
+    if method not in ("propagator", "bruteforce"):
+        raise NotImplementedError(f"method={method!r}: the device outer loop implements "
+                                  "'propagator' and 'bruteforce'")
     sid = engine.system_id(system)
     n, m = engine.system_dims(sid)
     dev = device or torch.device("cuda", torch.cuda.current_device())
@@ -105,6 +112,8 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     obs = None if obstacles is None or len(obstacles) == 0 else tt(obstacles)
     # w as a device scalar made once (a Python float would cost a fill launch per call)
     w_t = torch.full((1,), float(w), dtype=f64, device=dev)
+    w_f = float(w)
+    bits = torch.tensor([1 << i for i in range(8)], dtype=torch.int32, device=dev)
     cost = engine.CostParams(xg_t, ur_t, Q_t, R_t, Qf_t, w_t, obs, wrap_idx)
     if U_init is None:
         U = ur_t.reshape(-1, m).expand(Bn, m)[:, None, :].expand(Bn, N, m).contiguous()
@@ -170,10 +179,20 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         if obs is not None:
             c, cx, cxx = engine.obstacle_cost(s.X[:, :N], obs)
             ex = dict(qxx_extra=cxx, qx_extra=cx, c_extra=c)
-        sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, s.X, s.U, xg_t, ur_t, Q_t, R_inv,
-                                    P, w_t, wrap_idx=wrap_idx, n_use=T_max, t_min=T_min,
-                                    t_max=T_max, **ex)
-        T_star = sel.t_star
+        if method == "propagator":
+            sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, s.X, s.U, xg_t, ur_t, Q_t,
+                                        R_inv, P, w_t, wrap_idx=wrap_idx, n_use=T_max,
+                                        t_min=T_min, t_max=T_max, **ex)
+            T_star, sel_status, sel_J = sel.t_star, sel.status, sel.J
+        else:  # solver.py:607-614: the J curve at lm_lambda = 1e-6, argmin over [T_min, T_max]
+            sel_J, st_T = engine.bruteforce_jcurve(lin.A, lin.B, s.X, s.U, xg_t, ur_t, Q_t, R_t,
+                                                   Qf_t, T_max, lm_lambda=1e-6, w_stage=w_f,
+                                                   wrap_idx=wrap_idx, **ex)
+            T_star, _ = engine.select_horizon(sel_J, T_min, T_max)
+            # the reference raises at the first failing horizon: any horizon's
+            # failure bits make the problem's select status
+            sel_status = ((st_T.unsqueeze(-1) & bits) != 0).any(1).to(torch.int32).mul_(
+                bits).sum(1, dtype=torch.int32)
         clock("select", t0)
         t0 = time.perf_counter()
         ric = engine.riccati(lin.A, lin.B, s.X, s.U, xg_t, ur_t, Q_t, R_t, Qf_t, T_star, s.lm,
@@ -186,7 +205,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         # the reference raises out of ilqr_timeopt at the select (FloatingPointError /
         # LinAlgError): such problems become crashed and done; the line search runs
         # the others whose Riccati pass succeeded (one launch for both masks)
-        active = engine.ilqr_select_mask(s, sel.status, ric.status)
+        active = engine.ilqr_select_mask(s, sel_status, ric.status)
         fw = engine.forward_linesearch(sid, s.X, s.U, T_star, ric.K, ric.k, cost, dt,
                                        alphas=alphas, active=active)
         engine.ilqr_accept(s, fw.J, fw.accepted, T_star, warm=warm)
@@ -195,7 +214,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
             s.T_bar.copy_(T_star)
         s.X, s.U = fw.X, fw.U
         clock("forward", t0)
-        return sel.status, sel.J
+        return sel_status, sel_J
 
     # Problems that met the stop rule (or whose select raised) leave the batch: the
     # remaining ones run as a compact batch, so finished problems cost nothing (a
@@ -368,11 +387,13 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
                  lm_init: float = 1e-3, S_window: int = 20, wrap_idx: Optional[List[int]] = None,
                  use_central_diff: bool = True, extra_stage_cost=None,
                  onepass_preimage: str = "fixedpoint") -> Dict[str, Any]:
-    """solver.py:449-765 for one problem, method="propagator" (GPU end to end).
-    S_window / onepass_preimage only matter for method="onepass" (not on the device)."""
-    if method != "propagator":
+    """solver.py:449-765 for one problem, method="propagator" or "bruteforce" (GPU end
+    to end).  S_window / onepass_preimage only matter for method="onepass" (not on
+    the device)."""
+    if method not in ("propagator", "bruteforce"):
         raise NotImplementedError("the device outer loop implements method='propagator' "
-                                  "(the reference's 'ourmethod')")
+                                  "(the reference's 'ourmethod') and 'bruteforce' "
+                                  "('baseline1')")
     F = _dyn(F)
     obs = _obstacle_rows(extra_stage_cost)
     n = F.n
@@ -381,9 +402,11 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
                              as_terminal_weight(alpha, n), float(w), N, T_min, T_max, dt=F.dt,
                              U_init=U_init, max_iter=max_iter, lm_init=lm_init,
                              wrap_idx=wrap_idx, use_central_diff=use_central_diff,
-                             obstacles=obs, device=_dev())
+                             obstacles=obs, device=_dev(), method=method)
     if int(res["crashed"][0].item()):
-        raise np.linalg.LinAlgError("propagator_all_Jt_aug failed (non-finite or not PD)")
+        raise np.linalg.LinAlgError(
+            ("propagator_all_Jt_aug" if method == "propagator" else
+             "bruteforce_all_Jt_backward_expansion") + " failed (non-finite or not PD)")
     nh = int(res["n_hist"][0].item())
     return {"X": res["X"][0].cpu().numpy(), "U": res["U"][0].cpu().numpy(),
             "J_hist": [float(v) for v in res["J_hist"][0, :nh].cpu().numpy()],
@@ -395,3 +418,8 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
 
 def ilqr_timeopt_ourmethod(*args, **kwargs):
     return ilqr_timeopt(*args, method="propagator", **kwargs)
+
+
+def ilqr_timeopt_baseline1(*args, **kwargs):
+    """solver.py:775-776"""
+    return ilqr_timeopt(*args, method="bruteforce", **kwargs)

@@ -13,7 +13,7 @@ by construction.  The CPU leg runs the oracle's scalar line search
 (oracle/ilqr_oracle.forward_linesearch, one F call per step as the reference
 does) on a bounded sample.
 
-Line 2 (quadrotor, --loop): ilqr_timeopt_batch(method="propagator") for a
+Line 2 (quadrotor, --loop): ilqr_timeopt_batch(method=each of --methods) for a
 batch of problems around the maker's x0 (random offsets), fixed
 ``--loop-iters`` iterations (max_iter, the stop rule active): problem-iterations
 per second and the per-stage device time, next to the oracle's scalar outer
@@ -111,7 +111,7 @@ def bench_linesearch(sid, name, Bn, N, rounds, iters, cpu_seconds):
         "cpu_baseline": cpu}), flush=True)
 
 
-def bench_loop(Bn, N, iters, cpu_seconds, loop_rounds=5):
+def bench_loop(Bn, N, iters, cpu_seconds, loop_rounds=5, method="propagator"):
     import torch
     from time_opt_ilqr_amd import solver, systems
     from oracle import ilqr_oracle as io
@@ -120,7 +120,7 @@ def bench_loop(Bn, N, iters, cpu_seconds, loop_rounds=5):
     rng = np.random.default_rng(9)
     X0 = x0 + 0.2 * rng.standard_normal((Bn, F.n))
     Qf = io.orc.terminal_weight(alpha, F.n)
-    kw = dict(dt=F.dt, max_iter=iters, wrap_idx=wrap, use_central_diff=False)
+    kw = dict(dt=F.dt, max_iter=iters, wrap_idx=wrap, use_central_diff=False, method=method)
     # warm-up on the same batch: the first use of torch's gather / scatter kernels
     # (active-set compaction) loads them lazily
     solver.ilqr_timeopt_batch(2, X0, xg, u_ref, Q, R, Qf, w, N, T_min, T_max, **kw)
@@ -143,7 +143,7 @@ def bench_loop(Bn, N, iters, cpu_seconds, loop_rounds=5):
         done_its = 0
         while cnt < Bn and time.perf_counter() - t0 < cpu_seconds:
             o = io.ilqr_timeopt(2, F.dt, X0[cnt], xg, u_ref, Q, R, Qf, w, N, T_min, T_max,
-                                max_iter=iters, wrap_idx=wrap, central=False)
+                                max_iter=iters, wrap_idx=wrap, central=False, method=method)
             done_its += len(o["J_hist"])
             cnt += 1
         cel = time.perf_counter() - t0
@@ -151,7 +151,7 @@ def bench_loop(Bn, N, iters, cpu_seconds, loop_rounds=5):
                "sample": f"{cnt} outer loops (max_iter={iters}) of oracle/ilqr_oracle.py, "
                          f"{cel:.1f} s"}
     print(json.dumps({
-        "metric": "batched iLQR outer loop (propagator), quadrotor", "batch": Bn, "N": N,
+        "metric": f"batched iLQR outer loop ({method}), quadrotor", "batch": Bn, "N": N,
         "T_min": T_min, "T_max": T_max, "max_iter": iters, "iterations_run": its,
         "value": Bn / el, "unit": "problems/s", "problem_iterations_per_s": Bn * its / el,
         "wall_s": el, "wall_runs": len(walls), "stage_s": {k: round(v, 6) for k, v in res["timers"].items()},
@@ -169,6 +169,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--loop-iters", type=int, default=4)
     ap.add_argument("--no-loop", action="store_true")
+    ap.add_argument("--methods", default="propagator",
+                    help="comma list of outer-loop select methods (propagator, bruteforce)")
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     args = ap.parse_args()
     names = sorted(SYS, key=SYS.get) if args.system == "all" else [args.system]
@@ -176,7 +178,8 @@ def main():
         bench_linesearch(SYS[name], name, args.batch, args.N, args.rounds, args.iters,
                          args.cpu_seconds)
     if not args.no_loop:
-        bench_loop(args.batch, args.N, args.loop_iters, args.cpu_seconds)
+        for meth in args.methods.split(","):
+            bench_loop(args.batch, args.N, args.loop_iters, args.cpu_seconds, method=meth)
 
 
 if __name__ == "__main__":

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--prewarm-s", type=float, default=1.0)
     ap.add_argument("--variants", default="0", help="comma list; nonzero needs HOP_LIB=<dev build>")
     ap.add_argument("--generic", action="store_true", help="also time HOP_OPT_FORCE_GENERIC")
+    ap.add_argument("--jcurve", action="store_true",
+                    help="also time the brute-force J curve (mode 2 in the output)")
     ap.add_argument("--libs", default="",
                     help="comma list of library paths to A/B in this process (variant 0 of each)")
     args = ap.parse_args()
@@ -54,10 +56,16 @@ def main():
     from bench import riccati_bytes, riccati_flops  # SURVEY.md 8(d) count, term by term
     flop = {md: riccati_flops(n, m, N, md) for md in (0, 1)}
     byts = {md: riccati_bytes(n, m, N, md) for md in (0, 1)}
+    # "mode" 2 = the brute-force J curve (hop_bruteforce_jcurve): N value-expansion
+    # sweeps of lengths 1..N in one launch; flops summed over the horizons, bytes =
+    # the inputs once (A, B, X, U) + J and the per-horizon status written
+    flop[2] = sum(riccati_flops(n, m, T, 1) for T in range(1, N + 1))
+    byts[2] = 8 * (N * n * n + N * n * m + (N + 1) * n + N * m) + 12 * N
     libs = {"": _lib.load()}
     for p in filter(None, args.libs.split(",")):
         libs[p] = _lib.load(p)
-    cases = [(v, md, False, lp) for lp in libs for v in args.variants.split(",") for md in (0, 1)]
+    modes = (0, 1, 2) if args.jcurve else (0, 1)
+    cases = [(v, md, False, lp) for lp in libs for v in args.variants.split(",") for md in modes]
     if args.generic:
         cases += [("0", md, True, "") for md in (0, 1)]
 
@@ -65,6 +73,10 @@ def main():
         v, md, gen, lp = case
         _lib._lib = libs[lp]
         with _lib.options(variant=int(v), force_generic=gen):
+            if md == 2:
+                J, st = engine.bruteforce_jcurve(A, Bm, X, U, xg, ur, Q, R, Qf, N,
+                                                 lm_lambda=1e-6, w_stage=0.1)
+                return engine.RiccatiResult(None, None, st, None, None, J)
             return engine.riccati(A, Bm, X, U, xg, ur, Q, R, Qf, N, 1e-3, mode=md)
 
     t0 = time.perf_counter()
