@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   const T* Rp = a.R + pb * a.r_bstride;
   const T* Qfp = a.Qf + pb * a.qf_bstride;
   const bool JC = a.jc_J != nullptr;  // J-curve form: the grid's y index is the horizon
-  const int L = valid ? (JC ? (int)blockIdx.y + 1 : a.horizon[pb]) : 0;
+  const int L = valid ? (JC ? a.jc_tmax - (int)blockIdx.y : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));

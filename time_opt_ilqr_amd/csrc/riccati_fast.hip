@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   const double* Qp = a.Q + pb * a.q_bstride;
   const double* Rp = a.R + pb * a.r_bstride;
   const double* Qfp = a.Qf + pb * a.qf_bstride;
-  const int L = valid ? (JC ? (int)blockIdx.y + 1 : a.horizon[pb]) : 0;
+  const int L = valid ? (JC ? a.jc_tmax - (int)blockIdx.y : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
@@ -864,7 +864,7 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
   // (out-of-range store offsets start at 2 GiB)
   const long long NA = a.nalloc;
   if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0x7FFF0000ll) return hipErrorNotSupported;
-  if (a.jc_J) {  // the J-curve form: one launch, grid y = horizon 1..jc_tmax
+  if (a.jc_J) {  // the J-curve form: one launch, grid y = horizon jc_tmax..1
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
     hipLaunchKernelGGL((ricf::riccati_fast_kernel<1, false, false, 0, true>),
                        dim3((unsigned)blocks, (unsigned)a.jc_tmax), dim3(256),

@@ -228,7 +228,7 @@ def bruteforce_all_Jt_backward_expansion(A_list, B_list, X, U, xg, u_ref, Q, R, 
                                          T_max: int, *, lm_lambda: float = 1e-6, wrap_idx=None,
                                          extra_stage_cost=None) -> np.ndarray:
     """Exact quadratic-model J(T) curve: T_max independent Riccati sweeps of
-    lengths 1..T_max, run as ONE launch (hop_bruteforce_jcurve, grid y = T)."""
+    lengths 1..T_max, run as ONE launch (hop_bruteforce_jcurve, grid y = horizon)."""
     T_max = int(T_max)
     X = np.asarray(X, dtype=float)
     U = np.asarray(U, dtype=float)
