@@ -300,7 +300,8 @@ int hop_riccati_f32(const float* A, const float* Bm, const float* X, const float
  *          ilqr_timeopt(method="bruteforce"), solver.py:525-532 / 607-614)
  *   J[b][T-1] = V_0 of the length-T value-expansion sweep (mode 1 arithmetic with
  *   the fixed lm_lambda and chol_solve's jitter ladder) for T = 1..t_max: all
- *   t_max sweeps of every problem in ONE launch (grid y = t_max - T, longest first).  Inputs as
+ *   t_max sweeps of every problem in ONE launch (one workgroup per 16-problem block
+ *   and horizon, a block's horizons adjacent, longest first).  Inputs as
  *   hop_riccati_*; t_max <= n_alloc.
  *   Outputs: J [batch][t_max]; status [batch][t_max] per horizon (HOP_ST_FAIL /
  *   HOP_ST_NONFINITE where the reference raises LinAlgError / FloatingPointError;

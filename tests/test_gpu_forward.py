@@ -473,3 +473,27 @@ def test_ilqr_batch_bruteforce_mixed_problems_vs_oracle(dev):
         assert [int(t) for t in _np(res["T_hist"][b, :nh])] == o["T_hist"], b
         assert _rel(_np(res["J_hist"][b, :nh]), o["J_hist"]) <= 1e-9, b
     assert not _np(res["crashed"]).any()
+
+
+def test_ilqr_batch_bruteforce_per_problem_goals_vs_oracle(dev):
+    """per-problem goals xg [B, n] (the non-compact batch path: stopped rows are
+    masked, not gathered out) with method="bruteforce": each problem against the
+    oracle's scalar bruteforce loop"""
+    from time_opt_ilqr_amd import solver, systems
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, _ = \
+        systems.make_double_integrator(N=40)
+    rng = np.random.default_rng(21)
+    Bn = 5
+    XG = np.asarray(xg, float) + rng.uniform(-1.0, 1.0, (Bn, 2))
+    Qf = np.asarray(io.orc.terminal_weight(alpha, 2))
+    res = solver.ilqr_timeopt_batch(0, np.stack([x0] * Bn), XG, u_ref, Q, R, Qf, w, 40, 8, 40,
+                                    dt=F.dt, max_iter=6, use_central_diff=False,
+                                    method="bruteforce")
+    nh = _np(res["n_hist"])
+    for b in range(Bn):
+        o = io.ilqr_timeopt(0, F.dt, x0, XG[b], u_ref, Q, R, Qf, w, 40, 8, 40, max_iter=6,
+                            central=False, method="bruteforce")
+        assert _np(res["T_hist"][b, :nh[b]]).tolist() == o["T_hist"], b
+        assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9, b
+        assert int(res["T_star"][b]) == o["T_star"]
+    assert len(set(_np(res["T_star"]).tolist())) > 1  # the goals give different horizons

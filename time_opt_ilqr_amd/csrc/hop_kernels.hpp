@@ -105,9 +105,9 @@ struct RiccatiArgs {
   T* Vx;   // [B][nalloc+1][n] or null
   T* V0;   // [B][nalloc+1] or null
   int* status;  // [B]
-  // J-curve form (hop_bruteforce_jcurve_*, solver.py:293-358): when jc_J is set the
-  // grid's y index is the horizon, longest first (L = jc_tmax - blockIdx.y, the same
-  // for a whole wave: the dispatcher walks y last, so the short sweeps fill the tail),
+  // J-curve form (hop_bruteforce_jcurve_*, solver.py:293-358): when jc_J is set,
+  // workgroup x runs problem block x / jc_tmax at horizon L = jc_tmax - x % jc_tmax
+  // (one horizon per wave; a block's horizons adjacent, longest first),
   // lm is the scalar lm_value, no K / k / V is stored and each (problem, horizon)
   // writes J[b][L-1] = V_0 and its status to jc_status[b][L-1]
   T* jc_J = nullptr;          // [B][jc_tmax]

@@ -50,7 +50,13 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   T* smem = reinterpret_cast<T*>(smem_raw);
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4, w = tid >> 6;
-  const long long prob = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave + g;
+  // J-curve form: workgroups [b * jc_tmax, (b+1) * jc_tmax) run problem block b at every
+  // horizon, longest first, so the re-reads of its A, B, x, u meet in the caches
+  const bool JC = a.jc_J != nullptr;
+  const unsigned jtm = JC ? (unsigned)a.jc_tmax : 1u;
+  const long long blk = (long long)(blockIdx.x / jtm);
+  const int jc_h = (int)(blockIdx.x % jtm);
+  const long long prob = (blk * kWavesPerBlock + w) * kProbPerWave + g;
   const bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
   T* tile = smem + (w * kProbPerWave + g) * kLdsTile;
@@ -75,8 +81,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   const T* Qp = a.Q + pb * a.q_bstride;
   const T* Rp = a.R + pb * a.r_bstride;
   const T* Qfp = a.Qf + pb * a.qf_bstride;
-  const bool JC = a.jc_J != nullptr;  // J-curve form: the grid's y index is the horizon
-  const int L = valid ? (JC ? a.jc_tmax - (int)blockIdx.y : a.horizon[pb]) : 0;
+  const int L = valid ? (JC ? a.jc_tmax - jc_h : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
@@ -371,7 +376,7 @@ template <class T, int S, int MM>
 hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   const size_t lds = (size_t)2 * kProbPerBlock * kLdsTile * sizeof(T);
-  const dim3 grid((unsigned)blocks, a.jc_J ? (unsigned)a.jc_tmax : 1u);
+  const dim3 grid((unsigned)(blocks * (a.jc_J ? a.jc_tmax : 1)));
 #ifdef HOP_DEV
   if (opt(HOP_OPT_STAMPS)) {  // diagnostic: section stamps (tools/stamps_riccati.py)
     hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), grid, dim3(256), lds, stream, a);

@@ -412,7 +412,12 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
 #pragma unroll 1
   for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = 0.0;
 
-  const long long wave_prob0 = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave;
+  // J-curve form: workgroups [b * jc_tmax, (b+1) * jc_tmax) run problem block b at every
+  // horizon, longest first, so the re-reads of its A, B, x, u meet in the caches
+  const unsigned jtm = JC ? (unsigned)a.jc_tmax : 1u;
+  const int jc_h = (int)(blockIdx.x % jtm);
+  const long long wave_prob0 =
+      ((long long)(blockIdx.x / jtm) * kWavesPerBlock + w) * kProbPerWave;
   const long long prob = wave_prob0 + g;
   const bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
@@ -467,7 +472,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   const double* Qp = a.Q + pb * a.q_bstride;
   const double* Rp = a.R + pb * a.r_bstride;
   const double* Qfp = a.Qf + pb * a.qf_bstride;
-  const int L = valid ? (JC ? a.jc_tmax - (int)blockIdx.y : a.horizon[pb]) : 0;
+  const int L = valid ? (JC ? a.jc_tmax - jc_h : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
@@ -864,10 +869,10 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
   // (out-of-range store offsets start at 2 GiB)
   const long long NA = a.nalloc;
   if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0x7FFF0000ll) return hipErrorNotSupported;
-  if (a.jc_J) {  // the J-curve form: one launch, grid y = horizon jc_tmax..1
+  if (a.jc_J) {  // the J-curve form: one launch, jc_tmax workgroups per problem block
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
     hipLaunchKernelGGL((ricf::riccati_fast_kernel<1, false, false, 0, true>),
-                       dim3((unsigned)blocks, (unsigned)a.jc_tmax), dim3(256),
+                       dim3((unsigned)(blocks * a.jc_tmax)), dim3(256),
                        (size_t)kWavesPerBlock * ricf::WAVE_BYTES, stream, a);
     return hipGetLastError();
   }
