@@ -445,6 +445,57 @@ def main_ilqr_bruteforce():
         ilqr_bruteforce_capture(*case)
 
 
+# plots/summary.csv (the reference's committed output of its published comparison):
+# T*, J* of the DoubleIntegrator and Quadrotor_Hover rows, per method
+SUMMARY_ROWS = {"di": "DoubleIntegrator", "quadrotor": "Quadrotor_Hover"}
+
+
+def summary_capture(tag, maker, method):
+    """ilqr_timeopt with the published comparison's settings (max_iter=20, lm_init=1e-3,
+    central differences, each maker's default N / T_min / T_max; the legacy driver,
+    ilqr_propagator.py:759-790, that wrote plots/summary.csv) through the current
+    solver (solver.py:449-765), which reproduces the csv's T* and J* for these two
+    cases.  The csv row's values ride along as data."""
+    import csv
+    import time
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, extra = \
+        getattr(ref_systems, maker)()
+    T_max = min(T_max, N)
+    t0 = time.perf_counter()
+    sol = ref_solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max,
+                                  method=method, max_iter=20, lm_init=1e-3,
+                                  wrap_idx=wrap_idx, use_central_diff=True)
+    wall = time.perf_counter() - t0
+    row = None
+    with open(os.path.join(REF, "plots", "summary.csv")) as f:
+        for r in csv.DictReader(f):
+            if r["case"] == SUMMARY_ROWS[tag] and r["method"] == method:
+                row = r
+    d = dict(N=N, T_min=T_min, T_max=T_max, max_iter=20, central=1, dt=float(F.dt), x0=x0,
+             xg=xg, u_ref=u_ref, Q=Q, R=R, Qf=ref_utils.as_terminal_weight(alpha, len(x0)), w=w,
+             wrap_idx=np.array(wrap_idx if wrap_idx else [], dtype=np.int64),
+             X=sol["X"], U=sol["U"], J_hist=np.array(sol["J_hist"]),
+             T_hist=np.array(sol["T_hist"]), T_star=int(sol["T_star"]),
+             J_curve=np.array(sol["J_curve"]),
+             ref_here_timers=np.array([sol["timers"][k] for k in
+                                       ("linearize", "select", "backward", "forward")]),
+             ref_here_wall=wall,
+             csv_T_star=int(row["T_star"]), csv_J_star=float(row["J_star"]),
+             csv_timers=np.array([float(row[k]) for k in
+                                  ("t_linearize", "t_select", "t_backward", "t_forward")]),
+             csv_n_iterations=int(row["n_iterations"]))
+    np.savez_compressed(os.path.join(HERE, f"summary_{tag}_{method}.npz"), **d)
+    print(f"summary_{tag}_{method}: T*={sol['T_star']} J*={sol['J_hist'][-1]!r} "
+          f"(csv {row['T_star']}, {row['J_star']}) timers={sol['timers']}")
+
+
+def main_summary():
+    np.seterr(all="ignore")
+    for tag, maker in (("di", "make_double_integrator"), ("quadrotor", "make_quadrotor")):
+        for method in ("propagator", "bruteforce"):
+            summary_capture(tag, maker, method)
+
+
 def main_ilqr():
     np.seterr(all="ignore")
     for case in ILQR_CASES:
@@ -660,6 +711,8 @@ if __name__ == "__main__":
         main_traj()
     elif "--lin" in sys.argv:  # only the dynamics / linearisation fixtures
         main_lin()
+    elif "--summary" in sys.argv:  # the plots/summary.csv comparison, both methods
+        main_summary()
     elif "--ilqr-bf" in sys.argv:  # ilqr_timeopt(method="bruteforce") end to end
         main_ilqr_bruteforce()
     elif "--ilqr" in sys.argv:  # only the forward line search / outer loop fixtures

@@ -497,3 +497,26 @@ def test_ilqr_batch_bruteforce_per_problem_goals_vs_oracle(dev):
         assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9, b
         assert int(res["T_star"][b]) == o["T_star"]
     assert len(set(_np(res["T_star"]).tolist())) > 1  # the goals give different horizons
+
+
+@pytest.mark.parametrize("tag,method", [("di", "propagator"), ("di", "bruteforce"),
+                                        ("quadrotor", "propagator"),
+                                        ("quadrotor", "bruteforce")])
+def test_summary_csv_rows_on_the_device(dev, golden_dir, tag, method):
+    """The reference's published comparison (plots/summary.csv, written by the legacy
+    driver with max_iter=20, central differences, the makers' default N / T range):
+    the device drop-in reproduces the reference's current-solver run of it (T_hist,
+    J_hist 1e-9) and the committed csv row's T* and J* (to 1e-9), for both methods."""
+    from time_opt_ilqr_amd import solver, systems
+    d = np.load(os.path.join(golden_dir, f"summary_{tag}_{method}.npz"))
+    mk = systems.make_double_integrator if tag == "di" else systems.make_quadrotor
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, _ = mk()
+    assert (N, T_min, min(T_max, N)) == (int(d["N"]), int(d["T_min"]), int(d["T_max"]))
+    sol = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, int(d["T_max"]),
+                              method=method, max_iter=20, lm_init=1e-3, wrap_idx=wrap_idx,
+                              use_central_diff=True)
+    assert sol["T_hist"] == [int(t) for t in d["T_hist"]]
+    assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= 1e-9
+    assert sol["T_star"] == int(d["csv_T_star"])
+    assert abs(sol["J_hist"][-1] - float(d["csv_J_star"])) <= 1e-9 * abs(float(d["csv_J_star"]))
+    assert len(sol["J_hist"]) == int(d["csv_n_iterations"])
