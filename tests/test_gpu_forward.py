@@ -520,3 +520,25 @@ def test_summary_csv_rows_on_the_device(dev, golden_dir, tag, method):
     assert sol["T_star"] == int(d["csv_T_star"])
     assert abs(sol["J_hist"][-1] - float(d["csv_J_star"])) <= 1e-9 * abs(float(d["csv_J_star"]))
     assert len(sol["J_hist"]) == int(d["csv_n_iterations"])
+
+
+def test_bruteforce_jcurve_fp32_entry(dev):
+    """hop_bruteforce_jcurve_f32 (the generic kernel's fp32 instantiation) against the
+    fp64 curve on the same well-conditioned quadrotor linearisation: 1e-4 relative
+    (fp32 accumulation over up to 40 steps)"""
+    import torch
+    from time_opt_ilqr_amd import engine
+    n, m, N, Bn = 12, 4, 40, 6
+    rng = np.random.default_rng(17)
+    X = rng.standard_normal((Bn, N + 1, n)) * 0.3
+    U = rng.standard_normal((Bn, N, m)) * 0.1
+    lin = engine.linearize(2, _t(X, dev), _t(U, dev), 0.05, central=False)
+    args64 = [lin.A, lin.B, _t(X, dev), _t(U, dev), _t(np.zeros(n), dev),
+              _t(np.array([9.81, 0, 0, 0]), dev), _t(np.diag(rng.uniform(0.5, 2, n)), dev),
+              _t(np.diag(rng.uniform(0.5, 2, m)), dev), _t(20 * np.eye(n), dev)]
+    J64, s64 = engine.bruteforce_jcurve(*args64, N, lm_lambda=1e-6, w_stage=0.05)
+    J32, s32 = engine.bruteforce_jcurve(*[a.to(torch.float32) for a in args64], N,
+                                        lm_lambda=1e-6, w_stage=0.05)
+    assert J32.dtype == torch.float32 and J32.shape == (Bn, N)
+    assert (_np(s64) == 0).all() and (_np(s32) == 0).all()
+    assert _rel(_np(J32).astype(np.float64), _np(J64)) <= 1e-4
