@@ -542,3 +542,34 @@ def test_bruteforce_jcurve_fp32_entry(dev):
     assert J32.dtype == torch.float32 and J32.shape == (Bn, N)
     assert (_np(s64) == 0).all() and (_np(s32) == 0).all()
     assert _rel(_np(J32).astype(np.float64), _np(J64)) <= 1e-4
+
+
+def test_bruteforce_jcurve_full_size_spot_checks(dev):
+    """the bench size (B = 4096, N = T_max = 100, quadrotor shape; 409,600 sweeps in
+    one launch): the first, a middle and the last problem against the oracle's
+    bruteforce_J at 1e-9 relative, every status 0"""
+    import torch
+    from time_opt_ilqr_amd import engine
+    from oracle import hop_oracle as orc
+    Bn, N, n, m = 4096, 100, 12, 4
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    kw = dict(device=dev, dtype=torch.float64, generator=g)
+    A = torch.eye(n, device=dev, dtype=torch.float64) + 0.05 * torch.randn((Bn, N, n, n), **kw)
+    Bm = 0.1 * torch.randn((Bn, N, n, m), **kw)
+    X = 0.5 * torch.randn((Bn, N + 1, n), **kw)
+    U = 0.1 * torch.randn((Bn, N, m), **kw)
+    xg = 0.2 * torch.randn((n,), **kw)
+    ur = 0.05 * torch.randn((m,), **kw)
+    M = torch.randn((n, n), **kw)
+    Q = M @ M.T / n + 0.5 * torch.eye(n, device=dev, dtype=torch.float64)
+    R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
+    Qf = 10.0 * torch.eye(n, device=dev, dtype=torch.float64)
+    J, st = engine.bruteforce_jcurve(A, Bm, X, U, xg, ur, Q, R, Qf, N, lm_lambda=1e-6,
+                                     w_stage=0.1)
+    assert int((st != 0).sum()) == 0
+    Jn = _np(J)
+    for b in (0, Bn // 2 + 3, Bn - 1):
+        ref = orc.bruteforce_J(list(_np(A[b])), list(_np(Bm[b])), _np(X[b]), _np(U[b]), _np(xg),
+                               _np(ur), _np(Q), _np(R), _np(Qf), 0.1, N)
+        assert _rel(Jn[b], ref) <= 1e-9, b
