@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: batched LFT backward sweeps/s (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload lft|config3|config5|select_gains]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--workload lft|config3|config5|select_gains|bruteforce]
     torchrun --nproc-per-node N bench.py --gpus N ...      (driver form, N > 1)
 
 A "step" is one pass of the hot path over one batch: the fused LFT sweep
@@ -159,7 +160,35 @@ def _cpu_worker(args):
     return count, time.perf_counter() - t0
 
 
-def cpu_baseline(s, m, N, target_s=8.0):
+def _cpu_worker_bf(args):
+    seed0, count, n, m, N = args
+    from oracle import hop_oracle as orc
+    t0 = time.perf_counter()
+    for i in range(count):
+        A, Bm, X, U, xg, ur, Q, R, Qf = synth_riccati_problem(seed0 + i, n, m, N)
+        orc.bruteforce_J(list(A), list(Bm), X, U, xg, ur, Q, R, Qf, 0.5, N)
+    return count, time.perf_counter() - t0
+
+
+def synth_riccati_problem(seed, n, m, N):
+    """One problem of the Riccati workloads' distribution (NumPy PCG64; the device
+    runs draw the same distribution from torch's generator)."""
+    import numpy as np
+    rng = np.random.default_rng(int(seed))
+    A = np.eye(n) + 0.05 * rng.standard_normal((N, n, n))
+    Bm = 0.1 * rng.standard_normal((N, n, m))
+    X = 0.5 * rng.standard_normal((N + 1, n))
+    U = 0.3 * rng.standard_normal((N, m))
+    xg = 0.2 * rng.standard_normal(n)
+    ur = 0.1 * rng.standard_normal(m)
+    M = rng.standard_normal((n, n))
+    Q = M @ M.T / n + 0.5 * np.eye(n)
+    R = np.diag(0.5 + 1.5 * rng.random(m))
+    Qf = np.diag(1.0 + 9.0 * rng.random(n))
+    return A, Bm, X, U, xg, ur, Q, R, Qf
+
+
+def cpu_baseline(s, m, N, target_s=8.0, bruteforce=False):
     """Sweeps/s of the NumPy restatement on every usable host core (one process
     per core, one BLAS thread each); the per-process sample is sized from a
     one-sweep probe to about target_s seconds of work."""
@@ -168,15 +197,23 @@ def cpu_baseline(s, m, N, target_s=8.0):
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
     os.environ["OMP_NUM_THREADS"] = "1"
     ctx = mp.get_context("spawn")
+    work = _cpu_worker_bf if bruteforce else _cpu_worker
+    dim = s - 1 if bruteforce else s  # the brute-force curve runs on the raw n = s - 1
     with ctx.Pool(cores) as pool:
-        probe = pool.map(_cpu_worker, [(0, 2, s, m, N)] * cores)  # imports + timing probe
+        probe = pool.map(work, [(0, 1 if bruteforce else 2, dim, m, N)] * cores)  # imports + probe
         per_sweep = max(t / c for c, t in probe)
-        per_core = max(4, int(target_s / max(per_sweep, 1e-6)))
-        jobs = [(10_000 + c * per_core, per_core, s, m, N) for c in range(cores)]
+        per_core = max(2 if bruteforce else 4, int(target_s / max(per_sweep, 1e-6)))
+        jobs = [(10_000 + c * per_core, per_core, dim, m, N) for c in range(cores)]
         t0 = time.perf_counter()
-        res = pool.map(_cpu_worker, jobs)
+        res = pool.map(work, jobs)
         wall = time.perf_counter() - t0
     done = sum(r[0] for r in res)
+    if bruteforce:
+        return {"value": done / wall, "unit": "problems/s", "cores": cores, "kind": "port",
+                "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+                "sample": f"{done} brute-force J curves (n={dim}, m={m}, T_max={N}, fp64: "
+                          f"{N} Riccati sweeps each) of oracle/hop_oracle.bruteforce_J, {cores} "
+                          f"processes x 1 BLAS thread, {wall:.1f} s wall"}
     return {"value": done / wall, "unit": "sweeps/s", "cores": cores, "kind": "port",
             "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": f"{done} synthetic sweeps (s={s}, m={m}, N={N}, fp64) of the NumPy "
@@ -302,8 +339,44 @@ def _select_gains_workload(args, world, lo, hi, dev):
     return launch, info
 
 
+def _bruteforce_workload(args, world, lo, hi, dev):
+    """baseline1's select (solver.py:293-358 + the argmin of solver.py:613): the
+    brute-force J curve of T_max = N Riccati sweeps per problem in one launch."""
+    import types
+    import torch
+    from time_opt_ilqr_amd import engine
+    Bn, n, m, N = hi - lo, args.s - 1, args.m, args.N
+    g = torch.Generator(device=dev)
+    g.manual_seed(13 + lo)
+    kw = dict(device=dev, dtype=torch.float64, generator=g)
+    eye = torch.eye(n, device=dev, dtype=torch.float64)
+    A = eye + 0.05 * torch.randn((Bn, N, n, n), **kw)
+    Bm = 0.1 * torch.randn((Bn, N, n, m), **kw)
+    X = 0.5 * torch.randn((Bn, N + 1, n), **kw)
+    U = 0.3 * torch.randn((Bn, N, m), **kw)
+    xg = 0.2 * torch.randn((n,), **kw)
+    ur = 0.1 * torch.randn((m,), **kw)
+    M = torch.randn((n, n), **kw)
+    Q = M @ M.T / n + 0.5 * eye
+    R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
+    Qf = torch.diag(1.0 + 9.0 * torch.rand((n,), **kw))
+    t_min = min(args.t_min, N)
+
+    def launch():
+        J, st = engine.bruteforce_jcurve(A, Bm, X, U, xg, ur, Q, R, Qf, N, lm_lambda=1e-6,
+                                         w_stage=0.5)
+        t, j = engine.select_horizon(J, t_min, N)
+        return types.SimpleNamespace(t_star=t, j_star=j, J=J, status=st)
+
+    info = dict(kernel="riccati_fast_kernel<1,false,false,0,true> (J-curve form)", bound="fp64",
+                flops=sum(riccati_flops(n, m, T, 1) for T in range(1, N + 1)),
+                bytes=8 * (N * (n * n + n * m + m) + (N + 1) * n) + 12 * N, executed=None,
+                t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
+    return launch, info
+
+
 WORKLOADS = {"lft": _lft_workload, "config3": _lft_workload, "config5": _config5_workload,
-             "select_gains": _select_gains_workload}
+             "select_gains": _select_gains_workload, "bruteforce": _bruteforce_workload}
 
 
 def main():
@@ -342,7 +415,8 @@ def main():
     dflt = {"lft": (4096 if world == 1 else 32768, 13, 4, 100, "f64"),
             "config3": (65536, 5, 1, 200, "f32"),
             "config5": (16384, 13, 4, 128, "f32"),
-            "select_gains": (4096, 13, 4, 100, "f64")}[wl]
+            "select_gains": (4096, 13, 4, 100, "f64"),
+            "bruteforce": (4096, 13, 4, 100, "f64")}[wl]
     args.batch = args.batch or dflt[0]
     args.s = args.s or dflt[1]
     args.m = args.m or dflt[2]
@@ -467,7 +541,7 @@ def main():
             traffic = None
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(s, m, N)
+            cpu = cpu_baseline(s, m, N, bruteforce=wl == "bruteforce")
             if wl == "select_gains":
                 cpu["note"] = "LFT sweep only (the Riccati gains are not in the CPU sample)"
         roof = {"bound": info["bound"], "achieved": achieved, "peak": peak, "unit": unit,
@@ -496,11 +570,13 @@ def main():
                  "config5": "config 5: mixed Segway/Cartpole/Quadrotor (i mod 3), "
                             "LFT sweep + fused argmin",
                  "select_gains": "select (in-kernel augmentation + LFT + argmin) + truncated "
-                                 "Riccati gains at each T* (solver.py:581-597)"}
+                                 "Riccati gains at each T* (solver.py:581-597)",
+                 "bruteforce": "baseline1 select: brute-force J curve (T_max = N Riccati "
+                               "sweeps per problem, solver.py:293-358) + argmin"}
         line = {
             "metric": baseline_metric(),
             "value": value,
-            "unit": "sweeps/s" if wl != "select_gains" else "problems/s",
+            "unit": "sweeps/s" if wl not in ("select_gains", "bruteforce") else "problems/s",
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,

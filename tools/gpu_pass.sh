@@ -11,5 +11,6 @@ timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err && \
 timeout -k 10 300 python bench.py --workload config3 --no-cpu-baseline > $OUT/bench_config3.json 2> $OUT/bench_config3.err && \
 timeout -k 10 300 python bench.py --workload config5 --no-cpu-baseline > $OUT/bench_config5.json 2> $OUT/bench_config5.err && \
 timeout -k 10 300 python bench.py --workload select_gains --no-cpu-baseline > $OUT/bench_sg.json 2> $OUT/bench_sg.err && \
-timeout -k 10 300 python bench.py --batch 32768 --no-cpu-baseline > $OUT/bench_c4shard.json 2> $OUT/bench_c4shard.err
+timeout -k 10 300 python bench.py --batch 32768 --no-cpu-baseline > $OUT/bench_c4shard.json 2> $OUT/bench_c4shard.err && \
+timeout -k 10 300 python bench.py --workload bruteforce --steps 5 > $OUT/bench_bf.json 2> $OUT/bench_bf.err
 echo "gpu_pass rc=$?"
