@@ -564,8 +564,8 @@ def main():
             roof["batch_major_kernel_ms"] = alt_ms
             roof["batch_major_frac"] = (info["bytes"] * per_launch / (alt_ms * 1e-3) / 1e9
                                         / PEAK_HBM_GBS)
-        names = {"lft": ("config 2: LFT sweep + fused argmin" if world == 1 else
-                         "config 4 shard: LFT sweep + fused argmin"),
+        names = {"lft": ("config 2: LFT sweep + fused argmin" if world == 1 and Bn != 32768
+                         else "config 4 shard: LFT sweep + fused argmin"),
                  "config3": "config 3: LFT sweep + fused argmin (small-s kernel)",
                  "config5": "config 5: mixed Segway/Cartpole/Quadrotor (i mod 3), "
                             "LFT sweep + fused argmin",
