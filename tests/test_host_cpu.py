@@ -618,3 +618,21 @@ def test_tile64_descriptor_checks_shape():
                 torch.zeros(2, 3, 25, 64).transpose(0, 1)):
         with pytest.raises(ValueError):
             Tile64(bad, 70, 5, 5).check()
+
+
+def test_bench_bruteforce_counts_and_cpu_worker():
+    """bench.py --workload bruteforce: the FLOP count is the mode-1 Riccati count summed
+    over the horizons, and its CPU leg (the oracle's bruteforce_J on the workload's
+    distribution) equals the J curve of T_max separate oracle value sweeps"""
+    import bench
+    n, m, N = 4, 1, 6
+    assert sum(bench.riccati_flops(n, m, T, 1) for T in range(1, N + 1)) == \
+        bench.riccati_flops(n, m, 1, 1) * N * (N + 1) // 2
+    cnt, secs = bench._cpu_worker_bf((3, 1, n, m, N))
+    assert cnt == 1 and secs >= 0.0
+    A, Bm, X, U, xg, ur, Q, R, Qf = bench.synth_riccati_problem(3, n, m, N)
+    J = orc.bruteforce_J(list(A), list(Bm), X, U, xg, ur, Q, R, Qf, 0.5, N)
+    for T in (1, N):
+        _, _, V0, _, _ = orc.riccati_expand(list(A), list(Bm), X, U, xg, ur, Q, R, Qf, T, 0,
+                                            lm_lambda=1e-6, w_stage=0.5, reg_max_tries=1)
+        assert J[T - 1] == V0[0]
