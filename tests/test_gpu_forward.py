@@ -573,3 +573,40 @@ def test_bruteforce_jcurve_full_size_spot_checks(dev):
         ref = orc.bruteforce_J(list(_np(A[b])), list(_np(Bm[b])), _np(X[b]), _np(U[b]), _np(xg),
                                _np(ur), _np(Q), _np(R), _np(Qf), 0.1, N)
         assert _rel(Jn[b], ref) <= 1e-9, b
+
+
+def test_integration_md_ctypes_stubs_run(dev):
+    """INTEGRATION.md's ctypes stubs (the binding a maintainer would add to the
+    reference) run as written against the in-tree library and agree with engine"""
+    import re
+    import torch
+    from time_opt_ilqr_amd import _lib, engine
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(repo, "INTEGRATION.md")).read()
+    blocks = [b for b in re.findall(r"```python\n(.*?)```", text, re.S)
+              if "hop_lft_sweep_f64" in b or "hop_bruteforce_jcurve_f64" in b]
+    assert len(blocks) == 2
+    ns = {}
+    code = "\n".join(blocks).replace("/path/to/time_opt_ilqr_amd/libhop_amd.so", _lib.LIB_PATH)
+    exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    rng = np.random.default_rng(9)
+    n, m, N, Bn = 4, 2, 12, 3
+    A = np.eye(n) + 0.05 * rng.standard_normal((Bn, N, n, n))
+    Bm = 0.1 * rng.standard_normal((Bn, N, n, m))
+    X = 0.5 * rng.standard_normal((Bn, N + 1, n))
+    U = 0.1 * rng.standard_normal((Bn, N, m))
+    xg, ur = np.zeros(n), np.zeros(m)
+    Q, R, Qf = np.eye(n), 0.5 * np.eye(m), 10 * np.eye(n)
+    J, st = ns["bruteforce_all_Jt_batched"](A, Bm, X, U, xg, ur, Q, R, Qf, N, 0.1)
+    Je, se = engine.bruteforce_jcurve(_t(A, dev), _t(Bm, dev), _t(X, dev), _t(U, dev), _t(xg, dev),
+                                      _t(ur, dev), _t(Q, dev), _t(R, dev), _t(Qf, dev), N,
+                                      w_stage=0.1)
+    assert np.array_equal(J, _np(Je)) and np.array_equal(st, _np(se)) and (st == 0).all()
+    from oracle import hop_oracle as orc
+    Aa, Ba, Qa, Ra, Ri, z0, QT = orc.synth_lft_batch(40, 2, 5, 1, 16)
+    Jl, stl, tsl = ns["propagator_all_Jt_aug_batched"](Aa, Ba, Qa, Ri[0], z0[0], QT, 16, 3, 16)
+    r = engine.propagate(_t(Aa, dev), _t(Ba, dev), _t(Qa, dev), _t(Ri[0], dev), _t(z0[0], dev),
+                         _t(QT, dev), t_min=3, t_max=16)
+    assert _rel(Jl, _np(r.J)) <= 1e-12 and np.array_equal(tsl, _np(r.t_star))
+    assert (stl == 0).all()
+    del torch
