@@ -610,3 +610,24 @@ def test_integration_md_ctypes_stubs_run(dev):
     assert _rel(Jl, _np(r.J)) <= 1e-12 and np.array_equal(tsl, _np(r.t_star))
     assert (stl == 0).all()
     del torch
+
+
+def test_ilqr_batch_large_batch_spot_checks(dev):
+    """the device outer loop at B = 65,536 quadrotor problems (16x the bench batch:
+    A_k alone is 7.5 GB, the line search's candidate rows 4.2 GB): the first, a
+    middle and the last problem against the oracle's scalar loop"""
+    from time_opt_ilqr_amd import solver, systems
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap, _ = systems.make_quadrotor(N=100)
+    Bn, N, T_min, T_max = 65536, 100, 20, 100
+    rng = np.random.default_rng(31)
+    X0 = x0 + 0.2 * rng.standard_normal((Bn, 12))
+    Qf = np.asarray(io.orc.terminal_weight(alpha, 12))
+    res = solver.ilqr_timeopt_batch(2, X0, xg, u_ref, Q, R, Qf, w, N, T_min, T_max, dt=F.dt,
+                                    max_iter=2, wrap_idx=wrap, use_central_diff=False,
+                                    device=dev, stage_timers=False)
+    nh = _np(res["n_hist"])
+    for b in (0, Bn // 2 + 1, Bn - 1):
+        o = io.ilqr_timeopt(2, F.dt, X0[b], xg, u_ref, Q, R, Qf, w, N, T_min, T_max, max_iter=2,
+                            wrap_idx=wrap, central=False)
+        assert _np(res["T_hist"][b, :nh[b]]).tolist() == o["T_hist"], b
+        assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9, b
