@@ -69,3 +69,70 @@ def gather_curves(J, total: int, group=None):
     out = torch.empty((world * cap, N), dtype=J.dtype, device=J.device)
     dist.all_gather_into_tensor(out, packed, group=group)
     return torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
+
+
+def gather_columns(cols, total: int, group=None):
+    """All-gather per-problem columns (a list of equal-length 1-D tensors of this
+    rank's shard) into full [total] tensors, each returned in its own dtype.  One
+    collective: the columns travel packed as float64 (exact for the int32 fields)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        return list(cols)
+    sizes = [shard_bounds(total, r, world) for r in range(world)]
+    cap = max(hi - lo for lo, hi in sizes)
+    dev = cols[0].device
+    packed = torch.zeros((cap, len(cols)), dtype=torch.float64, device=dev)
+    for j, c in enumerate(cols):
+        packed[: c.numel(), j] = c.to(torch.float64)
+    out = torch.empty((world * cap, len(cols)), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, packed, group=group)
+    full = torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
+    return [full[:, j].to(c.dtype) for j, c in enumerate(cols)]
+
+
+def ilqr_timeopt_sharded(system, x0_all, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T_max: int,
+                         *, U_init=None, group=None, device=None, **kw):
+    """The device outer loop (solver.ilqr_timeopt_batch, either select method) over a
+    batch sharded across the ranks of a node: rank r solves the contiguous problems
+    shard_bounds(B, r, world) on its own GPU with no communication inside the loop,
+    then one all-gather collects every problem's (T*, final J, accepted iterations,
+    crashed).  x0_all [B, n] is the whole batch on every rank (a rank reads only its
+    rows); U_init, if given per problem ([B, N', m]), is sliced the same way.
+    Returns (full: dict of [B] tensors, local: this rank's ilqr_timeopt_batch result
+    or None for an empty shard, (lo, hi))."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from . import solver
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    x0_all = np.asarray(x0_all.cpu() if isinstance(x0_all, torch.Tensor) else x0_all,
+                        dtype=float)
+    if x0_all.ndim != 2:
+        raise ValueError("x0_all must be [B, n]")
+    total = x0_all.shape[0]
+    lo, hi = shard_bounds(total, rank, world)
+    dev = device or (torch.device("cuda", torch.cuda.current_device())
+                     if torch.cuda.is_available() else torch.device("cpu"))
+    local = None
+    if hi > lo:
+        ui = U_init
+        if ui is not None and np.ndim(ui) == 3 and np.shape(ui)[0] == total:
+            ui = ui[lo:hi]
+        local = solver.ilqr_timeopt_batch(system, x0_all[lo:hi], xg, u_ref, Q, R, Qf, w, N,
+                                          T_min, T_max, U_init=ui, device=dev, **kw)
+        nh = local["n_hist"].to(torch.int64)
+        last = (nh - 1).clamp(min=0)
+        J_last = local["J_hist"].gather(1, last[:, None])[:, 0]
+        J_last = torch.where(nh > 0, J_last, torch.full_like(J_last, float("nan")))
+        cols = [local["T_star"].to(torch.int32), J_last.to(torch.float64),
+                local["n_hist"].to(torch.int32), local["crashed"].to(torch.int32)]
+    else:  # an empty shard (more ranks than problems) still joins the collective
+        cols = [torch.zeros(0, dtype=torch.int32, device=dev),
+                torch.zeros(0, dtype=torch.float64, device=dev),
+                torch.zeros(0, dtype=torch.int32, device=dev),
+                torch.zeros(0, dtype=torch.int32, device=dev)]
+    T, J, nh, cr = gather_columns(cols, total, group)
+    return dict(T_star=T, J_star=J, n_hist=nh, crashed=cr), local, (lo, hi)
