@@ -2,7 +2,11 @@
 
 Run in the build container only (the reference tree is not on the GPU box):
 
-    cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/make_golden.py
+    cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/make_golden.py [FLAG]
+
+FLAG selects one group: --r2, --legacy, --traj, --lin, --ilqr (propagator outer loop),
+--ilqr-bf (ilqr_timeopt(method="bruteforce"), ilqr_bf_*.npz), --summary (the
+plots/summary.csv comparison runs, summary_*.npz); none runs the base groups.
 
 It imports the reference modules from /root/reference (read-only, no bytecode
 written) and stores inputs/outputs as .npz data files next to this script.
