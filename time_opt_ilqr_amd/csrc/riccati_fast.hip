@@ -386,10 +386,11 @@ __device__ __forceinline__ void st64(double v, __amdgpu_buffer_rsrc_t r, unsigne
 __device__ unsigned long long g_ricf_stamp[16];
 
 // EXP (developer builds, timing experiments only -- results are wrong): 1 drops
-// the stores, 2 the per-step LDS-DMA.  JC: the J-curve form (mode 1, the grid's y
-// index is the horizon, no K / k / V stores; RiccatiArgs::jc_J)
-template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool JC = false>
-__global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
+// the stores, 2 the per-step LDS-DMA.  JC: the J-curve form (mode 1 at horizon jl for
+// the whole wave, no K / k / V stores; RiccatiArgs::jc_J).  blk: the workgroup's
+// problem block.
+template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC>
+__device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long blk, int jl) {
   constexpr int S = NX, MM = MU;
   unsigned long long sec[12] = {};
   unsigned long long tprev = 0;
@@ -412,12 +413,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
 #pragma unroll 1
   for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = 0.0;
 
-  // J-curve form: workgroups [b * jc_tmax, (b+1) * jc_tmax) run problem block b at every
-  // horizon, longest first, so the re-reads of its A, B, x, u meet in the caches
-  const unsigned jtm = JC ? (unsigned)a.jc_tmax : 1u;
-  const int jc_h = (int)(blockIdx.x % jtm);
-  const long long wave_prob0 =
-      ((long long)(blockIdx.x / jtm) * kWavesPerBlock + w) * kProbPerWave;
+  const long long wave_prob0 = (blk * kWavesPerBlock + w) * kProbPerWave;
   const long long prob = wave_prob0 + g;
   const bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
@@ -472,7 +468,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   const double* Qp = a.Q + pb * a.q_bstride;
   const double* Rp = a.R + pb * a.r_bstride;
   const double* Qfp = a.Qf + pb * a.qf_bstride;
-  const int L = valid ? (JC ? a.jc_tmax - jc_h : a.horizon[pb]) : 0;
+  const int L = valid ? (JC ? jl : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
@@ -832,6 +828,24 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
   }
 }
 
+template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0>
+__global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
+  ric_body<MODE, WANTV, STAMP, EXP, false>(a, (long long)blockIdx.x, 0);
+}
+
+// The J-curve form: workgroups [b * P, (b+1) * P), P = ceil(jc_tmax / 2), run problem
+// block b; workgroup h sweeps horizon jc_tmax - h and then h + 1, so every wave runs
+// the same jc_tmax + 1 steps (11 % faster than one horizon per workgroup, longest
+// first) and a block's horizons sit in adjacent workgroups (its A, B, x, u re-reads
+// meet in the caches)
+__global__ __launch_bounds__(256, 1) void riccati_fast_jcurve_kernel(RiccatiArgs<double> a) {
+  const unsigned P = (unsigned)((a.jc_tmax + 1) / 2);
+  const int h = (int)(blockIdx.x % P);
+  const long long blk = (long long)(blockIdx.x / P);
+  ric_body<1, false, false, 0, true>(a, blk, a.jc_tmax - h);
+  if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true>(a, blk, h + 1);
+}
+
 template <int MODE, bool WANTV>
 hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
@@ -869,10 +883,10 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
   // (out-of-range store offsets start at 2 GiB)
   const long long NA = a.nalloc;
   if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0x7FFF0000ll) return hipErrorNotSupported;
-  if (a.jc_J) {  // the J-curve form: one launch, jc_tmax workgroups per problem block
+  if (a.jc_J) {  // the J-curve form: one launch, ceil(jc_tmax / 2) workgroups per block
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
-    hipLaunchKernelGGL((ricf::riccati_fast_kernel<1, false, false, 0, true>),
-                       dim3((unsigned)(blocks * a.jc_tmax)), dim3(256),
+    hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel,
+                       dim3((unsigned)(blocks * ((a.jc_tmax + 1) / 2))), dim3(256),
                        (size_t)kWavesPerBlock * ricf::WAVE_BYTES, stream, a);
     return hipGetLastError();
   }
