@@ -368,7 +368,7 @@ def _bruteforce_workload(args, world, lo, hi, dev):
         t, j = engine.select_horizon(J, t_min, N)
         return types.SimpleNamespace(t_star=t, j_star=j, J=J, status=st)
 
-    info = dict(kernel="riccati_fast_kernel<1,false,false,0,true> (J-curve form)", bound="fp64",
+    info = dict(kernel="riccati_fast_jcurve_kernel (J-curve form, horizon pairs)", bound="fp64",
                 flops=sum(riccati_flops(n, m, T, 1) for T in range(1, N + 1)),
                 bytes=8 * (N * (n * n + n * m + m) + (N + 1) * n) + 12 * N, executed=None,
                 t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
