@@ -106,7 +106,7 @@ struct RiccatiArgs {
   T* V0;   // [B][nalloc+1] or null
   int* status;  // [B]
   // J-curve form (hop_bruteforce_jcurve_*, solver.py:293-358): when jc_J is set, the
-  // generic kernel's workgroup x runs problem block x / jc_tmax at horizon
+  // generic J-curve kernel's workgroup x runs problem block x / jc_tmax at horizon
   // L = jc_tmax - x % jc_tmax, the exact-size kernel's workgroup x the pair of
   // horizons jc_tmax - h and h + 1 of block x / P (h = x % P, P = ceil(jc_tmax / 2));
   // one horizon per wave at a time, a block's horizons adjacent, longest first;

@@ -44,18 +44,14 @@ __device__ __forceinline__ void rload_row(const T* M, int rows, int cols, int c,
 // section stamps of the diagnostic instantiation (tools/stamps_riccati.py)
 __device__ unsigned long long g_ric_stamp[16];
 
-template <class T, int S, int MM, bool STAMP = false>
-__global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
+// One pass of problem block blk; JCK: the J-curve form at horizon jl for the whole wave.
+template <class T, int S, int MM, bool STAMP, bool JCK>
+__device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long blk, int jl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4, w = tid >> 6;
-  // J-curve form: workgroups [b * jc_tmax, (b+1) * jc_tmax) run problem block b at every
-  // horizon, longest first, so the re-reads of its A, B, x, u meet in the caches
-  const bool JC = a.jc_J != nullptr;
-  const unsigned jtm = JC ? (unsigned)a.jc_tmax : 1u;
-  const long long blk = (long long)(blockIdx.x / jtm);
-  const int jc_h = (int)(blockIdx.x % jtm);
+  constexpr bool JC = JCK;
   const long long prob = (blk * kWavesPerBlock + w) * kProbPerWave + g;
   const bool valid = prob < a.batch;
   const long long pb = valid ? prob : a.batch - 1;
@@ -81,7 +77,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   const T* Qp = a.Q + pb * a.q_bstride;
   const T* Rp = a.R + pb * a.r_bstride;
   const T* Qfp = a.Qf + pb * a.qf_bstride;
-  const int L = valid ? (JC ? a.jc_tmax - jc_h : a.horizon[pb]) : 0;
+  const int L = valid ? (JC ? jl : a.horizon[pb]) : 0;
   int Lw = L;
   Lw = max(Lw, __shfl_xor(Lw, 16));
   Lw = max(Lw, __shfl_xor(Lw, 32));
@@ -372,11 +368,34 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
   }
 }
 
+template <class T, int S, int MM, bool STAMP = false>
+__global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
+  riccati_body<T, S, MM, STAMP, false>(a, (long long)blockIdx.x, 0);
+}
+
+// The J-curve form: workgroups [b * jc_tmax, (b+1) * jc_tmax) run problem block b at
+// every horizon, longest first, so the re-reads of its A, B, x, u meet in the caches.
+// (Pairing horizons jc_tmax - h and h + 1 in one workgroup, as the exact-size kernel
+// does, measured 1.5x slower here: the two inlined passes double the live registers.)
+// A kernel of its own, so the single-pass modes compile without the J-curve branches
+// (measured 4-10 % faster on the generic shapes).
+template <class T, int S, int MM>
+__global__ __launch_bounds__(256, 1) void riccati_jcurve_kernel(RiccatiArgs<T> a) {
+  const unsigned tm = (unsigned)a.jc_tmax;
+  riccati_body<T, S, MM, false, true>(a, (long long)(blockIdx.x / tm),
+                                      a.jc_tmax - (int)(blockIdx.x % tm));
+}
+
 template <class T, int S, int MM>
 hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   const size_t lds = (size_t)2 * kProbPerBlock * kLdsTile * sizeof(T);
-  const dim3 grid((unsigned)(blocks * (a.jc_J ? a.jc_tmax : 1)));
+  if (a.jc_J) {
+    hipLaunchKernelGGL((riccati_jcurve_kernel<T, S, MM>),
+                       dim3((unsigned)(blocks * a.jc_tmax)), dim3(256), lds, stream, a);
+    return hipGetLastError();
+  }
+  const dim3 grid((unsigned)blocks);
 #ifdef HOP_DEV
   if (opt(HOP_OPT_STAMPS)) {  // diagnostic: section stamps (tools/stamps_riccati.py)
     hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), grid, dim3(256), lds, stream, a);
