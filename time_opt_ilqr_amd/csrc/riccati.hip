@@ -45,7 +45,7 @@ __device__ __forceinline__ void rload_row(const T* M, int rows, int cols, int c,
 __device__ unsigned long long g_ric_stamp[16];
 
 // One pass of problem block blk; JCK: the J-curve form at horizon jl for the whole wave.
-template <class T, int S, int MM, bool STAMP, bool JCK>
+template <class T, int S, int MM, bool STAMP, bool JCK, int MODE>
 __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long blk, int jl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
@@ -66,7 +66,8 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
   }
   wave_sync();
 
-  const int n = a.n, m = a.m, NA = a.nalloc, mode = a.mode;
+  const int n = a.n, m = a.m, NA = a.nalloc;
+  constexpr int mode = MODE;  // a.mode, as a template argument (each mode compiles alone)
   const long long nn = (long long)n * n, nm = (long long)n * m, mmx = (long long)m * m;
   const T* Ap = a.A + pb * NA * nn;
   const T* Bp = a.Bm + pb * NA * nm;
@@ -258,7 +259,7 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     T Qi[MM];
     stamp(3);
     bool solved = false;
-    if (mode == 0) {
+    if constexpr (mode == 0) {
 #pragma unroll
       for (int r = 0; r < MM; ++r) Qi[r] = T(0.5) * (Quu[r] + QuuT[r]) + ((c == r) ? lam0 : T(0));
       // the reference first checks cholesky(Quu_reg) (no jitter), then solves with jitter
@@ -296,7 +297,7 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     copy(Vn, Qxx);
     T vxn = qx;
     T v0n = v0;
-    if (mode == 0) {
+    if constexpr (mode == 0) {
       LaneDot<MM>::fma(vxn, qu, K);        // + K^T Qu
       LaneDot<MM>::fma(vxn, kv, Qux);      // + Qux^T k
       T qk = T(0);
@@ -368,9 +369,9 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
   }
 }
 
-template <class T, int S, int MM, bool STAMP = false>
+template <class T, int S, int MM, int MODE, bool STAMP = false>
 __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
-  riccati_body<T, S, MM, STAMP, false>(a, (long long)blockIdx.x, 0);
+  riccati_body<T, S, MM, STAMP, false, MODE>(a, (long long)blockIdx.x, 0);
 }
 
 // The J-curve form: workgroups [b * jc_tmax, (b+1) * jc_tmax) run problem block b at
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(256, 1) void riccati_kernel(RiccatiArgs<T> a) {
 template <class T, int S, int MM>
 __global__ __launch_bounds__(256, 1) void riccati_jcurve_kernel(RiccatiArgs<T> a) {
   const unsigned tm = (unsigned)a.jc_tmax;
-  riccati_body<T, S, MM, false, true>(a, (long long)(blockIdx.x / tm),
+  riccati_body<T, S, MM, false, true, 1>(a, (long long)(blockIdx.x / tm),
                                       a.jc_tmax - (int)(blockIdx.x % tm));
 }
 
@@ -398,11 +399,17 @@ hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   const dim3 grid((unsigned)blocks);
 #ifdef HOP_DEV
   if (opt(HOP_OPT_STAMPS)) {  // diagnostic: section stamps (tools/stamps_riccati.py)
-    hipLaunchKernelGGL((riccati_kernel<T, S, MM, true>), grid, dim3(256), lds, stream, a);
+    if (a.mode == 0)
+      hipLaunchKernelGGL((riccati_kernel<T, S, MM, 0, true>), grid, dim3(256), lds, stream, a);
+    else
+      hipLaunchKernelGGL((riccati_kernel<T, S, MM, 1, true>), grid, dim3(256), lds, stream, a);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL((riccati_kernel<T, S, MM>), grid, dim3(256), lds, stream, a);
+  if (a.mode == 0)
+    hipLaunchKernelGGL((riccati_kernel<T, S, MM, 0>), grid, dim3(256), lds, stream, a);
+  else
+    hipLaunchKernelGGL((riccati_kernel<T, S, MM, 1>), grid, dim3(256), lds, stream, a);
   return hipGetLastError();
 }
 
