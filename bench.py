@@ -379,7 +379,57 @@ WORKLOADS = {"lft": _lft_workload, "config3": _lft_workload, "config5": _config5
              "select_gains": _select_gains_workload, "bruteforce": _bruteforce_workload}
 
 
-def main():
+def _free_port():
+    import socket
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    return port
+
+
+def _self_launch(args, argv):
+    """`python bench.py --gpus N` with N > 1 and no torchrun environment: start one
+    rank per GPU through torch.distributed.run as a CHILD process (nothing in this
+    process has touched the GPU: torch.cuda.device_count() does not initialise it on
+    this image) and exit with its return code."""
+    import subprocess
+    if not args.dry_run:
+        import torch
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but only {have} HIP device(s) visible",
+                  file=sys.stderr, flush=True)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def _dry_workload(args, world, lo, hi, dev):
+    """--dry-run: the CPU stand-in for a rank's shard (no HIP), loaded from tests/
+    (it computes (T*, J*) with the oracle).  Only the gloo rehearsal of bench.py's
+    rank / shard / gather path uses it; the product path never does."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_bench_dry_standin", os.path.join(REPO, "tests", "bench_dry_standin.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.workload(args, world, lo, hi, dev)
+
+
+def args_with_batch(args, batch):
+    import copy
+    a = copy.copy(args)
+    a.batch = batch
+    return a
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -402,14 +452,33 @@ def main():
                     help="lft/config3: block layout (auto: tile64 for the config-3 small-s "
                          "shape, batch-major otherwise); config5: shape-bucketed (auto) or "
                          "padded to s=13")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo + CPU tensors + the oracle stand-in of tests/ (a "
+                         "rehearsal of the rank/shard/gather path, never a measurement)")
+    ap.add_argument("--dry-out", default=None,
+                    help="--dry-run: rank 0 writes the gathered (T*, J*) here (.npz)")
+    ap.add_argument("--no-anchor", action="store_true",
+                    help="N=1 lft: skip the config-4-shard anchor (32,768 problems)")
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+
+    from time_opt_ilqr_amd import distributed as hd
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and args.gpus > 1:
+        sys.exit(_self_launch(args, argv))
+    rank, world, local = hd.env_rank_world()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
-    from time_opt_ilqr_amd import build as hop_build
-    from time_opt_ilqr_amd import distributed as hd
-
-    rank, world, local = hd.env_rank_world()
+    dry = args.dry_run
+    if not dry and torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but {torch.cuda.device_count()} HIP device(s) visible",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     wl = args.workload
     # workload defaults (BASELINE.json configs)
     dflt = {"lft": (4096 if world == 1 else 32768, 13, 4, 100, "f64"),
@@ -417,6 +486,7 @@ def main():
             "config5": (16384, 13, 4, 128, "f32"),
             "select_gains": (4096, 13, 4, 100, "f64"),
             "bruteforce": (4096, 13, 4, 100, "f64")}[wl]
+    args.batch_given = args.batch
     args.batch = args.batch or dflt[0]
     args.s = args.s or dflt[1]
     args.m = args.m or dflt[2]
@@ -424,17 +494,39 @@ def main():
     args.dtype = args.dtype or dflt[4]
     if wl == "config3":
         args.t_min = min(args.t_min, 20)
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    if rank == 0:
-        hop_build.build(verbose=False)
+    if dry:
+        if world > 1:
+            dist.init_process_group("gloo")
+        dev = torch.device("cpu")
+    else:
+        if world > 1:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dev = torch.device("cuda", local if world > 1 else 0)
+        if rank == 0:
+            from time_opt_ilqr_amd import build as hop_build
+            hop_build.build(verbose=False)
     if world > 1:
         dist.barrier()
+
+    def sync():
+        if not dry:
+            torch.cuda.synchronize()
+
+    def event():
+        if dry:
+            class _Ev:  # wall clock stands in for HIP events in the rehearsal
+                def record(self):
+                    self.t = time.perf_counter()
+
+                def elapsed_time(self, other):
+                    return (other.t - self.t) * 1e3
+            return _Ev()
+        return torch.cuda.Event(enable_timing=True)
+
     Bn = args.batch
     lo, hi = hd.shard_bounds(Bn * world, rank, world)
-    launch, info = WORKLOADS[wl](args, world, lo, hi, dev)
+    launch, info = (_dry_workload if dry else WORKLOADS[wl])(args, world, lo, hi, dev)
     s, m, N = info["s"], info["m"], info["N"]
 
     def step():
@@ -442,6 +534,8 @@ def main():
         if world > 1:
             hd.gather_selection(r.t_star, r.j_star, Bn * world)
         return r
+
+    gathered = None
 
     # DVFS pre-warm: ~1 ms launches leave the chip below its steady clock for
     # the first ~30 launches (measured: 3 warm-up steps read 13 % slow), so spin
@@ -453,26 +547,25 @@ def main():
         for _ in range(8):  # local launches only: ranks may differ in count, no collective
             launch()
             prewarm += 1
-        torch.cuda.synchronize()
+        sync()
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     K = args.steps
     # HIP events on the stream the kernels are launched on (engine launches on
     # torch's current stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
+    ev = [(event(), event()) for _ in range(K)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(K):
         ev[i][0].record()
         r = launch()
         ev[i][1].record()
         if world > 1:
-            hd.gather_selection(r.t_star, r.j_star, Bn * world)
-    torch.cuda.synchronize()
+            gathered = hd.gather_selection(r.t_star, r.j_star, Bn * world)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -481,9 +574,52 @@ def main():
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
+    if gathered is None:
+        gathered = (r.t_star, r.j_star)
     status_ok = int(r.status.abs().sum().item()) == 0 and bool(torch.isfinite(r.J).all())
     if hasattr(r, "riccati_status"):
         status_ok = status_ok and int(r.riccati_status.abs().sum().item()) == 0
+    # every rank's shard must be clean, not only rank 0's
+    if world > 1:
+        ok = torch.tensor([0 if status_ok else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MAX)
+        status_ok = int(ok.item()) == 0
+    if dry:
+        if rank == 0 and args.dry_out:
+            import numpy as np
+            np.savez(args.dry_out, t_star=gathered[0].cpu().numpy(),
+                     j_star=gathered[1].cpu().numpy())
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "steps": K,
+                              "ms_per_step": elapsed / K * 1e3,
+                              "config": {"batch_per_gpu": Bn, "global_batch": Bn * world,
+                                         "parallelism": f"dp{world}"},
+                              "status_ok": status_ok}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # the config-4-shard anchor at N=1: the per-GPU batch of the N>1 lines (32,768),
+    # so a 1->N curve can compare equal per-GPU work (a side figure, not `value`)
+    anchor = None
+    if (rank == 0 and world == 1 and wl == "lft" and Bn != 32768 and not args.no_anchor
+            and args.batch_given is None):
+        launch_a, _ = WORKLOADS[wl](args_with_batch(args, 32768), 1, 0, 32768, dev)
+        for _ in range(3):
+            launch_a()
+        sync()
+        ka = max(3, K // 4)
+        ta = time.perf_counter()
+        for _ in range(ka):
+            launch_a()
+        sync()
+        ms_a = (time.perf_counter() - ta) / ka * 1e3
+        anchor = {"workload": "config 4 shard: LFT sweep + fused argmin (32,768 problems on "
+                  "one GPU, the per-GPU batch of the N>1 lines)", "batch_per_gpu": 32768,
+                  "steps": ka, "ms_per_step": ms_a, "value": 32768 / ms_a * 1e3,
+                  "unit": "sweeps/s"}
+        del launch_a
+        torch.cuda.empty_cache()
 
     # PCIe-inclusive side figure (never `value`): the step's inputs start in pinned
     # host memory and are copied H2D inside the timed region
@@ -595,6 +731,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d,
+            "config4_shard_anchor": anchor,
             "status_ok": status_ok,
         }
         print(json.dumps(line), flush=True)

@@ -365,11 +365,14 @@ def riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
                    reg_max_tries=12):
     """horizon_selection.py:97-212 -> (Vxx, Vx, V0, K, k), index i = t + S_right.
 
-    Raises FloatingPointError / LinAlgError where the reference does.
+    Raises FloatingPointError / LinAlgError where the reference does (the
+    finiteness checks of horizon_selection.py:138-139, 150-151, 172-173, 179-180,
+    188-189, 209-210).
     """
     n = X.shape[1]
     m = U.shape[1]
     Qf = terminal_weight(alpha, n)
+    fin = lambda a: bool(np.all(np.isfinite(a)))  # noqa: E731
     L = int(T_bar) + int(S_right)
     Vxx = [np.zeros((n, n)) for _ in range(L + 1)]
     Vx = [np.zeros(n) for _ in range(L + 1)]
@@ -398,15 +401,21 @@ def riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
             Qst = sym(Qst + np.asarray(cxx, dtype=np.float64))
         A = np.asarray(A_list[i], dtype=np.float64)
         B = np.asarray(B_list[i], dtype=np.float64)
+        if not (fin(A) and fin(B) and fin(Vx[i + 1]) and fin(Vxx[i + 1])):
+            raise FloatingPointError("non-finite A/B/V")
         Qx = lx + A.T @ Vx[i + 1]
         Qu = lu + B.T @ Vx[i + 1]
         Qxx = Qst + A.T @ Vxx[i + 1] @ A
         Quu = R + B.T @ Vxx[i + 1] @ B
         Qux = B.T @ Vxx[i + 1] @ A
+        if not (fin(Qx) and fin(Qu) and fin(Qxx) and fin(Quu) and fin(Qux)):
+            raise FloatingPointError("non-finite Q terms")
         lam = float(max(lm_lambda, 1e-12))
         sol = None
         for _ in range(int(reg_max_tries)):
             Quu_reg = sym(Quu) + lam * np.eye(m)
+            if not fin(Quu_reg):
+                raise FloatingPointError("non-finite Quu_reg")
             a, s1 = spd_solve(Quu_reg, Qu)
             b, s2 = spd_solve(Quu_reg, Qux)
             if a is not None and b is not None:
@@ -421,20 +430,100 @@ def riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
         Vxx[i] = sym(Qxx - Qux.T @ b)
         Vx[i] = Qx - Qux.T @ a
         V0[i] = l0 + V0[i + 1] - 0.5 * float(Qu @ a)
+        if not (fin(Vxx[i]) and fin(Vx[i]) and np.isfinite(V0[i])):
+            raise FloatingPointError("non-finite V")
     return Vxx, Vx, V0, K, kk
 
 
+def chol_solve_raise(A, B, jitter=JITTER0, max_tries=8):
+    """utils.py:96-120 exactly: FloatingPointError on a non-finite A or B, the
+    jitter ladder (a non-finite X counts as a failed try), LinAlgError at the end."""
+    A = sym(np.asarray(A, dtype=np.float64))
+    B = np.asarray(B, dtype=np.float64)
+    if not np.all(np.isfinite(A)):
+        raise FloatingPointError("Non-finite values in chol_solve(A)")
+    if not np.all(np.isfinite(B)):
+        raise FloatingPointError("Non-finite values in chol_solve(B)")
+    eye = np.eye(A.shape[0])
+    eps = float(jitter)
+    for _ in range(int(max_tries)):
+        try:
+            low = np.linalg.cholesky(A + eps * eye)
+            X = np.linalg.solve(low.T, np.linalg.solve(low, B))
+            if not np.all(np.isfinite(X)):
+                raise FloatingPointError
+            return X
+        except (np.linalg.LinAlgError, FloatingPointError):
+            eps *= 10.0
+    raise np.linalg.LinAlgError("chol_solve failed: matrix not PD")
+
+
+def chol_solve_legacy(A, B, jitter=JITTER0, max_tries=4):
+    """ilqr_propagator.py:33-43: 4 jitters (no finiteness checks), then the
+    least-squares solve of sym(A) (np.linalg.lstsq, rcond=None)."""
+    A = sym(np.asarray(A, dtype=np.float64))
+    eye = np.eye(A.shape[0])
+    eps = float(jitter)
+    for _ in range(int(max_tries)):
+        try:
+            low = np.linalg.cholesky(A + eps * eye)
+            return np.linalg.solve(low.T, np.linalg.solve(low, B)), 0
+        except np.linalg.LinAlgError:
+            eps *= 10.0
+    return np.linalg.lstsq(A, B, rcond=None)[0], ST_LU
+
+
 def bruteforce_J(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, w, T_max,
-                 lm_lambda=1e-6, wrap_idx=None, extra=None):
-    """solver.py:293-358: J[T-1] = V0 of a fresh Riccati sweep of length T."""
+                 lm_lambda=1e-6, wrap_idx=None, extra=None, legacy=False, want_status=False):
+    """solver.py:293-358: J[T-1] = V0[0] of a fresh Riccati sweep of length T.
+
+    Unlike value_expansions_and_gains_prefix it checks nothing itself: only its
+    chol_solve raises (non-finite Quu_reg / Qu / Qux, or no jitter factors), so a
+    non-finite e at t = 0, or a V_0 that overflows, just leaves inf/NaN in J.
+    legacy=True restates ilqr_propagator.py:426-454 instead: Vxx_T = alpha I,
+    Vx_T = alpha e_T, and the legacy chol_solve (4 jitters, then lstsq; it never
+    raises for finite data).  want_status: also return the per-horizon status
+    (ST_LU where the legacy lstsq ran)."""
+    n, m = X.shape[1], U.shape[1]
     J = np.zeros(int(T_max))
+    st = np.zeros(int(T_max), dtype=np.int32)
+    Qf = None if legacy else terminal_weight(alpha, n)
     for T in range(1, int(T_max) + 1):
-        _, _, V0, _, _ = riccati_expand(A_list, B_list, X, U, xg, u_ref, Q, R,
-                                         alpha, T, 0, lm_lambda=lm_lambda,
-                                         w_stage=w, wrap_idx=wrap_idx, extra=extra,
-                                         reg_max_tries=1)
-        J[T - 1] = V0[0]
-    return J
+        eT = wrap_angles(np.asarray(X[T] - xg, dtype=np.float64), wrap_idx).reshape(-1)
+        if legacy:
+            Vxx, Vx, V0 = float(alpha) * np.eye(n), float(alpha) * eT, 0.5 * float(alpha) * float(eT @ eT)
+        else:
+            Vxx, Vx, V0 = sym(Qf), Qf @ eT, 0.5 * float(eT @ (Qf @ eT))
+        for t in range(T - 1, -1, -1):
+            e = wrap_angles(np.asarray(X[t] - xg, dtype=np.float64), wrap_idx).reshape(-1)
+            du = np.atleast_1d(U[t] - u_ref).reshape(-1)
+            lx, lu = Q @ e, R @ du
+            l0 = 0.5 * float(e @ (Q @ e)) + 0.5 * float(du @ (R @ du)) + float(w)
+            Qst = Q
+            if extra is not None and not legacy:
+                c, cx, cxx = extra(X[t], U[t])
+                l0 += float(c)
+                lx = lx + np.asarray(cx, dtype=np.float64).reshape(-1)
+                Qst = sym(Qst + np.asarray(cxx, dtype=np.float64))
+            A, B = A_list[t], B_list[t]
+            Qx = lx + A.T @ Vx
+            Qu = lu + B.T @ Vx
+            Qxx = Qst + A.T @ Vxx @ A
+            Quu = R + B.T @ Vxx @ B
+            Qux = B.T @ Vxx @ A
+            Quu_reg = sym(Quu) + float(lm_lambda) * np.eye(m)
+            if legacy:
+                a, s1 = chol_solve_legacy(Quu_reg, Qu)
+                b, s2 = chol_solve_legacy(Quu_reg, Qux)
+                st[T - 1] |= s1 | s2
+            else:
+                a = chol_solve_raise(Quu_reg, Qu)
+                b = chol_solve_raise(Quu_reg, Qux)
+            Vxx = sym(Qxx - Qux.T @ b)
+            Vx = Qx - Qux.T @ a
+            V0 = l0 + V0 - 0.5 * float(Qu.T @ a)
+        J[T - 1] = float(V0)
+    return (J, st) if want_status else J
 
 
 # ---------------------------------------------------------------------------

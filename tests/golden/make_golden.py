@@ -4,7 +4,7 @@ Run in the build container only (the reference tree is not on the GPU box):
 
     cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/make_golden.py [FLAG]
 
-FLAG selects one group: --r2, --legacy, --traj, --lin, --ilqr (propagator outer loop),
+FLAG selects one group: --r3, --r2, --legacy, --traj, --lin, --ilqr (propagator outer loop),
 --ilqr-bf (ilqr_timeopt(method="bruteforce"), ilqr_bf_*.npz), --summary (the
 plots/summary.csv comparison runs, summary_*.npz); none runs the base groups.
 
@@ -692,6 +692,83 @@ def legacy_twin_cases(seed=9700):
     print("legacy_twin_cases:", sorted(d))
 
 
+def bruteforce_edge_cases(seed=9800):
+    """Round 3: where solver.py:293-358 raises and where it does not.  It checks
+    nothing itself -- only chol_solve raises (non-finite Quu_reg / Qu / Qux, or no
+    jitter factors) -- so a non-finite e at t = 0 or an overflowing V_0 leaves
+    inf/NaN in J without raising.  Shapes n=4/m=2 (generic kernel) and n=12/m=4
+    (the exact-size kernel); each case stores its perturbation, whether the
+    reference raised, and J when it did not."""
+    d = {}
+    for n, m, N in ((4, 2, 12), (12, 4, 12)):
+        tag = f"n{n}_m{m}"
+        cases = {"clean": None, "e0_nan": ("X", (0, 1), np.nan),
+                 "xT_huge": ("X", (5, 0), 1e160), "A0_inf": ("A", (0, 1, 1), np.inf),
+                 "du0_nan": ("U", (0, 0), np.nan), "x3_nan": ("X", (3, 2), np.nan)}
+        for name, pert in cases.items():
+            A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed, n, m, N)
+            arrs = {"A": A.copy(), "X": X.copy(), "U": U.copy()}
+            if pert is not None:
+                arrs[pert[0]][pert[1]] = pert[2]
+            raised = ""
+            J = np.full(N, np.nan)
+            try:
+                J = np.array(ref_solver.bruteforce_all_Jt_backward_expansion(
+                    list(arrs["A"]), list(B), arrs["X"], arrs["U"], xg, u_ref, Q, R, alpha,
+                    0.5, N))
+            except (FloatingPointError, np.linalg.LinAlgError) as e:
+                raised = type(e).__name__
+            k = f"{tag}_{name}"
+            d[f"{k}_A"], d[f"{k}_X"], d[f"{k}_U"] = arrs["A"], arrs["X"], arrs["U"]
+            d[f"{k}_raised"] = raised
+            d[f"{k}_J"] = J
+            print(f"bruteforce_edge {k}: raised={raised or '-'} J[:6]={J[:6]}")
+        d[f"{tag}_seed"] = seed
+    np.savez_compressed(os.path.join(HERE, "bruteforce_edge_cases.npz"), **d)
+
+
+def legacy_bruteforce_cases(seed=9850):
+    """Round 3: the legacy twin's brute force (ilqr_propagator.py:426-454) with its
+    chol_solve (ilqr_propagator.py:33-43: 4 jitters, then np.linalg.lstsq of
+    sym(A)).  Problem 0 has R = diag(-1, 1, ...): Quu_reg is indefinite at every
+    step, all 4 jitters fail and every solve is the least-squares one; problem 1
+    is clean (first try)."""
+    import ilqr_propagator as leg
+    d = {}
+    for n, m, N in ((4, 2, 10), (12, 4, 10)):
+        tag = f"n{n}_m{m}"
+        for i in range(2):
+            A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed + i, n, m, N)
+            if i == 0:
+                R = R.copy()
+                R[0, 0] = -1.0
+            calls = []
+            real = leg.np.linalg.lstsq
+
+            def spy(*a, **k):
+                calls.append(1)
+                return real(*a, **k)
+
+            leg.np.linalg.lstsq = spy
+            try:
+                J = leg.bruteforce_all_Jt_backward_expansion(list(A), list(B), X, U, xg, u_ref, Q,
+                                                             R, alpha, 0.5, N)
+            finally:
+                leg.np.linalg.lstsq = real
+            d[f"{tag}_p{i}_R"] = R
+            d[f"{tag}_p{i}_J"] = np.array(J)
+            d[f"{tag}_p{i}_lstsq_calls"] = len(calls)
+            print(f"legacy_bruteforce {tag} p{i}: lstsq calls {len(calls)} J[:4]={np.array(J)[:4]}")
+        d[f"{tag}_seed"] = seed
+    np.savez_compressed(os.path.join(HERE, "legacy_bruteforce_cases.npz"), **d)
+
+
+def main_r3():
+    np.seterr(all="ignore")
+    bruteforce_edge_cases()
+    legacy_bruteforce_cases()
+
+
 def main_r2():
     np.seterr(all="ignore")
     synthetic_lft_wide("s13_m4_N100", 13, 4, 100, 11000, 16, 40, 100)
@@ -706,7 +783,9 @@ def main_r2():
 
 
 if __name__ == "__main__":
-    if "--r2" in sys.argv:  # round-2 fixtures only
+    if "--r3" in sys.argv:  # round-3 fixtures only
+        main_r3()
+    elif "--r2" in sys.argv:  # round-2 fixtures only
         main_r2()
     elif "--legacy" in sys.argv:
         np.seterr(all="ignore")

@@ -631,3 +631,40 @@ def test_ilqr_batch_large_batch_spot_checks(dev):
                             wrap_idx=wrap, central=False)
         assert _np(res["T_hist"][b, :nh[b]]).tolist() == o["T_hist"], b
         assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9, b
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m", [(4, 2), (12, 4)])
+def test_bruteforce_jcurve_edge_cases_vs_reference(dev, golden_dir, n, m):
+    """Where solver.py:293-358 raises and where it does not (reference goldens,
+    bruteforce_edge_cases.npz): only its chol_solve raises, so a non-finite e at
+    t = 0 or an overflowing terminal V_0 leaves inf/NaN in J with a clean status,
+    while a non-finite A_0, du_0 or later state fails a horizon (the reference
+    raises out of the whole call).  n=4/m=2 runs the generic kernel, n=12/m=4 the
+    exact-size one."""
+    from time_opt_ilqr_amd import _lib, engine
+    from oracle import hop_oracle as orc
+    d = np.load(os.path.join(golden_dir, "bruteforce_edge_cases.npz"))
+    tag, N = f"n{n}_m{m}", 12
+    names = ("clean", "e0_nan", "xT_huge", "A0_inf", "du0_nan", "x3_nan")
+    _, B, _, _, xg, ur, Q, R, alpha = orc.synth_riccati_problem(int(d[f"{tag}_seed"]), n, m, N)
+    A = np.stack([d[f"{tag}_{k}_A"] for k in names])
+    X = np.stack([d[f"{tag}_{k}_X"] for k in names])
+    U = np.stack([d[f"{tag}_{k}_U"] for k in names])
+    Bb = np.stack([B] * len(names))
+    Qf = alpha * np.eye(n)
+    J, st = engine.bruteforce_jcurve(_t(A, dev), _t(Bb, dev), _t(X, dev), _t(U, dev), _t(xg, dev),
+                                     _t(ur, dev), _t(Q, dev), _t(R, dev), _t(Qf, dev), N,
+                                     lm_lambda=1e-6, w_stage=0.5)
+    J, st = _np(J), _np(st)
+    for b, k in enumerate(names):
+        raised = str(d[f"{tag}_{k}_raised"])
+        if raised:
+            assert (st[b] & _lib.ST_FAIL).any(), k
+        else:
+            ref = d[f"{tag}_{k}_J"]
+            assert (st[b] == 0).all(), (k, st[b])
+            assert np.array_equal(np.isfinite(J[b]), np.isfinite(ref)), (k, J[b], ref)
+            f = np.isfinite(ref)
+            if f.any():
+                assert np.max(np.abs(J[b][f] - ref[f]) / np.abs(ref[f])) <= 1e-9, k

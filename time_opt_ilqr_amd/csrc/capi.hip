@@ -209,8 +209,11 @@ int jcurve_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, i
   if (t_max < 1) return fail(HOP_E_ARG, "t_max < 1");
   // the reference slices A_list[:T] for T <= T_max (an IndexError past N)
   if (t_max > n_alloc) return fail(HOP_E_ARG, "t_max > n_alloc (reference IndexError)");
-  // one workgroup per (16-problem block, horizon): the 1-D grid must fit 32 bits
-  if ((batch + 15) / 16 * (int64_t)t_max > 0xFFFFFFFFll) return fail(HOP_E_SIZE, "batch * t_max too large");
+  // one 256-lane workgroup per (16-problem block, horizon): the dispatch limit is in
+  // work-items, so blocks * t_max * 256 must fit 32 bits (the generic kernel's grid;
+  // the exact-size kernel's horizon pairs use half of it)
+  if ((batch + 15) / 16 * (int64_t)t_max * 256 > 0xFFFFFFFFll)
+    return fail(HOP_E_SIZE, "batch * t_max too large for one launch");
   if ((wrap_mask >> n) != 0u) return fail(HOP_E_ARG, "wrap_mask names a state >= n");
   if (batch == 0) return HOP_OK;
   if (!A || !Bm || !X || !U || !xg || !u_ref || !Q || !R || !Qf || !J || !status)

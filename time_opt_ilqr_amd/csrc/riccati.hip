@@ -181,7 +181,10 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     if constexpr (!MERGE) copy(bcol, bcol_n);
     load_step(i > 0 ? i - 1 : 0);
     if (!__any(act)) continue;
-    const unsigned long long badm = __ballot(!(finite_val(e) && finite_val(du)));
+    // the brute-force curve (solver.py:326-356) checks nothing itself: only its
+    // chol_solve raises, so a non-finite e at t = 0 only feeds V_0 (inf/NaN in J)
+    const bool e_ok = (JC && i == 0) || finite_val(e);
+    const unsigned long long badm = __ballot(!(e_ok && finite_val(du)));
     const bool bad = ((badm >> (16 * g)) & 0xffffull) != 0ull;
 
     stamp(0);
@@ -316,9 +319,18 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     }
     stamp(6);
     symmetrize(Vn, tile, c);
-    bool vbad = !finite_val(vxn) || !finite_val(v0n);
+    // value_expansions (horizon_selection.py:209-210) raises on any non-finite V.
+    // The brute-force curve raises only through the next step's chol_solve: a
+    // non-finite Vxx / Vx fails there, a non-finite V_0 never does, and at t = 0
+    // nothing follows -- only chol_solve(Quu_reg, Qux) itself can raise (Qux).
+    bool vbad = !finite_val(vxn) || (!JC && !finite_val(v0n));
 #pragma unroll
     for (int r = 0; r < S; ++r) vbad = vbad || !finite_val(Vn[r]);
+    if (JC && i == 0) {
+      vbad = false;
+#pragma unroll
+      for (int r = 0; r < MM; ++r) vbad = vbad || !finite_val(Qux[r]);
+    }
     const unsigned long long vbm = __ballot(vbad && c < n);
     const bool vfail = act && (((vbm >> (16 * g)) & 0xffffull) != 0ull);
 

@@ -594,7 +594,10 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     double e = c < S ? xi - xg_c : 0.0;
     if (wrap_c) e = wrap_angle(e);
     const double du = c < MM ? ui - ur_c : 0.0;
-    const unsigned long long badm = __ballot(!(finite_val(e) && finite_val(du)));
+    // the brute-force curve (solver.py:326-356) checks nothing itself: only its
+    // chol_solve raises, so a non-finite e at t = 0 only feeds V_0 (inf/NaN in J)
+    const bool e_ok = (JC && i == 0) || finite_val(e);
+    const unsigned long long badm = __ballot(!(e_ok && finite_val(du)));
     const bool bad = ((badm >> (16 * g)) & 0xffffull) != 0ull;
 
     // lx = Q e, lu = R du (lanes < n / < m)
@@ -744,10 +747,18 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     stamp(9);
     lds_park12(Vn, twa);  // its transpose is read with the next step's image
     stamp(10);
-    // finiteness of the update: x * 0 is 0 for finite x, NaN otherwise
-    double z = __builtin_fma(vxn, 0.0, v0n * 0.0);
+    // finiteness of the update: x * 0 is 0 for finite x, NaN otherwise.
+    // value_expansions (horizon_selection.py:209-210) raises on any non-finite V;
+    // the brute-force curve only through the next step's chol_solve (Vxx, Vx: never
+    // V_0), and at t = 0 only through chol_solve(Quu_reg, Qux) itself
+    double z = __builtin_fma(vxn, 0.0, JC ? 0.0 : v0n * 0.0);
 #pragma unroll
     for (int r = 0; r < S; ++r) z = __builtin_fma(Vn[r], 0.0, z);
+    if (JC && i == 0) {
+      z = 0.0;
+#pragma unroll
+      for (int r = 0; r < MM; ++r) z = __builtin_fma(Qux[r], 0.0, z);
+    }
     const unsigned long long vbm = __ballot(!(z == z) && c < S);
     const bool vfail = act && (((vbm >> (16 * g)) & 0xffffull) != 0ull);
     const bool commit = act && !fail_row && !vfail;

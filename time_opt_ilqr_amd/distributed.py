@@ -61,7 +61,13 @@ def gather_curves(J, total: int, group=None):
     world = dist.get_world_size(group)
     if world == 1:
         return J
-    N = J.shape[1] if J.dim() == 2 else 0
+    # every rank must pack the same width: an empty shard may hold a [0] tensor, so
+    # the curve length is agreed on by one max all-reduce first
+    n_loc = torch.tensor([J.shape[1] if J.dim() == 2 else 0], dtype=torch.int64, device=J.device)
+    dist.all_reduce(n_loc, op=dist.ReduceOp.MAX, group=group)
+    N = int(n_loc.item())
+    if J.dim() != 2:
+        J = J.reshape(0, N)
     sizes = [shard_bounds(total, r, world) for r in range(world)]
     cap = max(hi - lo for lo, hi in sizes)
     packed = torch.full((cap, N), float("nan"), dtype=J.dtype, device=J.device)
@@ -99,7 +105,9 @@ def ilqr_timeopt_sharded(system, x0_all, xg, u_ref, Q, R, Qf, w, N: int, T_min: 
     shard_bounds(B, r, world) on its own GPU with no communication inside the loop,
     then one all-gather collects every problem's (T*, final J, accepted iterations,
     crashed).  x0_all [B, n] is the whole batch on every rank (a rank reads only its
-    rows); U_init, if given per problem ([B, N', m]), is sliced the same way.
+    rows); per-problem inputs -- U_init [B, N', m], xg [B, n], u_ref [B, m], Q [B, n, n]
+    (the batch shapes ilqr_timeopt_batch accepts) -- are sliced the same way; shared
+    ones ([N', m], [n], [m], [n, n]) pass through whole.
     Returns (full: dict of [B] tensors, local: this rank's ilqr_timeopt_batch result
     or None for an empty shard, (lo, hi))."""
     import numpy as np
@@ -116,12 +124,20 @@ def ilqr_timeopt_sharded(system, x0_all, xg, u_ref, Q, R, Qf, w, N: int, T_min: 
     lo, hi = shard_bounds(total, rank, world)
     dev = device or (torch.device("cuda", torch.cuda.current_device())
                      if torch.cuda.is_available() else torch.device("cpu"))
+    def shard(a, batch_ndim, name):
+        """rows [lo, hi) of a per-problem input (leading dim == total), else a shared one"""
+        if a is None or np.ndim(a) < batch_ndim:
+            return a
+        if np.ndim(a) > batch_ndim or np.shape(a)[0] != total:
+            raise ValueError(f"{name}: per-problem inputs need the leading dimension B={total} "
+                             f"(got shape {tuple(np.shape(a))})")
+        return a[lo:hi]
+
+    ui = shard(U_init, 3, "U_init")
+    xg_r, ur_r, Q_r = shard(xg, 2, "xg"), shard(u_ref, 2, "u_ref"), shard(Q, 3, "Q")
     local = None
     if hi > lo:
-        ui = U_init
-        if ui is not None and np.ndim(ui) == 3 and np.shape(ui)[0] == total:
-            ui = ui[lo:hi]
-        local = solver.ilqr_timeopt_batch(system, x0_all[lo:hi], xg, u_ref, Q, R, Qf, w, N,
+        local = solver.ilqr_timeopt_batch(system, x0_all[lo:hi], xg_r, ur_r, Q_r, R, Qf, w, N,
                                           T_min, T_max, U_init=ui, device=dev, **kw)
         nh = local["n_hist"].to(torch.int64)
         last = (nh - 1).clamp(min=0)

@@ -243,8 +243,13 @@ def mixed_plan(order, n_groups: int, device) -> MixedPlan:
     """order[i] = group of batch slot i; slot i takes the next unused member of
     its group (the convention of packing.pack_mixed)."""
     torch = _torch()
-    order = torch.as_tensor(order, dtype=torch.int64).cpu()
+    order = torch.as_tensor(order, dtype=torch.int64).cpu().reshape(-1)
+    if order.numel() and (int(order.min()) < 0 or int(order.max()) >= n_groups):
+        raise ValueError(f"mixed_plan: group ids must lie in [0, {n_groups}) "
+                         f"(got {int(order.min())}..{int(order.max())})")
     slots = [torch.nonzero(order == g).reshape(-1).to(device) for g in range(n_groups)]
+    if sum(int(sl.numel()) for sl in slots) != order.numel():  # every slot in one group
+        raise ValueError("mixed_plan: the groups' slots do not cover the batch")
     return MixedPlan(slots, int(order.numel()))
 
 
