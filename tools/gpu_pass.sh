@@ -13,4 +13,7 @@ timeout -k 10 300 python bench.py --workload config5 --no-cpu-baseline > $OUT/be
 timeout -k 10 300 python bench.py --workload select_gains --no-cpu-baseline > $OUT/bench_sg.json 2> $OUT/bench_sg.err && \
 timeout -k 10 300 python bench.py --batch 32768 --no-cpu-baseline > $OUT/bench_c4shard.json 2> $OUT/bench_c4shard.err && \
 timeout -k 10 300 python bench.py --workload bruteforce --steps 5 > $OUT/bench_bf.json 2> $OUT/bench_bf.err
-echo "gpu_pass rc=$?"
+rc=$?; echo "gpu_pass rc=$rc"
+# a 1-GPU box must refuse --gpus 2 (exit 2) instead of timing one rank
+timeout -k 10 120 python bench.py --gpus 2 --no-cpu-baseline > $OUT/bench_gpus2.out 2> $OUT/bench_gpus2.err; echo "gpus2 rc=$?" >> $OUT/bench_gpus2.err
+exit $rc
