@@ -272,7 +272,8 @@ def test_sweep_blocks_with_lds_reads_emulated(block):
     assert np.abs(out[1][:n, :n] - want).max() < 1e-12
 
 
-@pytest.mark.parametrize("n,block", [(3, "CondLdl"), (13, "CondLdl"), (13, "CondLdlN")])
+@pytest.mark.parametrize("n,block", [(3, "CondLdl"), (13, "CondLdl"), (13, "CondLdlN"),
+                                     (13, "CondLdl2")])
 def test_cond_ldl_block_emulated(n, block):
     """CondLdl<n> (the conditioned-prefix update of SchedCond): from the offset-form
     S - I and Psi = [Sigma | m] (m on lane n), stream Sigma' = Sigma - Sigma S^-1 Sigma,
@@ -296,6 +297,8 @@ def test_cond_ldl_block_emulated(n, block):
         col[:n] = S[i]
         if block == "CondLdl":  # offset form; CondLdlN takes S itself
             col[i] -= 1.0
+        elif block == "CondLdl2":  # the SYM2 kernel's offset 2
+            col[i] -= 2.0
         regs[i] = col
         for base in (n, 2 * n):
             col = np.zeros(16)
@@ -636,3 +639,47 @@ def test_bench_bruteforce_counts_and_cpu_worker():
         _, _, V0, _, _ = orc.riccati_expand(list(A), list(Bm), X, U, xg, ur, Q, R, Qf, T, 0,
                                             lm_lambda=1e-6, w_stage=0.5, reg_max_tries=1)
         assert J[T - 1] == V0[0]
+
+
+def test_predict_eps_block_emulated():
+    """PredictEps<13> (the SYM2 conditioned kernel's predict): T = [Sigma' | m'] A~^T
+    with A~^T's row 13 = e_13, the eps I rows read from the zero-padded LDS vector
+    (lane c, row I: element 15 + I - c), then X = eps I + A T -- so lanes 0..12 hold
+    eps I + A Sigma' A^T and lane 13 holds A m'."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    n = 13
+    rng = np.random.default_rng(77)
+    Sg = rng.standard_normal((n, n))
+    Sg = Sg @ Sg.T
+    mp = rng.standard_normal(n)
+    A = np.eye(n) + 0.1 * rng.standard_normal((n, n))
+    regs = {}
+    for i in range(n):
+        x = np.zeros(16)
+        x[:n] = Sg[i]
+        x[n] = mp[i]
+        x[n + 1:] = 7.0  # lanes > 13 are don't-care in the kernel
+        regs[i] = x
+        regs[n + i] = np.full(16, np.nan)  # T: outputs
+        at = np.zeros(16)
+        at[:n] = A[:, i]  # at[j] on lane c = A[c][j] (column j of A)
+        regs[2 * n + i] = at
+        ar = np.zeros(16)
+        ar[:n] = A[i]  # ar[i] on lane j = A[i][j]
+        regs[3 * n + 1 + i] = ar
+    es = np.zeros(16)
+    es[n] = 1.0
+    regs[3 * n] = es  # at[13] = e_13
+    base = 4096
+    lds = np.full(8192 // 8, np.nan)
+    lds[base // 8: base // 8 + 32] = 0.0
+    lds[base // 8 + 15] = 1e-9
+    regs[4 * n + 1] = base + 8.0 * (15 - np.arange(16))
+    E.run(E.extract(inc, "PredictEps", n), regs, lds=lds)
+    X = np.array([regs[i] for i in range(n)])
+    want = 1e-9 * np.eye(n) + A @ Sg @ A.T
+    assert np.abs(X[:, :n] - want).max() <= 1e-13 * np.abs(want).max()
+    assert np.abs(X[:, n] - A @ mp).max() <= 1e-13 * np.abs(A @ mp).max()

@@ -131,6 +131,22 @@ constexpr bool has_ldspipe() {
 struct SchedCondLStamped : SchedCondL {
   static constexpr int STAMP = 1;
 };
+// SYM2: the stage / terminal inverses of the UNHALVED symmetric sums (M + M^T:
+// inverse (2M)^-1 = M^-1 / 2, exact), consumed as fma(-2, NE, X) by the update and
+// the query with their diagonal offset at 2 (no 0.5 multiplies); the update's
+// Newton step on the reciprocal (CondLdl2); and the predict as one block whose
+// eps I rows come from LDS instead of lane selects (PredictEps)
+struct SchedCondL2 : SchedCondL {
+  static constexpr int SYM2 = 1;
+};
+struct SchedCondL2Stamped : SchedCondL2 {
+  static constexpr int STAMP = 1;
+};
+template <class C>
+constexpr bool has_sym2() {
+  if constexpr (requires { C::SYM2; }) return C::SYM2 != 0;
+  return false;
+}
 
 template <class C>
 constexpr bool has_arow() {
@@ -1197,7 +1213,7 @@ __device__ __forceinline__ void sym_from_z(const double* img, unsigned zaddr, in
   double t[S];
   LdsSym<S, S>::run(bc, br, r, t);
 #pragma unroll
-  for (int i = 0; i < S; ++i) r[i] = 0.5 * (r[i] + t[i]);
+  for (int i = 0; i < S; ++i) r[i] = has_sym2<C>() ? r[i] + t[i] : 0.5 * (r[i] + t[i]);
 }
 
 // Trajectory form of the conditioned-prefix kernel (SchedCondTraj): the
@@ -1341,6 +1357,16 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
   const unsigned zaddr = wlds + G::OFF_T;
 #pragma unroll 1
   for (int i = lane; i < S * S + 8; i += 64) zarea[i] = 0.0;
+  // SYM2: eps I rows for the predict, read as element 15 + I - c of a zero-padded
+  // vector holding eps at element 15 (after the zero area)
+  constexpr int EPSV = 192;  // doubles from the zero area's start
+  static_assert(G::TILE_W >= 8 * (EPSV + 32), "eps vector in the tile slot");
+  if constexpr (has_sym2<C>()) {
+    if (lane < 32) zarea[EPSV + lane] = lane == 15 ? 1e-9 : 0.0;
+  }
+  const unsigned eps_addr = zaddr + 8u * (EPSV + 15 - c);
+  constexpr double DOFF = has_sym2<C>() ? 1e-9 - 0.5 : 1e-9 - 1.0;  // image diagonal offset
+  constexpr double KOFF = has_sym2<C>() ? 2.0 : 1.0;  // update / query diagonal offset
   const T* imQ = reinterpret_cast<const T*>(wbase + G::OFF_Q + g * G::IMGM);
   const T* imA = reinterpret_cast<const T*>(wbase + G::OFF_A + g * G::IMGM);
   const T* imT = reinterpret_cast<const T*>(wbase + G::OFF_QT + g * G::IMGM);
@@ -1474,8 +1500,8 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
       const double* sR = reinterpret_cast<const double*>(wbase + G::OFF_B) + g * 2 * G::CHR;
       atil = tb.step(a, c, sX, sV, sU, sR, const_cast<double*>(imQ), const_cast<double*>(imT));
     } else {
-      diag_add<S, S>(imQ, c, 1e-9 - 1.0);
-      diag_add<S, S>(imT, c, 1e-9 - 1.0);
+      diag_add<S, S>(imQ, c, DOFF);
+      diag_add<S, S>(imT, c, DOFF);
     }
     // ---- NE = -(Q_k + eps I)^-1 + I, NX = -(QT_k + eps I)^-1 + I (first attempt only)
     double NE[S], NX[S];
@@ -1493,7 +1519,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
       double d1 = 1.0, d2 = 1.0;
       SweepQSym<S>::run(NE, d1, o, aq);
 #pragma unroll
-      for (int i = 0; i < S; ++i) NX[i] = 0.5 * (o[i] + o[S + i]);
+      for (int i = 0; i < S; ++i) NX[i] = has_sym2<C>() ? o[i] + o[S + i] : 0.5 * (o[i] + o[S + i]);
       double o2[2 * S + MM];
       const unsigned ab[3] = {in ? lds_addr(imA) + 8u * S * c : zaddr, lds_addr(imA) + 8u * c,
                               in ? lds_addr(imB) + 8u * MM * c : zaddr};
@@ -1568,11 +1594,16 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
       double r[S], Ht[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) {
-        r[i] = X[i] - NE[i];  // Sigma_eps + E_k - I (offset form)
-        Ht[i] = X[i];
+        // Sigma_eps + E_k - I (offset form); SYM2: NE = -E_k/2 + I, so - 2I
+        r[i] = has_sym2<C>() ? __builtin_fma(-2.0, NE[i], X[i]) : X[i] - NE[i];
+        if constexpr (has_sym2<C>())  // an opaque copy: X keeps its loop registers
+          asm("v_mov_b64 %0, %1" : "=v"(Ht[i]) : "v"(X[i]));
+        else
+          Ht[i] = X[i];
       }
       double dmin = 1.0;
-      CondLdl<S>::run(r, Ht, X, dmin);
+      if constexpr (has_sym2<C>()) CondLdl2<S>::run(r, Ht, X, dmin);
+      else CondLdl<S>::run(r, Ht, X, dmin);
       const double x = bcast<S - 1>(r[S - 1]);
       bad = bad || !(dmin > 0.0) || (x != x);
     }
@@ -1581,6 +1612,9 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     {
       double Tm[S];
       double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
+      if constexpr (has_sym2<C>()) {
+        PredictEps<S>::run(Xs, Tm, at, ar, eps_addr);  // eps I + A [Sigma' | m'] A~^T
+      } else {
       // T = [Sigma' | m'] A~^T; A~^T's row S is e_S, so its term is X masked to lane S
 #pragma unroll
       for (int i = 0; i < S; ++i) Tm[i] = X[i] * e_s;
@@ -1593,6 +1627,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
         double (&at13)[S] = reinterpret_cast<double (&)[S]>(at);
         gxty<C, false>(Xs, at13, Tm);  // + A T
       }
+      }
       double y[MM];
       zero(y);
       acc_xy<false, double, MM, MM>(y, rinv, brow);
@@ -1604,9 +1639,10 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     {
       double rq[S];
 #pragma unroll
-      for (int i = 0; i < S; ++i) rq[i] = X[i] - NX[i];
+      for (int i = 0; i < S; ++i)
+        rq[i] = has_sym2<C>() ? __builtin_fma(-2.0, NX[i], X[i]) : X[i] - NX[i];
       double acc = 0.0, dmin = 1.0;
-      ElimQ<S>::run(rq, acc, dmin, 1.0);
+      ElimQ<S>::run(rq, acc, dmin, KOFF);
       const double q = bcast<S>(acc);
       const double gam = bcast<S>(X[S]);
       bad = bad || !(dmin > 0.0) || (q != q);
@@ -1995,6 +2031,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return launch(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes, a);
     case 43:  // image reads not overlapped with the sweeps, no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCond, 13, 4>, bytes, a);
+    case 44:  // SYM2 conditioned kernel + rerun
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL2, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
+    case 45:  // SYM2 without the rerun launch
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL2, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
+    case 46:  // SYM2 stamps, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondL2Stamped, 13, 4>, bytes, a);
     case 41:  // conditioned kernel without the rerun launch (A/B timing of it alone)
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);

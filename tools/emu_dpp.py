@@ -23,10 +23,17 @@ def _val(tok, regs):
     return -v if neg else v
 
 
-def run(asm_lines, regs):
-    """regs: dict operand index -> np.array(16) (modified in place)."""
+def run(asm_lines, regs, lds=None):
+    """regs: dict operand index -> np.array(16) (modified in place).  lds: optional
+    float64 array addressed in bytes / 8; ds_read_b64 %d, %a offset:o then reads
+    lds[(a + o) / 8] per lane (without it, LDS reads are skipped: checked on the GPU)."""
     for line in asm_lines:
         line = line.split(" row_mask")[0].strip()
+        if line.startswith("ds_read_b64") and lds is not None:
+            m = re.match(r"ds_read_b64 %(\d+), %(\d+)(?: offset:(\d+))?", line)
+            addr = regs[int(m.group(2))].astype(np.int64) + int(m.group(3) or 0)
+            regs[int(m.group(1))] = lds[addr // 8].astype(float)
+            continue
         if not line or line.startswith(("s_nop", "s_waitcnt", "ds_read")):
             continue  # LDS reads riding in a block are checked on the GPU
         op, rest = line.split(None, 1)

@@ -50,7 +50,7 @@ def main():
                  torch.eye(m, device=dev, dtype=torch.float64), 5.0 * eye, 0.5)
         run = lambda: engine.propagate_traj(*targs)  # noqa: E731
     if args.cond:
-        args.variant = 42
+        args.variant = 42 if args.variant == 32 else args.variant  # 46: the SYM2 form
         NAMES[:8] = ["top wait (DMA of step k)", "J store + diag offsets", "Q/QT image reads (sym)",
                      "E/Xt sweeps", "A/B reads + DMA issue", "update (CondLdl)", "predict products",
                      "query (ElimQ)"]
