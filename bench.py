@@ -77,6 +77,22 @@ def cond_flops(N, s, m):
     return N * (29 * s ** 3 // 3 + 2 * s * m * m + 2 * s * s * m)
 
 
+def cf_flops(N, s, m):
+    """FLOPs the trajectory-form conditioned kernel (lft_cond_cf_kernel, closed-form
+    stage inverses) executes per sweep: cond_flops without the two per-step
+    Gauss-Jordan inverses (2 s^3), plus per step the three n x n mat-vecs (Qi q,
+    Q e, Pi e: 6 n^2) and the two rank-1 corrections of the closed forms (4 s^2),
+    and once per problem the two n x n inverses (Qs + eps I, P + eps I: 2 n^3)."""
+    n = s - 1
+    return N * (23 * s ** 3 // 3 + 2 * s * m * m + 2 * s * s * m + 6 * n * n + 4 * s * s) + 2 * n ** 3
+
+
+def small_flops(N, s, m):
+    """FLOPs the small-s kernel (lft_small_kernel, conditioned association, one
+    problem per lane) executes per sweep: the conditioned count at the true s."""
+    return cond_flops(N, s, m)
+
+
 def lft_bytes(N, s, m, w=8):
     """Algorithmic HBM bytes of one sweep."""
     return w * (N * (3 * s * s + s * m) + m * m + s + N)
@@ -255,7 +271,8 @@ def _lft_workload(args, world, lo, hi, dev):
         kname = kname[:-1] + (",LY=2 tile64>" if tiled else ",LY=1 batch-major>")
     w = 8 if args.dtype == "f64" else 4
     info = dict(kernel=kname, bound=bound, flops=lft_flops(N, s, m), bytes=lft_bytes(N, s, m, w),
-                executed=cond_flops(N, s, m) if kname.startswith("lft_cond") else None,
+                executed=(cond_flops(N, s, m) if kname.startswith("lft_cond") else
+                          small_flops(N, s, m) if kname.startswith("lft_small") else None),
                 t_min=t_min, t_max=t_max, s=s, m=m, N=N, host=host, alt=alt,
                 layout="tile64" if tiled else "batch-major")
     return launch, info
@@ -292,7 +309,8 @@ def _config5_workload(args, world, lo, hi, dev):
                  "lft_small_kernel<float,5,1,LY=2 tile64> (Segway/Cartpole, side stream)")
         alg_bytes = (lft_bytes(N, 13, 4, 4) + 2 * lft_bytes(N, 5, 1, 4)) // 3
         info = dict(kernel=kname, bound="fp64", flops=CONFIG5_ALG_FLOPS, bytes=alg_bytes,
-                    executed=None, t_min=t_min, t_max=N, s=13, m=4, N=N, host=None,
+                    executed=(cond_flops(N, 13, 4) + 2 * small_flops(N, 5, 1)) // 3,
+                    t_min=t_min, t_max=N, s=13, m=4, N=N, host=None,
                     alt=launch_padded, layout="shape-bucketed (true s; padded s=13 timed beside)")
         return launch, info
     info = dict(kernel="lft_cond_kernel<SchedCond,13,4,float>", bound="fp64",
@@ -332,9 +350,14 @@ def _select_gains_workload(args, world, lo, hi, dev):
         sel.riccati_status = ric.status
         return sel
 
+    # the Riccati gains run to each problem's T*, not to N: both counts take the
+    # batch's mean T* once the step has run (flops_fn / executed_fn)
     info = dict(kernel="lft_cond_cf_kernel<SchedCondTraj,13,4> + riccati_fast_kernel<0>",
                 bound="fp64", flops=lft_flops(N, n + 1, m) + riccati_flops(n, m, N),
-                bytes=8 * (N * (n * n + n * m + 2 * n + m) + n), executed=None,
+                bytes=8 * (N * (n * n + n * m + 2 * n + m) + n),
+                executed=cf_flops(N, n + 1, m) + riccati_flops(n, m, N),
+                flops_fn=lambda tbar: lft_flops(N, n + 1, m) + riccati_flops(n, m, 1) * tbar,
+                executed_fn=lambda tbar: cf_flops(N, n + 1, m) + riccati_flops(n, m, 1) * tbar,
                 t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
     return launch, info
 
@@ -368,9 +391,10 @@ def _bruteforce_workload(args, world, lo, hi, dev):
         t, j = engine.select_horizon(J, t_min, N)
         return types.SimpleNamespace(t_star=t, j_star=j, J=J, status=st)
 
+    bf = sum(riccati_flops(n, m, T, 1) for T in range(1, N + 1))
     info = dict(kernel="riccati_fast_jcurve_kernel (J-curve form, horizon pairs)", bound="fp64",
-                flops=sum(riccati_flops(n, m, T, 1) for T in range(1, N + 1)),
-                bytes=8 * (N * (n * n + n * m + m) + (N + 1) * n) + 12 * N, executed=None,
+                flops=bf, bytes=8 * (N * (n * n + n * m + m) + (N + 1) * n) + 12 * N,
+                executed=bf,  # the J-curve steps are mode-1 steps: the counted arithmetic
                 t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
     return launch, info
 
@@ -457,6 +481,8 @@ def main(argv=None):
                          "rehearsal of the rank/shard/gather path, never a measurement)")
     ap.add_argument("--dry-out", default=None,
                     help="--dry-run: rank 0 writes the gathered (T*, J*) here (.npz)")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip the side timing of the other layout (profiling passes)")
     ap.add_argument("--no-anchor", action="store_true",
                     help="N=1 lft: skip the config-4-shard anchor (32,768 problems)")
     args = ap.parse_args(argv)
@@ -576,6 +602,10 @@ def main(argv=None):
         elapsed, kern_ms = float(t[0]), float(t[1])
     if gathered is None:
         gathered = (r.t_star, r.j_star)
+    if "flops_fn" in info:  # counts that depend on the selected horizons (mean T*)
+        tbar = float(r.t_star.double().mean().item()) if r.t_star.numel() else 0.0
+        info["flops"], info["executed"] = info["flops_fn"](tbar), info["executed_fn"](tbar)
+        info["t_star_mean"] = tbar
     status_ok = int(r.status.abs().sum().item()) == 0 and bool(torch.isfinite(r.J).all())
     if hasattr(r, "riccati_status"):
         status_ok = status_ok and int(r.riccati_status.abs().sum().item()) == 0
@@ -644,7 +674,7 @@ def main(argv=None):
 
     # side figure: the same sweep on batch-major blocks (tile64 runs only)
     alt_ms = None
-    if rank == 0 and info.get("alt") is not None:
+    if rank == 0 and info.get("alt") is not None and not args.no_alt:
         ea = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(5)]
         info["alt"]()
@@ -684,10 +714,17 @@ def main(argv=None):
                 "frac": achieved / peak, "traffic": traffic, "kernel": info["kernel"],
                 "kernel_ms": kern_ms, "flops_per_sweep": info["flops"],
                 "alg_bytes_per_sweep": info["bytes"]}
-        if info["executed"]:
+        if info["executed"] and info["bound"] != "hbm":
             ex = info["executed"] * per_launch / (kern_ms * 1e-3) / 1e12
             roof.update(executed_flops_per_sweep=info["executed"], executed_tflops=ex,
                         executed_frac=ex / peak)
+        elif info["executed"]:  # HBM-bound: the executed arithmetic beside the byte roofline
+            ex = info["executed"] * per_launch / (kern_ms * 1e-3) / 1e12
+            pk = PEAK_F32_TFLOPS if args.dtype == "f32" else PEAK_F64_TFLOPS
+            roof.update(executed_flops_per_sweep=info["executed"], executed_tflops=ex,
+                        executed_frac_of_compute_peak=ex / pk)
+        if "t_star_mean" in info:
+            roof["t_star_mean"] = info["t_star_mean"]
         if args.dtype == "f32" and info["bound"] == "fp64":
             roof["arithmetic"] = "f64 (fp32 blocks in HBM/LDS)"
         if info["bound"] != "hbm":

@@ -1,6 +1,9 @@
 """Write profiles/traffic.json from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
-    python tools/make_traffic.py <prof_dir> <key> [kernel_substring]
+    python tools/make_traffic.py <prof_dir> <key> [kernel_substring[,substring...]]
+
+Several substrings (a step of more than one kernel: select + gains, the config-5
+buckets, J curve + argmin) sum their per-launch means: the traffic of one step.
 
 HBM bytes per launch = 2 x FETCH_SIZE (gfx950 tallies a 16-B/lane streaming read's
 128-B requests at 64 B: MI355X_MICROARCH.md, HBM section) + WRITE_SIZE, both
@@ -29,14 +32,21 @@ def mean_counter(root, name, pat):
 
 def main():
     root, key = sys.argv[1], sys.argv[2]
-    pat = sys.argv[3] if len(sys.argv) > 3 else "lft_sweep_v2_kernel"
-    fetch, nf = mean_counter(root, "FETCH_SIZE", pat)
-    write, nw = mean_counter(root, "WRITE_SIZE", pat)
+    pats = (sys.argv[3] if len(sys.argv) > 3 else "lft_sweep_v2_kernel").split(",")
+    fetch = write = 0.0
+    nf, nw = [], []
+    for pat in pats:
+        f_, n1 = mean_counter(root, "FETCH_SIZE", pat)
+        w_, n2 = mean_counter(root, "WRITE_SIZE", pat)
+        fetch, write = fetch + f_, write + w_
+        nf.append(n1)
+        nw.append(n2)
     hbm = 2.0 * fetch * 1024 + write * 1024
     path = os.path.join(REPO, "profiles", "traffic.json")
     tj = json.load(open(path)) if os.path.exists(path) else {}
     tj[key] = {"hbm_bytes_per_launch": hbm, "fetch_size_kib": fetch, "write_size_kib": write,
-               "dispatches": [nf, nw], "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950)",
+               "dispatches": [nf, nw], "kernels": pats,
+               "correction": "2 x FETCH_SIZE + WRITE_SIZE (gfx950)",
                "source": os.path.relpath(root, REPO)}
     os.makedirs(os.path.dirname(path), exist_ok=True)
     json.dump(tj, open(path, "w"), indent=1, sort_keys=True)
