@@ -137,14 +137,48 @@ struct SchedCondLStamped : SchedCondL {
 // Newton step on the reciprocal (CondLdl2); and the predict as one block whose
 // eps I rows come from LDS instead of lane selects (PredictEps)
 struct SchedCondL2 : SchedCondL {
-  static constexpr int SYM2 = 1;
+  static constexpr int SYM2 = 1, NEWT = 1, PEPS = 1;
 };
 struct SchedCondL2Stamped : SchedCondL2 {
   static constexpr int STAMP = 1;
 };
+// the three parts of SchedCondL2 alone (developer A/B)
+struct SchedCondLSym : SchedCondL {
+  static constexpr int SYM2 = 1, NEWT = 0, PEPS = 0;
+};
+struct SchedCondLNewt : SchedCondL {
+  static constexpr int SYM2 = 0, NEWT = 1, PEPS = 0;
+};
+struct SchedCondLPeps : SchedCondL {
+  static constexpr int SYM2 = 0, NEWT = 0, PEPS = 1;
+};
+// DMA placement A/B: DSTAG 1 = odd waves issue the step's pieces after the update
+// (the CU's waves no longer burst together); 2 = Q/QT pieces after the E sweep
+// (their images are read by then), A/B after the X sweep
+struct SchedCondLStag1 : SchedCondL {
+  static constexpr int DSTAG = 1;
+};
+struct SchedCondLStag2 : SchedCondL {
+  static constexpr int DSTAG = 2;
+};
+template <class C>
+constexpr int dstag() {
+  if constexpr (requires { C::DSTAG; }) return C::DSTAG;
+  return 0;
+}
 template <class C>
 constexpr bool has_sym2() {
   if constexpr (requires { C::SYM2; }) return C::SYM2 != 0;
+  return false;
+}
+template <class C>
+constexpr bool has_newt() {
+  if constexpr (requires { C::NEWT; }) return C::NEWT != 0;
+  return false;
+}
+template <class C>
+constexpr bool has_peps() {
+  if constexpr (requires { C::PEPS; }) return C::PEPS != 0;
   return false;
 }
 
@@ -669,6 +703,57 @@ __device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsign
 #undef HOP_P
 }
 
+
+// The same 20 pieces in two groups (DSTAG 2): Q and QT (12) as soon as their
+// images are read, A and B (8) after the X sweep's reads
+template <int OQ, int OT>
+__device__ __forceinline__ void dma_stepQT(const unsigned (&vm)[6], __amdgpu_buffer_rsrc_t rQ,
+                                           __amdgpu_buffer_rsrc_t rT, unsigned wlds, unsigned soM) {
+  unsigned keep;
+#define HOP_P(R, V, OFF, SO)                                                  \
+  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
+  "], %[" #SO "] offen lds\n\t"
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %[keep], m0\n\t"
+      HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
+      HOP_P(rq, v3, %[q3], sm) HOP_P(rq, v4, %[q4], sm) HOP_P(rq, v5, %[q5], sm)
+      HOP_P(rt, v0, %[t0], sm) HOP_P(rt, v1, %[t1], sm) HOP_P(rt, v2, %[t2], sm)
+      HOP_P(rt, v3, %[t3], sm) HOP_P(rt, v4, %[t4], sm) HOP_P(rt, v5, %[t5], sm)
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [w] "s"(wlds), [sm] "s"(soM), [rq] "s"(rQ), [rt] "s"(rT), [v0] "v"(vm[0]),
+        [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]), [v4] "v"(vm[4]), [v5] "v"(vm[5]),
+        [q0] "i"(OQ), [q1] "i"(OQ + 1024), [q2] "i"(OQ + 2048), [q3] "i"(OQ + 3072),
+        [q4] "i"(OQ + 4096), [q5] "i"(OQ + 5120), [t0] "i"(OT), [t1] "i"(OT + 1024),
+        [t2] "i"(OT + 2048), [t3] "i"(OT + 3072), [t4] "i"(OT + 4096), [t5] "i"(OT + 5120)
+      : "memory", "scc");
+#undef HOP_P
+}
+template <int OA, int OB>
+__device__ __forceinline__ void dma_stepAB(const unsigned (&vm)[6], const unsigned (&vb)[2],
+                                           __amdgpu_buffer_rsrc_t rA, __amdgpu_buffer_rsrc_t rB,
+                                           unsigned wlds, unsigned soM, unsigned soB) {
+  unsigned keep;
+#define HOP_P(R, V, OFF, SO)                                                  \
+  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
+  "], %[" #SO "] offen lds\n\t"
+  asm volatile(
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_mov_b32 %[keep], m0\n\t"
+      HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
+      HOP_P(ra, v3, %[a3], sm) HOP_P(ra, v4, %[a4], sm) HOP_P(ra, v5, %[a5], sm)
+      HOP_P(rb, u0, %[b0], sb) HOP_P(rb, u1, %[b1], sb)
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep)
+      : [w] "s"(wlds), [sm] "s"(soM), [sb] "s"(soB), [ra] "s"(rA), [rb] "s"(rB),
+        [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]), [v4] "v"(vm[4]),
+        [v5] "v"(vm[5]), [u0] "v"(vb[0]), [u1] "v"(vb[1]), [a0] "i"(OA), [a1] "i"(OA + 1024),
+        [a2] "i"(OA + 2048), [a3] "i"(OA + 3072), [a4] "i"(OA + 4096), [a5] "i"(OA + 5120),
+        [b0] "i"(OB), [b1] "i"(OB + 1024)
+      : "memory", "scc");
+#undef HOP_P
+}
 
 template <int S, int MM, int ES = 8>  // ES: bytes per element of the streamed blocks
 struct Geo {
@@ -1361,7 +1446,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
   // vector holding eps at element 15 (after the zero area)
   constexpr int EPSV = 192;  // doubles from the zero area's start
   static_assert(G::TILE_W >= 8 * (EPSV + 32), "eps vector in the tile slot");
-  if constexpr (has_sym2<C>()) {
+  if constexpr (has_peps<C>()) {
     if (lane < 32) zarea[EPSV + lane] = lane == 15 ? 1e-9 : 0.0;
   }
   const unsigned eps_addr = zaddr + 8u * (EPSV + 15 - c);
@@ -1518,6 +1603,11 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
                               in ? lds_addr(imT) + 8u * S * c : zaddr};
       double d1 = 1.0, d2 = 1.0;
       SweepQSym<S>::run(NE, d1, o, aq);
+      if constexpr (dstag<C>() == 2) {  // the Q and QT images are read: refill them now
+        wave_sync();
+        if (k + 1 < N)
+          dma_stepQT<G::OFF_Q, G::OFF_QT>(voM, rQ, rT, wlds, (unsigned)((k + 1) * SS * ES));
+      }
 #pragma unroll
       for (int i = 0; i < S; ++i) NX[i] = has_sym2<C>() ? o[i] + o[S + i] : 0.5 * (o[i] + o[S + i]);
       double o2[2 * S + MM];
@@ -1586,8 +1676,16 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     }
     }
     at[S] = e_s;
-    wave_sync();
-    if (k + 1 < N) dma_step(k + 1);
+    const bool dma_late = dstag<C>() == 1 && (w & 1);
+    if constexpr (dstag<C>() == 2) {
+      wave_sync();
+      if (k + 1 < N)
+        dma_stepAB<G::OFF_A, G::OFF_B>(voM, voB, rA, rB, wlds, (unsigned)((k + 1) * SS * ES),
+                                       (unsigned)((k + 1) * SM * ES));
+    } else if (!dma_late) {
+      wave_sync();
+      if (k + 1 < N) dma_step(k + 1);
+    }
     stamp(4);
     // ---- update: condition the prefix on stage k's cost
     {
@@ -1596,23 +1694,29 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
       for (int i = 0; i < S; ++i) {
         // Sigma_eps + E_k - I (offset form); SYM2: NE = -E_k/2 + I, so - 2I
         r[i] = has_sym2<C>() ? __builtin_fma(-2.0, NE[i], X[i]) : X[i] - NE[i];
-        if constexpr (has_sym2<C>())  // an opaque copy: X keeps its loop registers
+        if constexpr (has_peps<C>())  // an opaque copy: X keeps its loop registers
           asm("v_mov_b64 %0, %1" : "=v"(Ht[i]) : "v"(X[i]));
         else
           Ht[i] = X[i];
       }
       double dmin = 1.0;
-      if constexpr (has_sym2<C>()) CondLdl2<S>::run(r, Ht, X, dmin);
+      if constexpr (has_sym2<C>() && has_newt<C>()) CondLdl2<S>::run(r, Ht, X, dmin);
+      else if constexpr (has_sym2<C>()) CondLdlO2R0<S>::run(r, Ht, X, dmin);
+      else if constexpr (has_newt<C>()) CondLdlO1R1<S>::run(r, Ht, X, dmin);
       else CondLdl<S>::run(r, Ht, X, dmin);
       const double x = bcast<S - 1>(r[S - 1]);
       bad = bad || !(dmin > 0.0) || (x != x);
+    }
+    if (dma_late) {  // DSTAG 1: the odd waves' pieces, half a step after the even waves'
+      wave_sync();
+      if (k + 1 < N) dma_step(k + 1);
     }
     stamp(5);
     // ---- predict: Sigma_{k+1} = A Sigma' A^T + B R^-1 B^T + eps I, m_{k+1} = A m'
     {
       double Tm[S];
       double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
-      if constexpr (has_sym2<C>()) {
+      if constexpr (has_peps<C>()) {
         PredictEps<S>::run(Xs, Tm, at, ar, eps_addr);  // eps I + A [Sigma' | m'] A~^T
       } else {
       // T = [Sigma' | m'] A~^T; A~^T's row S is e_S, so its term is X masked to lane S
@@ -2039,6 +2143,16 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
     case 46:  // SYM2 stamps, no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondL2Stamped, 13, 4>, bytes, a);
+    case 50:  // DMA: odd waves after the update, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLStag1, 13, 4>, bytes, a);
+    case 51:  // DMA: Q/QT after the E sweep, A/B after the X sweep, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLStag2, 13, 4>, bytes, a);
+    case 47:  // the unhalved sums alone, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>, bytes, a);
+    case 48:  // the update's Newton on the reciprocal alone, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLNewt, 13, 4>, bytes, a);
+    case 49:  // the one-block predict with LDS eps rows alone, no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLPeps, 13, 4>, bytes, a);
     case 41:  // conditioned kernel without the rerun launch (A/B timing of it alone)
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
