@@ -623,6 +623,7 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
                                       unsigned soff) {
   unsigned keep;
   asm volatile(
+      ".p2align 3\n\t"  // the 8-byte buffer_load at 0 mod 8 (code placement)
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
@@ -649,7 +650,9 @@ __device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsign
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
       "s_mov_b32 %[keep], m0\n\t"
+      "s_nop 0\n\t"
       HOP_P(ra, a0, %[o0], sa) HOP_P(ra, a1, %[o1], sa) HOP_P(ra, a2, %[o2], sa)
       HOP_P(ra, a3, %[o3], sa) HOP_P(ra, a4, %[o4], sa)
       HOP_P(rb, b0, %[p0], sb) HOP_P(rb, b1, %[p1], sb)
@@ -681,7 +684,9 @@ __device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsign
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
       "s_mov_b32 %[keep], m0\n\t"
+      "s_nop 0\n\t"
       HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
       HOP_P(rq, v3, %[q3], sm) HOP_P(rq, v4, %[q4], sm) HOP_P(rq, v5, %[q5], sm)
       HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
@@ -714,6 +719,7 @@ __device__ __forceinline__ void dma_stepQT(const unsigned (&vm)[6], __amdgpu_buf
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %[keep], m0\n\t"
       HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
@@ -739,6 +745,7 @@ __device__ __forceinline__ void dma_stepAB(const unsigned (&vm)[6], const unsign
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %[keep], m0\n\t"
       HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
