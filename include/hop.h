@@ -327,6 +327,39 @@ int hop_bruteforce_jcurve_f32(const float* A, const float* Bm, const float* X, c
                               void* stream);
 
 /*
+ * hop_riccati_legacy_f64 / hop_bruteforce_jcurve_legacy_f64
+ * The legacy twin's passes (ilqr_propagator.py): mode 0 replaces its
+ *   backward_pass_truncated (ilqr_propagator.py:375-400), mode 1 its
+ *   value_expansions_and_gains_prefix (ilqr_propagator.py:237-287), the J-curve
+ *   entry its bruteforce_all_Jt_backward_expansion (ilqr_propagator.py:426-454).
+ *   Every solve is the legacy chol_solve (ilqr_propagator.py:33-43): 4 jitters,
+ *   then np.linalg.lstsq of sym(Quu_reg) -- the minimum-norm pinv solve, marked
+ *   HOP_ST_LU -- instead of a failure; Quu_reg = _sym(Quu) + lm I (no floor, no
+ *   lambda ladder); no finiteness checks (NaN propagates; a non-finite Quu_reg
+ *   that reaches lstsq fails the row, as numpy's lstsq raises).  The terminal
+ *   weight is Qf = alpha I (the legacy passes take a scalar alpha).  Arguments as
+ *   hop_riccati_f64 / hop_bruteforce_jcurve_f64 without the extra stage cost and
+ *   reg_max_tries; m <= 11 (HOP_E_SIZE otherwise).
+ */
+int hop_riccati_legacy_f64(const double* A, const double* Bm, const double* X, const double* U,
+                           const double* xg, int64_t xg_batch_stride, const double* u_ref,
+                           int64_t u_ref_batch_stride, const double* Q, int64_t q_batch_stride,
+                           const double* R, int64_t r_batch_stride, const double* Qf,
+                           int64_t qf_batch_stride, const int32_t* horizon, const double* lm,
+                           double w_stage, uint32_t wrap_mask, int32_t mode, int64_t batch,
+                           int32_t n_alloc, int32_t n, int32_t m, double* K, double* k,
+                           double* Vxx, double* Vx, double* V0, int32_t* status, void* stream);
+int hop_bruteforce_jcurve_legacy_f64(const double* A, const double* Bm, const double* X,
+                                     const double* U, const double* xg, int64_t xg_batch_stride,
+                                     const double* u_ref, int64_t u_ref_batch_stride,
+                                     const double* Q, int64_t q_batch_stride, const double* R,
+                                     int64_t r_batch_stride, const double* Qf,
+                                     int64_t qf_batch_stride, double lm_lambda, double w_stage,
+                                     uint32_t wrap_mask, int64_t batch, int32_t n_alloc,
+                                     int32_t n, int32_t m, int32_t t_max, double* J,
+                                     int32_t* status, void* stream);
+
+/*
  * Batched dynamics and finite-difference linearisation.
  * System ids (the reference's systems.py makers, F discretised with the given dt):
  *   0 double integrator  make_double_integrator     systems.py:28-50    n=2,  m=1

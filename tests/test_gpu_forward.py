@@ -668,3 +668,36 @@ def test_bruteforce_jcurve_edge_cases_vs_reference(dev, golden_dir, n, m):
             f = np.isfinite(ref)
             if f.any():
                 assert np.max(np.abs(J[b][f] - ref[f]) / np.abs(ref[f])) <= 1e-9, k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m", [(4, 2), (12, 4)])
+def test_legacy_bruteforce_lstsq_vs_reference(dev, golden_dir, n, m):
+    """The legacy twin's brute force (ilqr_propagator.py:426-454) with its chol_solve
+    (ilqr_propagator.py:33-43: 4 jitters, then np.linalg.lstsq): problem 0's R[0,0] =
+    -1 makes Quu_reg indefinite, every such solve takes the least-squares fallback
+    (ST_LU) instead of failing; problem 1 is clean.  Reference goldens
+    legacy_bruteforce_cases.npz; the generic kernel runs both shapes."""
+    from time_opt_ilqr_amd import _lib, engine
+    from oracle import hop_oracle as orc
+    d = np.load(os.path.join(golden_dir, "legacy_bruteforce_cases.npz"))
+    tag, N = f"n{n}_m{m}", 10
+    for i in range(2):
+        A, B, X, U, xg, ur, Q, R, alpha = orc.synth_riccati_problem(int(d[f"{tag}_seed"]) + i, n,
+                                                                   m, N)
+        R = d[f"{tag}_p{i}_R"]
+        J, st = engine.bruteforce_jcurve(_t(A[None], dev), _t(B[None], dev), _t(X[None], dev),
+                                         _t(U[None], dev), _t(xg, dev), _t(ur, dev), _t(Q, dev),
+                                         _t(R, dev), _t(alpha * np.eye(n), dev), N,
+                                         lm_lambda=1e-6, w_stage=0.5, legacy=True)
+        J, st = _np(J)[0], _np(st)[0]
+        assert _rel(J, d[f"{tag}_p{i}_J"]) <= 1e-10, (i, J, d[f"{tag}_p{i}_J"])
+        assert not (st & _lib.ST_FAIL).any()
+        assert bool((st & _lib.ST_LU).any()) == (int(d[f"{tag}_p{i}_lstsq_calls"]) > 0)
+        if i == 0:  # the modern brute force raises there (chol_solve has no fallback)
+            Jm, sm = engine.bruteforce_jcurve(_t(A[None], dev), _t(B[None], dev),
+                                              _t(X[None], dev), _t(U[None], dev), _t(xg, dev),
+                                              _t(ur, dev), _t(Q, dev), _t(R, dev),
+                                              _t(alpha * np.eye(n), dev), N, lm_lambda=1e-6,
+                                              w_stage=0.5)
+            assert (_np(sm)[0] & _lib.ST_FAIL).any()

@@ -30,7 +30,7 @@ def _header_functions():
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 32
+    assert len(names) == 34
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:

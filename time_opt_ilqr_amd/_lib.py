@@ -40,6 +40,12 @@ _RIC32[19] = C.c_float
 # J-curve form: the 17 Riccati inputs, lm w wrap batch n_alloc n m t_max J status stream
 _JC64 = _RIC64[:17] + [C.c_double, C.c_double, _U32, _I64, _I32, _I32, _I32, _I32, _P, _P, _P]
 _JC32 = _RIC64[:17] + [C.c_float, C.c_float, _U32, _I64, _I32, _I32, _I32, _I32, _P, _P, _P]
+# the legacy twin's passes: A Bm X U, (xg u_ref Q R Qf) with batch strides, then
+# horizon lm w wrap mode batch n_alloc n m K k Vxx Vx V0 status stream / the J-curve tail
+_LEG_IN = [_P, _P, _P, _P] + [_P, _I64] * 5
+_RICLEG = _LEG_IN + [_P, _P, C.c_double, _U32, _I32, _I64, _I32, _I32, _I32, _P, _P, _P, _P, _P,
+                     _P, _P]
+_JCLEG = _LEG_IN + [C.c_double, C.c_double, _U32, _I64, _I32, _I32, _I32, _I32, _P, _P, _P]
 # trajectory-form inputs shared by hop_augment_* and hop_lft_sweep_traj_*:
 # A Bm a_res X U xg xg_bs u_ref ur_bs Q q_bs P p_bs w w_bs qxx qx c wrap q_reg rho_reg
 _TRJ64 = [_P, _P, _P, _P, _P, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _P, _P, _U32,
@@ -74,6 +80,8 @@ SIGNATURES = {
     "hop_riccati_f32": (C.c_int, _RIC32),
     "hop_bruteforce_jcurve_f64": (C.c_int, _JC64),
     "hop_bruteforce_jcurve_f32": (C.c_int, _JC32),
+    "hop_riccati_legacy_f64": (C.c_int, _RICLEG),
+    "hop_bruteforce_jcurve_legacy_f64": (C.c_int, _JCLEG),
     "hop_system_dims": (C.c_int, [_I32, _P, _P]),
     "hop_linearize_f64": (C.c_int, [_I32, C.c_double, _P, _P, _I64, _I32, _I32, _I32,
                                     C.c_double, C.c_double, C.c_double, C.c_double, _P, _P, _P,

@@ -172,7 +172,7 @@ int riccati_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, 
                   const T* qx_extra, const T* c_extra, const int32_t* horizon, const T* lm,
                   T w_stage, uint32_t wrap_mask, int32_t mode, int32_t reg_max_tries,
                   int64_t batch, int32_t n_alloc, int32_t n, int32_t m, T* K, T* k, T* Vxx,
-                  T* Vx, T* V0, int32_t* status, void* stream) {
+                  T* Vx, T* V0, int32_t* status, void* stream, int legacy = 0) {
   if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
   if (batch == 0) return HOP_OK;
   if (n < 1 || n > HOP_MAX_DIM) return fail(HOP_E_SIZE, "n must be in [1, 16]");
@@ -192,6 +192,8 @@ int riccati_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, 
   a.batch = batch; a.nalloc = n_alloc; a.n = n; a.m = m; a.mode = mode;
   a.reg_max_tries = reg_max_tries; a.max_tries = 8; a.wrap_mask = wrap_mask; a.w_stage = w_stage;
   a.K = K; a.k = k; a.Vxx = Vxx; a.Vx = Vx; a.V0 = V0; a.status = status;
+  a.legacy = legacy;
+  if (legacy && m > 11) return fail(HOP_E_SIZE, "legacy lstsq fallback: m must be <= 11");
   return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
 }
 
@@ -202,7 +204,7 @@ int jcurve_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, i
                  int64_t r_bs, const T* Qf, int64_t qf_bs, const T* qxx_extra,
                  const T* qx_extra, const T* c_extra, T lm_lambda, T w_stage, uint32_t wrap_mask,
                  int64_t batch, int32_t n_alloc, int32_t n, int32_t m, int32_t t_max, T* J,
-                 int32_t* status, void* stream) {
+                 int32_t* status, void* stream, int legacy = 0) {
   if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
   if (n < 1 || n > HOP_MAX_DIM) return fail(HOP_E_SIZE, "n must be in [1, 16]");
   if (m < 1 || m > HOP_MAX_DIM) return fail(HOP_E_SIZE, "m must be in [1, 16]");
@@ -229,6 +231,8 @@ int jcurve_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, i
   a.K = nullptr; a.k = nullptr; a.Vxx = nullptr; a.Vx = nullptr; a.V0 = nullptr;
   a.status = nullptr;
   a.jc_J = J; a.jc_status = status; a.jc_tmax = t_max; a.lm_value = lm_lambda;
+  a.legacy = legacy;
+  if (legacy && m > 11) return fail(HOP_E_SIZE, "legacy lstsq fallback: m must be <= 11");
   return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
 }
 
@@ -469,6 +473,32 @@ int hop_bruteforce_jcurve_f32(const float* A, const float* Bm, const float* X, c
   return jcurve_entry<float>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
                              qxx_extra, qx_extra, c_extra, lm_lambda, w_stage, wrap_mask, batch,
                              n_alloc, n, m, t_max, J, status, stream);
+}
+
+int hop_riccati_legacy_f64(const double* A, const double* Bm, const double* X, const double* U,
+                           const double* xg, int64_t xg_bs, const double* u_ref, int64_t ur_bs,
+                           const double* Q, int64_t q_bs, const double* R, int64_t r_bs,
+                           const double* Qf, int64_t qf_bs, const int32_t* horizon,
+                           const double* lm, double w_stage, uint32_t wrap_mask, int32_t mode,
+                           int64_t batch, int32_t n_alloc, int32_t n, int32_t m, double* K,
+                           double* k, double* Vxx, double* Vx, double* V0, int32_t* status,
+                           void* stream) {
+  return riccati_entry<double>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
+                               nullptr, nullptr, nullptr, horizon, lm, w_stage, wrap_mask, mode,
+                               1, batch, n_alloc, n, m, K, k, Vxx, Vx, V0, status, stream, 1);
+}
+
+int hop_bruteforce_jcurve_legacy_f64(const double* A, const double* Bm, const double* X,
+                                     const double* U, const double* xg, int64_t xg_bs,
+                                     const double* u_ref, int64_t ur_bs, const double* Q,
+                                     int64_t q_bs, const double* R, int64_t r_bs,
+                                     const double* Qf, int64_t qf_bs, double lm_lambda,
+                                     double w_stage, uint32_t wrap_mask, int64_t batch,
+                                     int32_t n_alloc, int32_t n, int32_t m, int32_t t_max,
+                                     double* J, int32_t* status, void* stream) {
+  return jcurve_entry<double>(A, Bm, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, R, r_bs, Qf, qf_bs,
+                              nullptr, nullptr, nullptr, lm_lambda, w_stage, wrap_mask, batch,
+                              n_alloc, n, m, t_max, J, status, stream, 1);
 }
 
 int hop_augment_f64(const double* A, const double* Bm, const double* a_res, const double* X,

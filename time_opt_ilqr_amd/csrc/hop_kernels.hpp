@@ -116,6 +116,12 @@ struct RiccatiArgs {
   int* jc_status = nullptr;   // [B][jc_tmax]
   int jc_tmax = 0;
   T lm_value = T(0);
+  // legacy twin (ilqr_propagator.py): chol_solve with 4 jitters, then the
+  // least-squares solve of sym(Quu_reg) (np.linalg.lstsq, ilqr_propagator.py:33-43)
+  // instead of the crash mark; no finiteness checks (the legacy loops have none);
+  // Quu_reg = _sym(Quu) + lm I with lm as given (no 1e-12 floor, no lambda ladder).
+  // Runs on the generic kernel only.
+  int legacy = 0;
 };
 
 // batched finite-difference linearisation (linearize.hip, dynamics.hpp)

@@ -44,6 +44,89 @@ __device__ __forceinline__ void rload_row(const T* M, int rows, int cols, int c,
 // section stamps of the diagnostic instantiation (tools/stamps_riccati.py)
 __device__ unsigned long long g_ric_stamp[16];
 
+// The legacy chol_solve's last resort (ilqr_propagator.py:43): np.linalg.lstsq(A, B)
+// of the symmetric A = Quu_reg is the minimum-norm solution pinv(A) B, and
+// pinv(A) = V diag(1/lambda_k) V^T over the eigenpairs with |lambda_k| > rcond
+// max|lambda| (gelsd's cutoff, rcond = eps * m: the singular values of a symmetric
+// matrix are |lambda_k|).  Rare path, one lane per problem: cyclic Jacobi on A
+// parked in the problem's tile (A at [0, m^2), V at [m^2, 2 m^2), m <= 11), then
+// lane c forms column c of pinv(A).  need: this row takes the fallback.
+template <class T, int MM>
+__device__ __forceinline__ bool legacy_pinv(T (&Qi)[MM], const T (&A)[MM], T* tile, int c, int m,
+                                            bool need) {
+  const bool fits = 2 * m * m <= kLdsTile;
+  wave_sync();
+  if (need && fits && c < m) {
+#pragma unroll
+    for (int r = 0; r < MM; ++r)
+      if (r < m) tile[r * m + c] = A[r];
+  }
+  wave_sync();
+  T* a = tile;
+  T* v = tile + m * m;
+  if (need && fits && c == 0) {
+    for (int i = 0; i < m * m; ++i) v[i] = T(0);
+    for (int i = 0; i < m; ++i) v[i * m + i] = T(1);
+    for (int sweep = 0; sweep < 64; ++sweep) {
+      T off = T(0), tot = T(0);
+      for (int p = 0; p < m; ++p)
+        for (int q = 0; q < m; ++q) {
+          const T x = a[p * m + q] * a[p * m + q];
+          tot += x;
+          if (p != q) off += x;
+        }
+      if (!(off > T(1e-60) * tot) || !(tot == tot)) break;
+      for (int p = 0; p < m - 1; ++p)
+        for (int q = p + 1; q < m; ++q) {
+          const T apq = a[p * m + q];
+          if (apq == T(0)) continue;
+          const T theta = (a[q * m + q] - a[p * m + p]) / (T(2) * apq);
+          T t = T(1) / (fabs(theta) + sqrt(theta * theta + T(1)));
+          if (theta < T(0)) t = -t;
+          const T cs = T(1) / sqrt(t * t + T(1)), sn = t * cs;
+          for (int k = 0; k < m; ++k) {  // A <- A J (columns p, q)
+            const T akp = a[k * m + p], akq = a[k * m + q];
+            a[k * m + p] = cs * akp - sn * akq;
+            a[k * m + q] = sn * akp + cs * akq;
+          }
+          for (int k = 0; k < m; ++k) {  // A <- J^T A (rows p, q)
+            const T apk = a[p * m + k], aqk = a[q * m + k];
+            a[p * m + k] = cs * apk - sn * aqk;
+            a[q * m + k] = sn * apk + cs * aqk;
+          }
+          a[p * m + q] = T(0);
+          a[q * m + p] = T(0);
+          for (int k = 0; k < m; ++k) {  // V <- V J
+            const T vkp = v[k * m + p], vkq = v[k * m + q];
+            v[k * m + p] = cs * vkp - sn * vkq;
+            v[k * m + q] = sn * vkp + cs * vkq;
+          }
+        }
+    }
+  }
+  wave_sync();
+  bool finite = true;
+  if (need && fits) {
+    T lmax = T(0);
+    for (int k = 0; k < m; ++k) lmax = fmax(lmax, fabs(a[k * m + k]));
+    const T cut = T(sizeof(T) == 8 ? 2.220446049250313e-16 : 1.1920929e-07) * T(m) * lmax;
+    const int cc = c < m ? c : 0;
+#pragma unroll
+    for (int r = 0; r < MM; ++r) {
+      T acc = T(0);
+      if (r < m && c < m)
+        for (int k = 0; k < m; ++k) {
+          const T lk = a[k * m + k];
+          if (fabs(lk) > cut) acc += v[r * m + k] * v[cc * m + k] / lk;
+        }
+      Qi[r] = acc;
+      finite = finite && (acc == acc) && (acc - acc == T(0));
+    }
+  }
+  wave_sync();
+  return fits && finite;
+}
+
 // One pass of problem block blk; JCK: the J-curve form at horizon jl for the whole wave.
 template <class T, int S, int MM, bool STAMP, bool JCK, int MODE>
 __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long blk, int jl) {
@@ -124,7 +207,7 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     T eT = (c < n) ? Xp[(long long)iT * n + (c < n ? c : 0)] - xg_c : T(0);
     if (wrap_c) eT = wrap_angle(eT);
     const bool fin = ((__ballot(!finite_val(eT)) >> (16 * g)) & 0xffffull) == 0ull;
-    if (!fin) {
+    if (!fin && !a.legacy) {  // the legacy loops check nothing: NaN propagates
       st |= ST_NONFINITE | ST_FAIL;
       alive = false;
     }
@@ -185,7 +268,7 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     // chol_solve raises, so a non-finite e at t = 0 only feeds V_0 (inf/NaN in J)
     const bool e_ok = (JC && i == 0) || finite_val(e);
     const unsigned long long badm = __ballot(!(e_ok && finite_val(du)));
-    const bool bad = ((badm >> (16 * g)) & 0xffffull) != 0ull;
+    const bool bad = !a.legacy && ((badm >> (16 * g)) & 0xffffull) != 0ull;
 
     stamp(0);
     // lx = Q e (+ cx), lu = R du, l0
@@ -268,6 +351,32 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
       // the reference first checks cholesky(Quu_reg) (no jitter), then solves with jitter
       bool ok = true;
       solved = spd_inverse_nofallback_chk(Qi, tile, c, 8, st, ok) && ok;
+    } else if (a.legacy) {
+      // legacy chol_solve (ilqr_propagator.py:33-43) on Quu_reg = _sym(Quu) + lm I:
+      // 4 jitters, then lstsq (a non-finite Quu_reg: lstsq raises, the row fails)
+      T Qs[MM];
+#pragma unroll
+      for (int r = 0; r < MM; ++r) Qs[r] = T(0.5) * (Quu[r] + QuuT[r]) + ((c == r) ? lam0 : T(0));
+      copy(Qi, Qs);
+      const bool okr = spd_inverse_nofallback(Qi, tile, c, 4, st);
+      solved = okr;
+      const bool need = act && !okr;
+      if (__any(need)) {
+        T z = T(0);
+#pragma unroll
+        for (int r = 0; r < MM; ++r) z = z + Qs[r] * T(0);
+        const unsigned long long nm = __ballot(!(z == z) && c < m);
+        const bool nonfin = ((nm >> (16 * g)) & 0xffffull) != 0ull;
+        T P[MM];
+        const bool okp = legacy_pinv<T, MM>(P, Qs, tile, c, m, need && !nonfin);
+        if (need && !nonfin) {
+#pragma unroll
+          for (int r = 0; r < MM; ++r) Qi[r] = P[r];
+          st |= ST_LU;
+          solved = okp;
+        }
+        if (need && nonfin) st |= ST_NONFINITE;
+      }
     } else {
       T lam = lam0 > T(1e-12) ? lam0 : T(1e-12);
       int tries = 0;
@@ -323,10 +432,10 @@ __device__ __forceinline__ void riccati_body(const RiccatiArgs<T>& a, long long 
     // The brute-force curve raises only through the next step's chol_solve: a
     // non-finite Vxx / Vx fails there, a non-finite V_0 never does, and at t = 0
     // nothing follows -- only chol_solve(Quu_reg, Qux) itself can raise (Qux).
-    bool vbad = !finite_val(vxn) || (!JC && !finite_val(v0n));
+    bool vbad = !a.legacy && (!finite_val(vxn) || (!JC && !finite_val(v0n)));
 #pragma unroll
-    for (int r = 0; r < S; ++r) vbad = vbad || !finite_val(Vn[r]);
-    if (JC && i == 0) {
+    for (int r = 0; r < S; ++r) vbad = vbad || (!a.legacy && !finite_val(Vn[r]));
+    if (JC && i == 0 && !a.legacy) {
       vbad = false;
 #pragma unroll
       for (int r = 0; r < MM; ++r) vbad = vbad || !finite_val(Qux[r]);
@@ -428,7 +537,7 @@ hipError_t launch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
 template <class T>
 hipError_t dispatch_riccati(const RiccatiArgs<T>& a, hipStream_t stream) {
   if constexpr (sizeof(T) == 8) {
-    if (!opt(HOP_OPT_FORCE_GENERIC)) {  // (HOP_OPT_STAMPS: the fast kernel's own stamps)
+    if (!opt(HOP_OPT_FORCE_GENERIC) && !a.legacy) {  // (HOP_OPT_STAMPS: the fast kernel's own stamps)
       const hipError_t e = dispatch_riccati_fast(a, stream);
       if (e != hipErrorNotSupported) return e;
     }

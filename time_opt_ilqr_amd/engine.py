@@ -379,12 +379,15 @@ def _scalar_or_vec(v, dtype, dev, name):
 
 def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
             w_stage: float = 0.0, wrap_idx=None, qxx_extra=None, qx_extra=None, c_extra=None,
-            reg_max_tries: int = 12, want_v: bool = False) -> RiccatiResult:
+            reg_max_tries: int = 12, want_v: bool = False, legacy: bool = False) -> RiccatiResult:
     """Batched Riccati pass.  mode 0: backward_pass_truncated (solver.py:156-230);
     mode 1: value_expansions_and_gains_prefix (horizon_selection.py:97-212).
 
     A [B,N,n,n], Bm [B,N,n,m], X [B,N+1,n], U [B,N,m]; xg/u_ref/Q/R/Qf shared or
     per problem; horizon [B] int (T* or T_bar+S_right); lm [B] or scalar.
+    legacy=True: the legacy twin's passes (ilqr_propagator.py:375-400 / 237-287,
+    hop_riccati_legacy_f64): its chol_solve (4 jitters, then lstsq, ST_LU), no
+    finiteness checks, Qf = alpha I; fp64, no extra stage cost.
     """
     torch = _torch()
     dt = A.dtype
@@ -417,26 +420,37 @@ def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
     Vxx = torch.empty((Bn, N + 1, n, n), dtype=dt, device=dev) if want else None
     Vx = torch.empty((Bn, N + 1, n), dtype=dt, device=dev) if want else None
     V0 = torch.empty((Bn, N + 1), dtype=dt, device=dev) if want else None
-    rc = _fn("hop_riccati", dt)(
-        _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(X), _lib.ptr(U),
-        _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref), _bstride(u_ref, 1, "u_ref", Bn),
-        _lib.ptr(Q), _bstride(Q, 2, "Q", Bn), _lib.ptr(R), _bstride(R, 2, "R", Bn),
-        _lib.ptr(Qf), _bstride(Qf, 2, "Qf", Bn),
-        _lib.ptr(ex[0]), _lib.ptr(ex[1]), _lib.ptr(ex[2]), _lib.ptr(horizon), _lib.ptr(lm),
-        float(w_stage), wrap_mask(wrap_idx, n), int(mode), int(reg_max_tries), Bn, N, n, m,
-        _lib.ptr(K), _lib.ptr(k), _lib.ptr(Vxx), _lib.ptr(Vx), _lib.ptr(V0), _lib.ptr(status),
-        _lib.stream_handle(dev))
+    ins = [_lib.ptr(A), _lib.ptr(Bm), _lib.ptr(X), _lib.ptr(U),
+           _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref), _bstride(u_ref, 1, "u_ref", Bn),
+           _lib.ptr(Q), _bstride(Q, 2, "Q", Bn), _lib.ptr(R), _bstride(R, 2, "R", Bn),
+           _lib.ptr(Qf), _bstride(Qf, 2, "Qf", Bn)]
+    outs = [_lib.ptr(K), _lib.ptr(k), _lib.ptr(Vxx), _lib.ptr(Vx), _lib.ptr(V0), _lib.ptr(status),
+            _lib.stream_handle(dev)]
+    if legacy:
+        if dt != torch.float64 or any(t is not None for t in ex):
+            raise ValueError("legacy passes: fp64 and no extra stage cost (ilqr_propagator.py)")
+        rc = _lib.load().hop_riccati_legacy_f64(
+            *ins, _lib.ptr(horizon), _lib.ptr(lm), float(w_stage), wrap_mask(wrap_idx, n),
+            int(mode), Bn, N, n, m, *outs)
+    else:
+        rc = _fn("hop_riccati", dt)(
+            *ins, _lib.ptr(ex[0]), _lib.ptr(ex[1]), _lib.ptr(ex[2]), _lib.ptr(horizon),
+            _lib.ptr(lm), float(w_stage), wrap_mask(wrap_idx, n), int(mode), int(reg_max_tries),
+            Bn, N, n, m, *outs)
     _lib.check(rc)
     return RiccatiResult(K, k, status, Vxx, Vx, V0)
 
 
 def bruteforce_jcurve(A, Bm, X, U, xg, u_ref, Q, R, Qf, t_max: int, *, lm_lambda: float = 1e-6,
                       w_stage: float = 0.0, wrap_idx=None, qxx_extra=None, qx_extra=None,
-                      c_extra=None):
+                      c_extra=None, legacy: bool = False):
     """bruteforce_all_Jt_backward_expansion (solver.py:293-358) for a batch: J [B, t_max]
     with J[:, T-1] = V_0 of the length-T sweep, and the per-horizon status [B, t_max]
     (ST_FAIL / ST_NONFINITE where the reference raises).  All t_max sweeps of every
-    problem run in one launch (hop_bruteforce_jcurve_*).  Inputs as riccati()."""
+    problem run in one launch (hop_bruteforce_jcurve_*).  Inputs as riccati().
+    legacy=True: the legacy twin's brute force (ilqr_propagator.py:426-454,
+    hop_bruteforce_jcurve_legacy_f64): chol_solve with 4 jitters then lstsq (ST_LU
+    where it ran), Qf = alpha I; fp64, no extra stage cost."""
     torch = _torch()
     dt = A.dtype
     A = _dev(A, "A", dt)
@@ -462,6 +476,18 @@ def bruteforce_jcurve(A, Bm, X, U, xg, u_ref, Q, R, Qf, t_max: int, *, lm_lambda
     t_max = int(t_max)
     J = torch.empty((Bn, t_max), dtype=dt, device=dev)
     status = torch.empty((Bn, t_max), dtype=torch.int32, device=dev)
+    if legacy:
+        if dt != torch.float64 or any(t is not None for t in ex):
+            raise ValueError("legacy passes: fp64 and no extra stage cost (ilqr_propagator.py)")
+        rc = _lib.load().hop_bruteforce_jcurve_legacy_f64(
+            _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(X), _lib.ptr(U),
+            _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref),
+            _bstride(u_ref, 1, "u_ref", Bn), _lib.ptr(Q), _bstride(Q, 2, "Q", Bn), _lib.ptr(R),
+            _bstride(R, 2, "R", Bn), _lib.ptr(Qf), _bstride(Qf, 2, "Qf", Bn), float(lm_lambda),
+            float(w_stage), wrap_mask(wrap_idx, n), Bn, N, n, m, t_max, _lib.ptr(J),
+            _lib.ptr(status), _lib.stream_handle(dev))
+        _lib.check(rc)
+        return J, status
     rc = _fn("hop_bruteforce_jcurve", dt)(
         _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(X), _lib.ptr(U),
         _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref), _bstride(u_ref, 1, "u_ref", Bn),

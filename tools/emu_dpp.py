@@ -34,9 +34,11 @@ def run(asm_lines, regs, lds=None):
             addr = regs[int(m.group(2))].astype(np.int64) + int(m.group(3) or 0)
             regs[int(m.group(1))] = lds[addr // 8].astype(float)
             continue
-        if not line or line.startswith(("s_nop", "s_waitcnt", "ds_read")):
-            continue  # LDS reads riding in a block are checked on the GPU
+        if not line or line.startswith(("s_nop", "s_waitcnt", "ds_read", ".")):
+            continue  # LDS reads riding in a block are checked on the GPU; directives
         op, rest = line.split(None, 1)
+        if op.endswith("_e64"):  # the 8-byte VOP3 encoding of a VOP1 op (code placement)
+            op = op[:-4]
         bc = None
         m = re.search(r"row_newbcast:(\d+)", rest)
         if m:
