@@ -763,10 +763,48 @@ def legacy_bruteforce_cases(seed=9850):
     np.savez_compressed(os.path.join(HERE, "legacy_bruteforce_cases.npz"), **d)
 
 
+def lu_pivot_cases(seed=9900):
+    """Round 3: chol_inv's LU slot where the row exchanges of gesv's partial pivoting
+    matter (utils.py:88-93): an indefinite block with A[0, 0] = -0.1, so the leading
+    entry of A + 0.1 I -- the first pivot of an unpivoted elimination -- is exactly
+    zero while the block is regular.  Alone (inv_s*) and inside propagator sweeps
+    (Q_k of problem 0 at step 3, QT of problem 1 at step 5), s = 3 (small-s kernel),
+    5 (generic kernel) and 13 (hand-over -> rerun kernel)."""
+    rng = np.random.default_rng(seed)
+    d = {}
+
+    def indef0(s):
+        Qm, _ = np.linalg.qr(rng.standard_normal((s, s)))
+        ev = rng.uniform(0.5, 3.0, s) * np.where(np.arange(s) % 2 == 0, 1.0, -1.0)
+        M = Qm @ np.diag(ev) @ Qm.T
+        M = 0.5 * (M + M.T)
+        M[0, 0] = -0.1
+        return M
+
+    for s in (3, 5, 13):
+        M = indef0(s)
+        d[f"inv_s{s}_in"] = M
+        d[f"inv_s{s}_out"] = ref_utils.chol_inv(M)
+    for tag, s, m, N in (("s13_m4_N20", 13, 4, 20), ("s5_m1_N20", 5, 1, 20),
+                         ("s3_m1_N20", 3, 1, 20)):
+        probs = [list(orc.synth_lft_problem(seed + 10 + i, s, m, N)) for i in range(3)]
+        probs[0][2] = probs[0][2].copy()
+        probs[0][2][3] = indef0(s)
+        probs[1][6] = probs[1][6].copy()
+        probs[1][6][5] = indef0(s)
+        d[f"lft_{tag}_Q03"] = probs[0][2][3]
+        d[f"lft_{tag}_QT15"] = probs[1][6][5]
+        d[f"lft_{tag}_J"] = np.array([_prop(tuple(p), N) for p in probs])
+        d[f"lft_{tag}_base_seed"] = seed + 10
+    np.savez_compressed(os.path.join(HERE, "lu_pivot_cases.npz"), **d)
+    print("lu_pivot_cases:", sorted(d))
+
+
 def main_r3():
     np.seterr(all="ignore")
     bruteforce_edge_cases()
     legacy_bruteforce_cases()
+    lu_pivot_cases()
 
 
 def main_r2():

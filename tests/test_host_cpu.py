@@ -683,3 +683,36 @@ def test_predict_eps_block_emulated():
     want = 1e-9 * np.eye(n) + A @ Sg @ A.T
     assert np.abs(X[:, :n] - want).max() <= 1e-13 * np.abs(want).max()
     assert np.abs(X[:, n] - A @ mp).max() <= 1e-13 * np.abs(A @ mp).max()
+
+
+def test_lu_slot_pivoting_host_build(small_host, golden_dir):
+    """lu_pivot.hpp (the kernels' LU slot, utils.py:88-93) on the host: the
+    reference's chol_inv outputs for blocks whose A + 0.1 I has a zero leading entry
+    (an unpivoted elimination divides by zero there) and random regular ones."""
+    fn = small_host.small_host_lu_sym_solve_f64
+    fn.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p, C.c_void_p]
+    fn.restype = C.c_int
+    d = np.load(os.path.join(golden_dir, "lu_pivot_cases.npz"))
+
+    def inv(A, eps):
+        n = A.shape[0]
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        out = np.zeros((n, n))
+        for c in range(n):
+            b = np.zeros(n)
+            b[c] = 1.0
+            x = np.zeros(n)
+            assert fn(A.ctypes.data, n, eps, b.ctypes.data, x.ctypes.data) == 0
+            out[:, c] = x
+        return out
+
+    for s in (3, 5, 13):
+        got = inv(d[f"inv_s{s}_in"], 0.1)
+        ref = d[f"inv_s{s}_out"]
+        assert np.max(np.abs(got - ref)) <= 1e-12 * np.max(np.abs(ref)), s
+    rng = np.random.default_rng(3)
+    for n in (2, 7, 16):
+        A = rng.standard_normal((n, n))
+        ref = np.linalg.solve(0.5 * (A + A.T) + 1e-3 * np.eye(n), np.eye(n))
+        got = inv(A, 1e-3)
+        assert np.max(np.abs(got - ref)) <= 1e-10 * np.max(np.abs(ref)), n

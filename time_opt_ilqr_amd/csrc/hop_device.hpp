@@ -14,6 +14,7 @@
 #include <utility>
 
 #include "dpp_blocks.inc"
+#include "lu_pivot.hpp"
 #include "wrap.hpp"
 
 namespace hop {
@@ -213,7 +214,7 @@ __device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int m
   }
   T eps = T(1e-9);
   int tries = 0;
-  bool done = false, nf = false;
+  bool done = false, nf = false, lu = false;
 #pragma unroll 1
   while (true) {
     bool ok = true;
@@ -231,7 +232,10 @@ __device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int m
       if (nf) st |= ST_NONFINITE;
     }
     const bool last = tries >= max_tries;
-    if (!done && !ok && !nf && last) st |= ST_LU;
+    if (!done && !ok && !nf && last) {
+      st |= ST_LU;
+      lu = true;
+    }
     done = ok || last || nf;
     if (!__any(!done)) break;
     if (!done) {
@@ -243,6 +247,17 @@ __device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int m
     lds_get_t(tile, c, t);
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = T(0.5) * (tile[i * kLdsRow + c] + t[i]);
+  }
+  if (__any(lu)) {  // the LU slot (utils.py:88-93): column c of solve(sym(A) + eps I, I)
+    if (lu) {
+      T x[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) x[i] = (i == c) ? T(1) : T(0);
+      const bool okl =
+          lu_sym_solve<T, S>([&](int i, int j) { return tile[i * kLdsRow + j]; }, S, eps, x);
+#pragma unroll
+      for (int i = 0; i < S; ++i) r[i] = okl ? -x[i] : T(__builtin_nan(""));
+    }
   }
   wave_sync();
 #pragma unroll

@@ -351,7 +351,7 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
   double cur = 1e-9;               // offset form: jitter currently in the LDS diagonal
   int tries = ok0 ? 0 : 1;
   const bool nf = !ok0 && row_input_nonfinite<S, LD>(img, c);
-  bool done = ok0 || nf;
+  bool done = ok0 || nf, lu = false;
   if (!ok0) st |= nf ? ST_NONFINITE : ST_JITTER;
 #pragma unroll 1
   while (__any(!done)) {
@@ -363,12 +363,30 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
     bool ok = true;
     sweep<C, S>(r, eps, ok);
     const bool last = tries >= max_tries;
-    if (!done && !ok && last) st |= ST_LU;
+    if (!done && !ok && last) {
+      st |= ST_LU;
+      lu = true;
+    }
     done = done || ok || last;
     if (!__any(!done)) break;
     if (!done) {
       eps *= 10.0;
       ++tries;
+    }
+  }
+  if (__any(lu)) {  // the LU slot (utils.py:88-93): solve(sym(A) + eps I, I), pivoted
+    wave_sync();
+    if (lu) {
+      constexpr bool OFFF = offset_form<C>();  // offset form: the image diagonal is value - 1 + eps
+      double x[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+      const bool okl = lu_sym_solve<double, S>(
+          [&](int i, int j) { return img[i * LD + j] + ((OFFF && i == j) ? 1.0 : 0.0); }, S,
+          OFFF ? 0.0 : eps, x);
+#pragma unroll
+      for (int i = 0; i < S; ++i)
+        r[i] = okl ? ((OFFF && i == c) ? 1.0 : 0.0) - x[i] : __builtin_nan("");
     }
   }
   if (nf) {
@@ -448,7 +466,7 @@ __device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c
     double eps = ok0 ? 1e-9 : 1e-8;
     int tries = ok0 ? 0 : 1;
     const bool nf = !ok0 && row_input_nonfinite<S, kLdsRow, S + 1>(tile, c);
-    bool done = ok0 || nf;
+    bool done = ok0 || nf, lu = false;
     if (!ok0) st |= nf ? ST_NONFINITE : ST_JITTER;
 #pragma unroll 1
     while (__any(!done)) {
@@ -456,13 +474,27 @@ __device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c
       bool ok2 = true;
       q = elim_quad<C, S>(r, eps, ok2);
       const bool last = tries >= mt;
-      if (!done && !ok2 && last) st |= ST_LU;
+      if (!done && !ok2 && last) {
+        st |= ST_LU;
+        lu = true;
+      }
       done = done || ok2 || last;
       if (!__any(!done)) break;
       if (!done) {
         eps *= 10.0;
         ++tries;
       }
+    }
+    if (lu) {  // the LU slot: z0^T solve(sym(X0) + eps I, z0), pivoted (z0 in the tile's row S)
+      double y[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) y[i] = tile[S * kLdsRow + i];
+      const bool okl =
+          lu_sym_solve<double, S>([&](int i, int j) { return tile[i * kLdsRow + j]; }, S, eps, y);
+      double qq = 0.0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) qq += tile[S * kLdsRow + i] * y[i];
+      q = okl ? qq : __builtin_nan("");
     }
     if (nf) q = __builtin_nan("");
   }
@@ -500,7 +532,7 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
       const unsigned long long m = __ballot(c < S && !(z == z));
       nf = nf || (!ok0 && ((m >> (16 * ((threadIdx.x & 63) >> 4))) & 0xffffull) != 0ull);
     }
-    bool done = ok0 || nf;
+    bool done = ok0 || nf, lu = false;
     if (!ok0) st |= nf ? ST_NONFINITE : ST_JITTER;
 #pragma unroll 1
     while (__any(!done)) {
@@ -513,13 +545,34 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
       QueryLdl<S>::run(r, Ht, X0, dmin);
       const bool ok = pivots_ok(X0, dmin);
       const bool last = tries >= mt;
-      if (!done && !ok && last) st |= ST_LU;
+      if (!done && !ok && last) {
+        st |= ST_LU;
+        lu = true;
+      }
       done = done || ok || last;
       if (!__any(!done)) break;
       if (!done) {
         eps *= 10.0;
         ++tries;
       }
+    }
+    if (__any(lu)) {
+      // the LU slot of Wt = chol_inv(Xt + Gbar) (utils.py:88-93, pivoted): lane c
+      // solves (Mt + eps I) v = (column c of Fbar^T), then X0 = Ebar - Fbar Wt Fbar^T
+      // = Ebar - sum_j H_j (x) v_j (the tile holds Mt in offset form: diag - 1 + eps)
+      wave_sync();
+      double v[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) v[i] = H[i];
+      bool okl = true;
+      if (lu)
+        okl = lu_sym_solve<double, S>(
+            [&](int i, int j) { return tile[i * kLdsRow + j] + (i == j ? 1.0 : 0.0); }, S, 0.0, v);
+      double Xl[S];
+      copy(Xl, Eb);
+      acc_xty<true>(Xl, H, v);  // Ebar - Fbar (Mt + eps I)^-1 Fbar^T
+#pragma unroll
+      for (int i = 0; i < S; ++i) X0[i] = lu ? (okl ? Xl[i] : __builtin_nan("")) : X0[i];
     }
     if (nf) {
 #pragma unroll

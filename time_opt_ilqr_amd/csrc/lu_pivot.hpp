@@ -1,0 +1,86 @@
+// chol_inv's last resort, the LU slot (utils.py:88-93): np.linalg.solve(A + eps I, I)
+// after every jitter failed, i.e. LAPACK gesv -- an LU factorisation with partial
+// pivoting (the row of largest |a_ip| at or below the diagonal, the first one on a
+// tie, as idamax) and triangular solves.  Without the row exchanges a block whose
+// leading minors vanish (a zero pivot) cannot be solved although it is regular.
+//
+// Rare path: the kernels call it only for problems flagged ST_LU.  Each lane factors
+// its own private copy (the arrays live in scratch for the larger sizes), so no
+// LDS, no cross-lane traffic and no synchronisation are involved; the host test
+// build (small_host.cpp) exercises the same code against NumPy.
+#pragma once
+
+#ifndef HOP_HD
+#define HOP_HD __host__ __device__
+#endif
+
+namespace hop {
+
+// In place: a (n x n, row-major in a[S][S]) <- L\U of P a, perm[i] = original row
+// of row i.  Returns false on an exactly zero pivot (gesv: singular, LinAlgError).
+template <class T, int S>
+HOP_HD inline bool lu_factor(T (&a)[S][S], int n, int (&perm)[S]) {
+  bool ok = true;
+  for (int i = 0; i < n; ++i) perm[i] = i;
+  for (int p = 0; p < n; ++p) {
+    int piv = p;
+    T big = a[p][p] < T(0) ? -a[p][p] : a[p][p];
+    for (int i = p + 1; i < n; ++i) {
+      const T v = a[i][p] < T(0) ? -a[i][p] : a[i][p];
+      if (v > big) {
+        big = v;
+        piv = i;
+      }
+    }
+    if (piv != p) {
+      for (int j = 0; j < n; ++j) {
+        const T t = a[p][j];
+        a[p][j] = a[piv][j];
+        a[piv][j] = t;
+      }
+      const int t = perm[p];
+      perm[p] = perm[piv];
+      perm[piv] = t;
+    }
+    const T d = a[p][p];
+    if (!(d != T(0))) {
+      ok = false;
+      continue;
+    }
+    for (int i = p + 1; i < n; ++i) {
+      const T l = a[i][p] / d;
+      a[i][p] = l;
+      for (int j = p + 1; j < n; ++j) a[i][j] -= l * a[p][j];
+    }
+  }
+  return ok;
+}
+
+// x <- (P^T L U)^-1 b for the factors of lu_factor (b is overwritten)
+template <class T, int S>
+HOP_HD inline void lu_solve(const T (&a)[S][S], int n, const int (&perm)[S], T (&b)[S]) {
+  T y[S];
+  for (int i = 0; i < n; ++i) y[i] = b[perm[i]];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < i; ++j) y[i] -= a[i][j] * y[j];
+  for (int i = n - 1; i >= 0; --i) {
+    T v = y[i];
+    for (int j = i + 1; j < n; ++j) v -= a[i][j] * b[j];
+    b[i] = v / a[i][i];
+  }
+  for (int i = n; i < S; ++i) b[i] = T(0);
+}
+
+// x = (sym(M) + eps I)^-1 rhs with M(i, j) = at(i, j), n x n; false when singular
+template <class T, int S, class F>
+HOP_HD inline bool lu_sym_solve(F at, int n, T eps, T (&x)[S]) {
+  T a[S][S];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) a[i][j] = T(0.5) * (at(i, j) + at(j, i)) + (i == j ? eps : T(0));
+  int perm[S];
+  const bool ok = lu_factor<T, S>(a, n, perm);
+  if (ok) lu_solve<T, S>(a, n, perm, x);
+  return ok;
+}
+
+}  // namespace hop

@@ -133,3 +133,15 @@ extern "C" void small_host_wrap_f64(const double* in, double* out, int64_t n) {
 extern "C" void small_host_wrap_f32(const float* in, float* out, int64_t n) {
   for (int64_t i = 0; i < n; ++i) out[i] = hop::wrap_angle(in[i]);
 }
+
+// The LU slot (lu_pivot.hpp) on the host: x = (sym(A) + eps I)^-1 b, n <= 16; 0 or -1
+// when the pivoted factorisation meets an exactly zero pivot
+extern "C" int small_host_lu_sym_solve_f64(const double* A, int n, double eps, const double* b,
+                                           double* x) {
+  double y[16];
+  for (int i = 0; i < 16; ++i) y[i] = i < n ? b[i] : 0.0;
+  const bool ok =
+      hop::lu_sym_solve<double, 16>([&](int i, int j) { return A[i * n + j]; }, n, eps, y);
+  for (int i = 0; i < n; ++i) x[i] = y[i];
+  return ok ? 0 : -1;
+}

@@ -15,6 +15,8 @@
 #define HOP_HD __host__ __device__
 #endif
 
+#include "lu_pivot.hpp"
+
 namespace hop {
 namespace small {
 
@@ -110,7 +112,18 @@ HOP_HD inline void spd_inverse(Sym<T, S>& m, int max_tries, unsigned& st) {
       ok = sweep_neg_inverse(m, eps);
       if (ok) break;
       if (tries >= max_tries) {
+        // the LU slot: np.linalg.solve(A + eps I, I), partial pivoting (lu_pivot.hpp)
         st |= kStLu;
+        T inv[S][S];
+        bool okl = true;
+        for (int c = 0; c < S; ++c) {
+          T x[S];
+          for (int i = 0; i < S; ++i) x[i] = i == c ? T(1) : T(0);
+          okl = okl && lu_sym_solve<T, S>([&](int i, int j) { return in.at(i, j); }, S, eps, x);
+          for (int i = 0; i < S; ++i) inv[i][c] = x[i];
+        }
+        for (int i = 0; i < S; ++i)
+          for (int j = i; j < S; ++j) m.at(i, j) = okl ? -inv[i][j] : T(__builtin_nan(""));
         break;
       }
     }
@@ -155,9 +168,15 @@ HOP_HD inline T quad_inverse(const Sym<T, S>& x0, const T (&z)[S], int max_tries
       }
       st |= kStJitter;
     }
-    if (tries >= max_tries) {
+    if (tries >= max_tries) {  // the LU slot: z^T solve(X + eps I, z), partial pivoting
       st |= kStLu;
-      return acc;
+      T y[S];
+      for (int i = 0; i < S; ++i) y[i] = z[i];
+      if (!lu_sym_solve<T, S>([&](int i, int j) { return x0.at(i, j); }, S, eps, y))
+        return T(__builtin_nan(""));
+      T q = T(0);
+      for (int i = 0; i < S; ++i) q += z[i] * y[i];
+      return q;
     }
     eps *= T(10);
   }
