@@ -253,8 +253,7 @@ __device__ __forceinline__ void sym_spd_inverse(T (&r)[S], T* tile, int c, int m
       T x[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) x[i] = (i == c) ? T(1) : T(0);
-      const bool okl =
-          lu_sym_solve<T, S>([&](int i, int j) { return tile[i * kLdsRow + j]; }, S, eps, x);
+      const bool okl = lu_lds_solve<T>(tile, kLdsRow, S, T(0), eps, x) == 0;
 #pragma unroll
       for (int i = 0; i < S; ++i) r[i] = okl ? -x[i] : T(__builtin_nan(""));
     }

@@ -381,9 +381,7 @@ __device__ __forceinline__ void retry_inverse(double (&r)[S], const double* img,
       double x[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) x[i] = (i == c) ? 1.0 : 0.0;
-      const bool okl = lu_sym_solve<double, S>(
-          [&](int i, int j) { return img[i * LD + j] + ((OFFF && i == j) ? 1.0 : 0.0); }, S,
-          OFFF ? 0.0 : eps, x);
+      const bool okl = lu_lds_solve<double>(img, LD, S, OFFF ? 1.0 : 0.0, OFFF ? 0.0 : eps, x) == 0;
 #pragma unroll
       for (int i = 0; i < S; ++i)
         r[i] = okl ? ((OFFF && i == c) ? 1.0 : 0.0) - x[i] : __builtin_nan("");
@@ -489,8 +487,7 @@ __device__ __forceinline__ double quad_retry(double (&r)[S], double* tile, int c
       double y[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) y[i] = tile[S * kLdsRow + i];
-      const bool okl =
-          lu_sym_solve<double, S>([&](int i, int j) { return tile[i * kLdsRow + j]; }, S, eps, y);
+      const bool okl = lu_lds_solve<double>(tile, kLdsRow, S, 0.0, eps, y) == 0;
       double qq = 0.0;
 #pragma unroll
       for (int i = 0; i < S; ++i) qq += tile[S * kLdsRow + i] * y[i];
@@ -565,9 +562,7 @@ __device__ __forceinline__ void query_x0_ldl(double (&r)[S], const double (&H)[S
 #pragma unroll
       for (int i = 0; i < S; ++i) v[i] = H[i];
       bool okl = true;
-      if (lu)
-        okl = lu_sym_solve<double, S>(
-            [&](int i, int j) { return tile[i * kLdsRow + j] + (i == j ? 1.0 : 0.0); }, S, 0.0, v);
+      if (lu) okl = lu_lds_solve<double>(tile, kLdsRow, S, 1.0, 0.0, v) == 0;
       double Xl[S];
       copy(Xl, Eb);
       acc_xty<true>(Xl, H, v);  // Ebar - Fbar (Mt + eps I)^-1 Fbar^T

@@ -83,4 +83,20 @@ HOP_HD inline bool lu_sym_solve(F at, int n, T eps, T (&x)[S]) {
   return ok;
 }
 
+#ifdef __HIPCC__
+// The kernels' LU slot as an out-of-line call (a rare path: inlined, its private
+// arrays raised the register pressure of the sweep loops around it).
+// x (n values, private memory) <- (sym(M) + (diag + eps) I)^-1 x, M(i, j) = M[i ld + j]
+// in LDS; returns 0, or -1 on an exactly zero pivot.
+template <class T>
+__device__ __noinline__ int lu_lds_solve(const T* M, int ld, int n, T diag, T eps, T* x) {
+  T b[16];
+  for (int i = 0; i < 16; ++i) b[i] = i < n ? x[i] : T(0);
+  const bool ok = lu_sym_solve<T, 16>(
+      [&](int i, int j) { return M[i * ld + j] + (i == j ? diag : T(0)); }, n, eps, b);
+  for (int i = 0; i < n; ++i) x[i] = b[i];
+  return ok ? 0 : -1;
+}
+#endif
+
 }  // namespace hop
