@@ -1,6 +1,6 @@
 """Write profiles/traffic.json from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
-    python tools/make_traffic.py <prof_dir> <key> [kernel_substring[,substring...]]
+    python tools/make_traffic.py <prof_dir> <key> [kernel_substring[;substring...]]
 
 Several substrings (a step of more than one kernel: select + gains, the config-5
 buckets, J curve + argmin) sum their per-launch means: the traffic of one step.
@@ -32,7 +32,7 @@ def mean_counter(root, name, pat):
 
 def main():
     root, key = sys.argv[1], sys.argv[2]
-    pats = (sys.argv[3] if len(sys.argv) > 3 else "lft_sweep_v2_kernel").split(",")
+    pats = (sys.argv[3] if len(sys.argv) > 3 else "lft_sweep_v2_kernel").split(";")  # names hold commas
     fetch = write = 0.0
     nf, nw = [], []
     for pat in pats:
