@@ -152,6 +152,10 @@ struct SchedCondLNewt : SchedCondL {
 struct SchedCondLPeps : SchedCondL {
   static constexpr int SYM2 = 0, NEWT = 0, PEPS = 1;
 };
+// SYM2 + the reciprocal Newton without the one-block predict (49 measured slower)
+struct SchedCondLSN : SchedCondL {
+  static constexpr int SYM2 = 1, NEWT = 1, PEPS = 0;
+};
 // DMA placement A/B: DSTAG 1 = odd waves issue the step's pieces after the update
 // (the CU's waves no longer burst together); 2 = Q/QT pieces after the E sweep
 // (their images are read by then), A/B after the X sweep
@@ -179,6 +183,17 @@ constexpr bool has_newt() {
 template <class C>
 constexpr bool has_peps() {
   if constexpr (requires { C::PEPS; }) return C::PEPS != 0;
+  return false;
+}
+
+// fp32 blocks (config 5): the predict's two products A~ and A T on the f32 matrix
+// cores, one problem per v_mfma_f32_16x16x4_f32 tile
+struct SchedCondMfma : SchedCond {
+  static constexpr int MFMA = 1;
+};
+template <class C>
+constexpr bool has_mfma() {
+  if constexpr (requires { C::MFMA; }) return C::MFMA != 0;
   return false;
 }
 
@@ -1495,8 +1510,24 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
   const unsigned wlds = (unsigned)(uintptr_t)wbase;
   double* zarea = reinterpret_cast<double*>(wbase + G::OFF_T);
   const unsigned zaddr = wlds + G::OFF_T;
+  constexpr bool MF = has_mfma<C>();
+  static_assert(!MF || (F32 && S == 13 && MM == 4), "MFMA predict: fp32 blocks, s = 13");
+  // MFMA: the zero area grows to 2,112 B (a zero read for every problem's image
+  // offset, 3 x IMGM past it) and the f32 staging region follows it
+  constexpr int ZB = MF ? 2112 : 8 * (S * S + 8);
+  constexpr int MFB = 2112, MFP = 1152;  // staging region offset, bytes per problem
+  static_assert(!MF || (MFB + 4 * MFP <= G::TILE_W && 3 * G::IMGM + 4 <= ZB && G::IMGM == 688),
+                "MFMA staging in the tile slot");
 #pragma unroll 1
-  for (int i = lane; i < S * S + 8; i += 64) zarea[i] = 0.0;
+  for (int i = lane; i < ZB / 8; i += 64) zarea[i] = 0.0;
+  if constexpr (MF) {
+    float* mz = reinterpret_cast<float*>(wbase + G::OFF_T + MFB);
+#pragma unroll 1
+    for (int i = lane; i < 4 * MFP / 4; i += 64) mz[i] = 0.0f;
+    // A~[13][13] = 1 (the row carrying m'): one 1.0f per problem image offset, at a
+    // float index no other zero-area read uses (13 i and i, i < 13)
+    if (lane < 4) reinterpret_cast<float*>(zarea)[200 + lane * (G::IMGM / 4)] = 1.0f;
+  }
   // SYM2: eps I rows for the predict, read as element 15 + I - c of a zero-padded
   // vector holding eps at element 15 (after the zero area)
   constexpr int EPSV = 192;  // doubles from the zero area's start
@@ -1619,6 +1650,32 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
       tprev = t;
     }
   };
+
+  // MFMA operand addresses (loop-invariant; problem p at an immediate offset):
+  //   X staged as [p][row][17] f32 (row i of [Sigma' | m'] written by lane c = column);
+  //   prod 1 (T = X A~^T) k-slice kk: lane (g, c) carries k = 4 g + kk, A operand
+  //   X[c][k], B operand A~[c][k] (the A image; (13, 13): 1; else the zero area);
+  //   prod 2 (A T): A operand A[c][4 g + kk], B operand = register kk of T's
+  //   accumulator (row 4 g + kk, column c): the same k, no lane movement;
+  //   the result (row 4 g + r, column c) goes back as [p][column][18] f32.
+  unsigned mx_w = 0, mx_a = 0, ma_b[4] = {}, ma_a[4] = {}, ms_w = 0, ms_r = 0;
+  const unsigned lds0 = (unsigned)(uintptr_t)smem_raw;
+  auto lds_ptr = [&](unsigned ad) { return smem_raw + (ad - lds0); };
+  if constexpr (MF) {
+    const unsigned mfb = zaddr + MFB;
+    mx_w = mfb + g * MFP + 4u * c;
+    mx_a = mfb + 4u * (17 * c + 4 * g);
+    ms_w = mfb + 4u * (18 * c + 4 * g);
+    ms_r = mfb + g * MFP + 4u * 18 * c;
+    const unsigned ia = lds_addr(imA) - (unsigned)(g * G::IMGM);  // problem 0's image
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kx = 4 * g + kk;
+      const bool in = c < S && kx < S;
+      ma_b[kk] = in ? ia + 4u * (S * c + kx) : (c == S && kx == S ? zaddr + 800u : zaddr);
+      ma_a[kk] = in ? ia + 4u * (S * c + kx) : zaddr;
+    }
+  }
 
   dma_step(0);
   double best = 0.0, jprev = 0.0;
@@ -1771,7 +1828,43 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     {
       double Tm[S];
       double (&Xs)[S] = reinterpret_cast<double (&)[S]>(X);
-      if constexpr (has_peps<C>()) {
+      if constexpr (MF) {
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        // stage [Sigma' | m'] as f32 rows
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+          *reinterpret_cast<float*>(lds_ptr(mx_w + 68u * i)) = (float)X[i];
+        f4 D1[4], D2[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) D1[p] = D2[p] = (f4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const float xa = *reinterpret_cast<const float*>(lds_ptr(mx_a + p * MFP + 4u * kk));
+            const float ab = *reinterpret_cast<const float*>(lds_ptr(ma_b[kk] + p * G::IMGM));
+            D1[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, ab, D1[p], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const float aa = *reinterpret_cast<const float*>(lds_ptr(ma_a[kk] + p * G::IMGM));
+            D2[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa, D1[p][kk], D2[p], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          *reinterpret_cast<f2*>(lds_ptr(ms_w + p * MFP)) = (f2){D2[p][0], D2[p][1]};
+          *reinterpret_cast<f2*>(lds_ptr(ms_w + p * MFP + 8u)) = (f2){D2[p][2], D2[p][3]};
+        }
+        static_for<S>([&](auto I) {
+          X[I] = (double)*reinterpret_cast<const float*>(lds_ptr(ms_r + 4u * I)) +
+                 sel_lane<I>(0.0, 1e-9);
+        });
+      } else if constexpr (has_peps<C>()) {
         PredictEps<S>::run(Xs, Tm, at, ar, eps_addr);  // eps I + A [Sigma' | m'] A~^T
       } else {
       // T = [Sigma' | m'] A~^T; A~^T's row S is e_S, so its term is X masked to lane S
@@ -2208,6 +2301,8 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return launch(v2::lft_cond_kernel<v2::SchedCondLNewt, 13, 4>, bytes, a);
     case 49:  // the one-block predict with LDS eps rows alone, no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLPeps, 13, 4>, bytes, a);
+    case 52:  // the unhalved sums + the reciprocal Newton (47 + 48), no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLSN, 13, 4>, bytes, a);
     case 41:  // conditioned kernel without the rerun launch (A/B timing of it alone)
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
@@ -2237,16 +2332,24 @@ namespace hop {
 hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv || a.traj) return hipErrorNotSupported;
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
-  if (opt(HOP_OPT_REFERENCE_ASSOC) || (g_opt_variant != 0 && g_opt_variant != 40 &&
-                                       g_opt_variant != 41))
+  const int var = g_opt_variant;
+  if (opt(HOP_OPT_REFERENCE_ASSOC) ||
+      (var != 0 && var != 40 && var != 41 && (!kDevBuild || (var != 56 && var != 57))))
     return hipErrorNotSupported;
   using G = v2::Geo<13, 4, 4>;
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
   LftArgs<float> c = a;
   c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+#ifdef HOP_DEV
+  if (var == 56 || var == 57)  // the predict on the f32 matrix cores (SchedCondMfma)
+    hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondMfma, 13, 4, float>),
+                       dim3((unsigned)blocks), dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock),
+                       stream, c);
+  else
+#endif
   hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4, float>), dim3((unsigned)blocks),
                      dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
-  if (g_opt_variant == 41) return hipGetLastError();
+  if (var == 41 || var == 57) return hipGetLastError();
   LftArgs<float> r = a;
   r.cond = 1;
   return dispatch_lft<float>(r, stream);
