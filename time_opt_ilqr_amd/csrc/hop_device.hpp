@@ -136,6 +136,19 @@ __device__ __forceinline__ double row_sum_dpp(double v) {
   return v;
 }
 
+// Sum of lanes [0, N) of x, on every lane of the row: N DPP broadcast FMAs against
+// 1.0 (the reference's float(e @ (Q @ e)) style reductions).  fp64 DPP has only
+// row_newbcast on gfx950, so the rotate-and-add butterfly (row_sum_dpp) costs two
+// 32-bit DPP moves, their zero fills and an add per stage: 20 instructions against
+// N + 1 here.
+template <int N>
+__device__ __forceinline__ double lane_sum(double x) {
+  double acc = 0.0, one[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) one[j] = 1.0;
+  LaneDot<N>::fma(acc, x, one);
+  return acc;
+}
 // Sum over the 16 lanes of a row (every lane of the row gets the total).
 template <class T>
 __device__ __forceinline__ T row_sum(T v) {

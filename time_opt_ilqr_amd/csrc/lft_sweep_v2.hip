@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       for (int j = 0; j < NN; ++j) qr0[j] = c < NN ? Qg[cc * NN + j] : 0.0;
       LaneDot4<NN>::fma(q4, e0, qr0);
       qe_k = (q4[0] + q4[1]) + (q4[2] + q4[3]);
-      eqe_k = row_sum_dpp(c < NN ? e0 * qe_k : 0.0);
+      eqe_k = lane_sum<NN>(e0 * qe_k);
     }
     if (c < NN) {  // column c: _sym(Q) + q_reg I, and P (augmented.py:33, 82)
 #pragma unroll
@@ -1175,8 +1175,8 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
       atil = av - bd;
       stamp(12);
       // e^T Q e and e^T P e: row sums (lane NN's value is the one stored)
-      const double eqe1 = row_sum_dpp(in ? e1 * qe1 : 0.0);
-      const double epe = row_sum_dpp(in ? e1 * pe : 0.0);
+      const double eqe1 = lane_sum<NN>(e1 * qe1);
+      const double epe = lane_sum<NN>(e1 * pe);
       stamp(13);
       double* wq = const_cast<double*>(imQ);
       double* wt = const_cast<double*>(imT);
@@ -1422,7 +1422,7 @@ struct CondTraj {
       for (int j = 0; j < NN; ++j) qr0[j] = c < NN ? Qg[cc * NN + j] : 0.0;
       LaneDot4<NN>::fma(q4, e0, qr0);
       qe_k = (q4[0] + q4[1]) + (q4[2] + q4[3]);
-      eqe_k = row_sum_dpp(c < NN ? e0 * qe_k : 0.0);
+      eqe_k = lane_sum<NN>(e0 * qe_k);
     }
     if (c < NN) {  // column c: _sym(Q) + q_reg I, and P (augmented.py:33, 82)
 #pragma unroll
@@ -1469,8 +1469,8 @@ struct CondTraj {
     const double qe1 = (q4[0] + q4[1]) + (q4[2] + q4[3]);
     const double pe = (p4[0] + p4[1]) + (p4[2] + p4[3]);
     const double atil = av - bd;
-    const double eqe1 = row_sum_dpp(in ? e1 * qe1 : 0.0);
-    const double epe = row_sum_dpp(in ? e1 * pe : 0.0);
+    const double eqe1 = lane_sum<NN>(e1 * qe1);
+    const double epe = lane_sum<NN>(e1 * pe);
     if (c < NN) {
       wq[c * S + NN] = qe_k;
       wq[NN * S + c] = qe_k;
@@ -2076,7 +2076,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     double qr[NN];
     rows(lq, qr);
     lane_matvec<NN>(qe_k, e0, qr);
-    eqe_k = row_sum_dpp(in ? e0 * qe_k : 0.0);
+    eqe_k = lane_sum<NN>(e0 * qe_k);
   }
   double rinv[MM];
   {
@@ -2133,7 +2133,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       rows(lqi, Qi);
       double v;
       lane_matvec<NN>(v, qe_k, Qi);  // Qi q
-      const double qv = row_sum_dpp(in ? qe_k * v : 0.0);
+      const double qv = lane_sum<NN>(qe_k * v);
       const double sig = (((eqe_k + w2) + t.rho_reg) + eps) - qv;
       bad = bad || !(sig > 0.0);
       const double vp = in ? v : m1;
@@ -2151,7 +2151,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       rows(lq, qr);
       lane_matvec<NN>(qe1, e1, qr);
     }
-    const double eqe1 = row_sum_dpp(in ? e1 * qe1 : 0.0);
+    const double eqe1 = lane_sum<NN>(e1 * qe1);
     // ---- update: condition the prefix on stage k's cost
     {
       double Ht[S];
@@ -2183,7 +2183,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       double z;
       lane_matvec<NN>(z, e1, Pi);  // Pi e
       const double u = in ? e1 - eps * z : m1;  // Pi P e = e - eps Pi e
-      const double eu = row_sum_dpp(in ? e1 * u : 0.0);
+      const double eu = lane_sum<NN>(e1 * u);
       const double sig = (t.rho_reg + eps) + eps * eu;
       bad = bad || !(sig > 0.0);
       const double wq = u * recip_nr(sig);

@@ -371,6 +371,20 @@ __device__ __forceinline__ void lds_transpose<4>(const double (&x)[4], double (&
       : "memory");
 }
 
+// sum_r x[r] at lane r (the trace of a row-per-register 4 x 4 block), on every lane
+__device__ __forceinline__ double diag_sum4(const double (&x)[4]) {
+  double acc = 0.0;
+  const double one = 1.0;
+  asm(HOP_NOP2
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:0" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:1" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %0, %3, %5 row_newbcast:2" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:3" HOP_DPP_TAIL
+      : "+&v"(acc)
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(one));
+  return acc;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   const unsigned nrec = bytes > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)(bytes > 0 ? bytes : 0);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec,
@@ -520,7 +534,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     }
     vx = 0.0;
     LaneDot<S>::fma(vx, eT, qfrow);
-    v0 = 0.5 * row_sum_dpp(c < S ? eT * vx : 0.0);
+    v0 = 0.5 * lane_sum<S>(eT * vx);
     symmetrize(V, tile, c);
     if (alive && wantv) {  // the terminal expansion (plain stores, before the loop)
       double* o = a.Vxx + (pb * (NA + 1) + L) * (long long)(S * S);
@@ -606,7 +620,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     LaneDot<MM>::fma(lu, du, rrow);
     double l0 = 0.0;
     if constexpr (MODE == 1)
-      l0 = 0.5 * row_sum_dpp(c < S ? e * lx : 0.0) + 0.5 * row_sum_dpp(c < MM ? du * lu : 0.0) +
+      l0 = 0.5 * lane_sum<S>(e * lx) + 0.5 * lane_sum<MM>(du * lu) +
            a.w_stage;
     // Q-function: qab = [A|B]^T Vx; VA = V [A|B]; [A|B]^T V [A|B]
     double qab = 0.0;
@@ -664,10 +678,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
       for (int r = 0; r < MM; ++r) Qi[r] = ((c == r) ? 1.0 : 0.0) - rj[r];  // +(M+eps I)^-1
       bool ok0 = true;
       if constexpr (MODE == 0) {
-        double dg = 0.0;  // this lane's diagonal entry of (M + eps I)^-1
-#pragma unroll
-        for (int r = 0; r < MM; ++r) dg = (c == r) ? Qi[r] : dg;
-        const double tr = row_sum_dpp(dg);
+        const double tr = diag_sum4(Qi);  // trace((M + eps I)^-1)
         const bool sure = okj && (tr < 1e6);
         if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
           double rc[MM];
@@ -742,7 +753,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
         ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);
       });
       LaneDot<MM>::fma(vxn, kv, Qux);             // Qx - Qux^T Quu^-1 Qu
-      v0n = l0 + v0 + 0.5 * row_sum_dpp(c < MM ? qu * kv : 0.0);
+      v0n = l0 + v0 + 0.5 * lane_sum<MM>(qu * kv);
     }
     stamp(9);
     lds_park12(Vn, twa);  // its transpose is read with the next step's image

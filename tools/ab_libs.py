@@ -53,6 +53,17 @@ def main():
     for md in (0, 1):
         work[f"riccati_mode{md}"] = (lambda md=md: engine.riccati(
             rA, rB, rX, rU, xg, ur, rQ, rR, rQf, N, 1e-3, mode=md).K)
+    # the brute-force J curve (bench --workload bruteforce shape) and the select
+    # block's closed-form trajectory kernel (bench --workload select_gains)
+    jX = 0.5 * torch.randn((Bn, N + 1, n), **kw)
+    jU = 0.3 * torch.randn((Bn, N, m), **kw)
+    jxg, jur = 0.2 * torch.randn((n,), **kw), 0.1 * torch.randn((m,), **kw)
+    work["bruteforce_jcurve"] = lambda: engine.bruteforce_jcurve(
+        rA, rB, jX, jU, jxg, jur, rQ, rR, rQf, N, lm_lambda=1e-6, w_stage=0.5)[0]
+    ares = 0.02 * torch.randn((Bn, N, n), **kw)
+    rRi = torch.linalg.inv(rR)
+    work["select_traj_cf"] = lambda: engine.propagate_traj(
+        rA, rB, ares, jX, jU, jxg, jur, rQ, rRi, rQf, 0.5, t_min=40, t_max=N, rho_reg=1.0).J
     from time_opt_ilqr_amd import systems
     F, x0, xg_q, ur_q, *_ = systems.make_quadrotor(N=100)
     Uq = torch.as_tensor(ur_q, device=dev) + 0.05 * torch.randn((4096, 100, 4), **kw)
