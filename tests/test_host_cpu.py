@@ -716,3 +716,14 @@ def test_lu_slot_pivoting_host_build(small_host, golden_dir):
         ref = np.linalg.solve(0.5 * (A + A.T) + 1e-3 * np.eye(n), np.eye(n))
         got = inv(A, 1e-3)
         assert np.max(np.abs(got - ref)) <= 1e-10 * np.max(np.abs(ref)), n
+
+
+def test_mfma_predict_lane_maps_emulated():
+    """The fp32-block kernel's MFMA predict (SchedCondMfma): LDS staging addresses, the
+    v_mfma_f32_16x16x4_f32 operand / result lane maps and the write-back, emulated for
+    one wave of 4 problems (tools/emu_mfma_predict.py), give A [Sigma' | m'] A~^T to
+    f32 rounding; lanes 14, 15 come back 0."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_mfma_predict as emu
+    assert emu.main() < 5e-7

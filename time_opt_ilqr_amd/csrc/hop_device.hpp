@@ -111,9 +111,11 @@ __device__ __forceinline__ void transpose(T (&dst)[S], const T (&src)[S], T* til
 // of one lane only.
 template <int ROR>
 __device__ __forceinline__ double ror_row(double v) {
+  // a rotation within the row reads only enabled lanes, so no "old" value is ever
+  // kept: mov_dpp (undefined old) spares the zero fill update_dpp(0, ...) costs
   const int2 w = __builtin_bit_cast(int2, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, w.x, 0x120 + ROR, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x120 + ROR, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(w.x, 0x120 + ROR, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(w.y, 0x120 + ROR, 0xf, 0xf, false);
   return __builtin_bit_cast(double, make_int2(lo, hi));
 }
 template <int ROR>

@@ -143,8 +143,11 @@ struct SchedCondL2Stamped : SchedCondL2 {
   static constexpr int STAMP = 1;
 };
 // the three parts of SchedCondL2 alone (developer A/B)
-struct SchedCondLSym : SchedCondL {
+struct SchedCondLSym : SchedCondL {  // the default since round 3
   static constexpr int SYM2 = 1, NEWT = 0, PEPS = 0;
+};
+struct SchedCondLSymStamped : SchedCondLSym {
+  static constexpr int STAMP = 1;
 };
 struct SchedCondLNewt : SchedCondL {
   static constexpr int SYM2 = 0, NEWT = 1, PEPS = 0;
@@ -1512,11 +1515,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
   const unsigned zaddr = wlds + G::OFF_T;
   constexpr bool MF = has_mfma<C>();
   static_assert(!MF || (F32 && S == 13 && MM == 4), "MFMA predict: fp32 blocks, s = 13");
-  // MFMA: the zero area grows to 2,112 B (a zero read for every problem's image
-  // offset, 3 x IMGM past it) and the f32 staging region follows it
-  constexpr int ZB = MF ? 2112 : 8 * (S * S + 8);
-  constexpr int MFB = 2112, MFP = 1152;  // staging region offset, bytes per problem
-  static_assert(!MF || (MFB + 4 * MFP <= G::TILE_W && 3 * G::IMGM + 4 <= ZB && G::IMGM == 688),
+  // MFMA: the zero area grows to 2,880 B (a zero and a 1.0f for every problem's
+  // image offset p * IMGM, p < 4) and the f32 staging region follows it
+  constexpr int ZB = MF ? 2880 : 8 * (S * S + 8);
+  constexpr int MFB = 2880, MFP = 1152;  // staging region offset, bytes per problem
+  static_assert(!MF || (MFB + 4 * MFP <= G::TILE_W && 800 + 3 * G::IMGM + 4 <= ZB &&
+                        G::IMGM == 688),
                 "MFMA staging in the tile slot");
 #pragma unroll 1
   for (int i = lane; i < ZB / 8; i += 64) zarea[i] = 0.0;
@@ -2279,7 +2283,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, a);
 #ifdef HOP_DEV
   switch (variant) {
-    case 42:  // stamps (tools/stamps.py --cond), no rerun
+    case 42:  // stamps of the default (tools/stamps.py --cond), no rerun
+      return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
+    case 59:  // stamps of the round-2 default (halved sums), no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes, a);
     case 43:  // image reads not overlapped with the sweeps, no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCond, 13, 4>, bytes, a);
@@ -2295,7 +2301,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return launch(v2::lft_cond_kernel<v2::SchedCondLStag1, 13, 4>, bytes, a);
     case 51:  // DMA: Q/QT after the E sweep, A/B after the X sweep, no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLStag2, 13, 4>, bytes, a);
-    case 47:  // the unhalved sums alone, no rerun
+    case 47:  // the unhalved sums alone (the default's kernel), no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>, bytes, a);
     case 48:  // the update's Newton on the reciprocal alone, no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLNewt, 13, 4>, bytes, a);
@@ -2303,9 +2309,11 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return launch(v2::lft_cond_kernel<v2::SchedCondLPeps, 13, 4>, bytes, a);
     case 52:  // the unhalved sums + the reciprocal Newton (47 + 48), no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLSN, 13, 4>, bytes, a);
-    case 41:  // conditioned kernel without the rerun launch (A/B timing of it alone)
-      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
+    case 41:  // the default's conditioned kernel without the rerun launch (A/B timing)
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
+    case 58:  // round-2 default (halved symmetric sums) without the rerun launch
+      return launch(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>, bytes, a);
     case 2: return launch(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes, a);
     case 8: return launch(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes, a);
     case 10: return launch(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes, a);
@@ -2316,10 +2324,12 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     default: break;
   }
   if (opt(HOP_OPT_STAMPS))
-    return launch(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes, a);
+    return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
 #endif
-  // default (variant 40): conditioned prefix + rerun of the problems it flagged
-  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>,
+  // default (variant 40): conditioned prefix + rerun of the problems it flagged; the
+  // stage / terminal inverses of the unhalved symmetric sums (SYM2: 1-2 % faster than
+  // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_pb_dev_ab.txt)
+  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
                     v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
 }
 
