@@ -209,6 +209,20 @@ constexpr bool has_arow() {
 struct SchedCondTraj : SchedLdlDma {
   static constexpr int TRAJ = 1;
 };
+// fused hand-over: a wave whose problems the conditioned kernel flagged recomputes
+// them with the reference association (lft_v2_body) at the end of the same launch,
+// instead of a second (rerun) launch that every wave enters to read its status
+struct SchedCondLSymF : SchedCondLSym {
+  static constexpr int FUSE = 1;
+};
+struct SchedCondTrajF : SchedCondTraj {
+  static constexpr int FUSE = 1;
+};
+template <class C>
+constexpr bool has_fuse() {
+  if constexpr (requires { C::FUSE; }) return C::FUSE != 0;
+  return false;
+}
 template <class C>
 constexpr bool has_traj() {
   if constexpr (requires { C::TRAJ; }) return C::TRAJ != 0;
@@ -874,8 +888,12 @@ __device__ __forceinline__ unsigned chunk_voff(int j, int lane, long long wave_p
   return (q < kProbPerWave * CH) ? (unsigned)((pe - pb0) * pstr + r * 16) : 0x7FFFFFFFu;
 }
 
+// The exact-size LFT sweep of one wave's 4 problems (the kernel below).  need: -1 =
+// a.cond's semantics (rerun launch: the problems whose status carries ST_RERUN);
+// 0 / 1 = this lane's problem is (not) recomputed -- the conditioned kernel's fused
+// hand-over passes its own flags here instead of a second launch.
 template <class C, int S, int MM>
-__global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a) {
+__device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
   using G = Geo<S, MM>;
   constexpr bool OFF = offset_form<C>();
   constexpr bool TRAJ = has_traj<C>();
@@ -899,7 +917,10 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   const long long wave_prob0 = ((long long)blockIdx.x * kWavesPerBlock + w) * kProbPerWave;
   const long long prob = wave_prob0 + g;
   bool valid = prob < a.batch;
-  if (a.cond & 1) {  // rerun launch after SchedCond: only the problems it handed over
+  if (need_in >= 0) {  // fused hand-over: the caller's flags
+    valid = valid && need_in != 0;
+    if (!__any(valid)) return;
+  } else if (a.cond & 1) {  // rerun launch after SchedCond: only the problems it handed over
     const bool need = valid && (a.status[prob] & (int)ST_RERUN);
     if (!__any(need)) return;  // wave-uniform; no workgroup barrier in this kernel
     valid = need;
@@ -1324,6 +1345,11 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
   }
 }
 
+template <class C, int S, int MM>
+__global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a) {
+  lft_v2_body<C, S, MM>(a, -1);
+}
+
 
 // ===========================================================================
 // SchedCond: the same J(t) by the conditioned prefix (z0 eliminated first).
@@ -1708,6 +1734,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     double NE[S], NX[S];
     double at[S + 1], brow[MM];  // at[j] = column j of A~ (lanes > S-1: 0), at[S] = e_S
     double ar[has_arow<C>() ? S : 1];  // AROW: rows of A_k, read before the image is refilled
+    float mb[MF ? 4 : 1][4], ma[MF ? 4 : 1][4];  // MFMA predict operands (likewise)
     stamp(1);
     if constexpr (has_ldspipe<C>() && !TRAJ) {
       // QT's sym reads ride under the E sweep, A_k / B_k's under the X sweep
@@ -1767,7 +1794,17 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
     }
     stamp(3);
-    if constexpr (has_arow<C>()) {
+    // MFMA: the A~ / A operands of the predict's two products, read here because the
+    // step's DMA (issued below, before the update) refills the A image
+    if constexpr (MF) {
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          mb[kk][p] = *reinterpret_cast<const float*>(lds_ptr(ma_b[kk] + p * G::IMGM));
+          ma[kk][p] = *reinterpret_cast<const float*>(lds_ptr(ma_a[kk] + p * G::IMGM));
+        }
+    } else if constexpr (has_arow<C>()) {
       const T* pr = imA + c;  // lanes > S-1 read the next row: unused (bcast_j, j < S)
 #pragma unroll
       for (int i = 0; i < S; ++i) ar[i] = (double)pr[i * S];
@@ -1847,16 +1884,14 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
             const float xa = *reinterpret_cast<const float*>(lds_ptr(mx_a + p * MFP + 4u * kk));
-            const float ab = *reinterpret_cast<const float*>(lds_ptr(ma_b[kk] + p * G::IMGM));
-            D1[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, ab, D1[p], 0, 0, 0);
+            D1[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa, mb[kk][p], D1[p], 0, 0, 0);
           }
         }
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
 #pragma unroll
           for (int p = 0; p < 4; ++p) {
-            const float aa = *reinterpret_cast<const float*>(lds_ptr(ma_a[kk] + p * G::IMGM));
-            D2[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(aa, D1[p][kk], D2[p], 0, 0, 0);
+            D2[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(ma[kk][p], D1[p][kk], D2[p], 0, 0, 0);
           }
         }
 #pragma unroll
@@ -1935,6 +1970,16 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = (T)best;
+    }
+  }
+  if constexpr (has_fuse<C>()) {
+    static_assert(!F32, "fused hand-over: fp64 blocks");
+    const bool hand = valid && bad;
+    if (__any(hand)) {  // wave-uniform; the rerun body uses this wave's LDS only
+      LftArgs<double> r = a;
+      r.cond = 1;
+      using RC = std::conditional_t<TRAJ, SchedLdlTraj, SchedLdlDma>;
+      lft_v2_body<RC, S, MM>(r, hand ? 1 : 0);
     }
   }
 }
@@ -2230,6 +2275,14 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       a.j_star[prob] = best;
     }
   }
+  if constexpr (has_fuse<C>()) {  // the fused hand-over (see SchedCondTrajF)
+    const bool hand = valid && bad;
+    if (__any(hand)) {
+      LftArgs<double> r = a;
+      r.cond = 1;
+      lft_v2_body<SchedLdlTraj, S, MM>(r, hand ? 1 : 0);
+    }
+  }
 }
 
 }  // namespace v2
@@ -2272,10 +2325,17 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
                         v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, variant == 40);
     if (variant == 24 || opt(HOP_OPT_STAMPS))  // section stamps (tools/stamps.py --traj)
       return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlTrajStamped, 13, 4>, bytes, a);
+    if (variant == 61)  // closed-form kernel + a separate rerun launch (round-2 default)
+      return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
 #endif
-    // default: closed-form stage inverses + rerun
-    return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
-                      v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
+    // default: closed-form stage inverses, flagged problems recomputed in the same
+    // launch (fused hand-over)
+    {
+      LftArgs<double> c = a;
+      c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+      return launch(v2::lft_cond_cf_kernel<v2::SchedCondTrajF, 13, 4>, bytes, c);
+    }
   }
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
   constexpr size_t bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
@@ -2314,6 +2374,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
     case 58:  // round-2 default (halved symmetric sums) without the rerun launch
       return launch(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>, bytes, a);
+    case 60:  // the default's kernel + a separate rerun launch (unfused hand-over)
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
     case 2: return launch(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes, a);
     case 8: return launch(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes, a);
     case 10: return launch(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes, a);
@@ -2326,11 +2389,13 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (opt(HOP_OPT_STAMPS))
     return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
 #endif
-  // default (variant 40): conditioned prefix + rerun of the problems it flagged; the
+  // default (variant 40): conditioned prefix, the problems it flagged recomputed with
+  // the reference association at the end of the same launch (fused hand-over); the
   // stage / terminal inverses of the unhalved symmetric sums (SYM2: 1-2 % faster than
-  // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_pb_dev_ab.txt)
-  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
-                    v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
+  // the halved sums, profiles/r03_ab1_cond_schedules.txt)
+  LftArgs<double> c = a;
+  c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+  return launch(v2::lft_cond_kernel<v2::SchedCondLSymF, 13, 4>, bytes, c);
 }
 
 }  // namespace hop

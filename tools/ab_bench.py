@@ -49,8 +49,9 @@ def main():
         rel = float(((r.J - ref).abs() / ref.abs()).max())
         print(f"variant {v}: max rel vs first = {rel:.3e}", flush=True)
     times = {v: [] for v in variants}
-    for _ in range(args.rounds):
-        for v in variants:
+    for rnd in range(args.rounds):
+        # alternate the order every round (the first timing of a round can be biased)
+        for v in (variants if rnd % 2 == 0 else variants[::-1]):
             setv(v)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()

@@ -9,7 +9,7 @@ set -o pipefail
 OUT=gpurun_out/$1
 mkdir -p $OUT
 export TMPDIR=/tmp HOP_DEV_BUILD=1 HOP_LIB=$PWD/time_opt_ilqr_amd/libhop_amd_dev.so
-timeout -k 10 300 python -u tools/ab_bench.py --variants 41,52,47,48 --rounds 9 --iters 10 > $OUT/ab_c2.log 2>&1 && \
+timeout -k 10 300 python -u tools/ab_bench.py --variants 0,60,58,52 --rounds 10 --iters 10 > $OUT/ab_c2.log 2>&1 && \
 timeout -k 10 300 python -u tools/ab_bench.py --variants 41,57 --rounds 9 --iters 10 --dtype f32 --N 128 --batch 5462 > $OUT/ab_c5_s13.log 2>&1 && \
 timeout -k 10 300 python -u tools/ab_bench.py --variants 0,56,41,57 --rounds 7 --iters 5 --dtype f32 --N 128 --batch 16384 > $OUT/ab_c5_pad.log 2>&1 && \
 timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 120 --timeout-method thread -k "mfma or config5" > $OUT/pytest_mfma.log 2>&1 && \
