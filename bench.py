@@ -56,7 +56,7 @@ def kernel_path(s, m, dtype):
     The s=13 kernels are compute-bound on the fp64 pipe (MI355X: vector fp64 peak ==
     matrix fp64 peak); they issue DPP-broadcast FMAs, not MFMA."""
     if dtype == "f64" and (s, m) == (13, 4):
-        return "lft_cond_kernel<SchedCondL,13,4>", "fp64"
+        return "lft_cond_kernel<SchedCondLSym,13,4>", "fp64"
     if dtype == "f32" and (s, m) == (13, 4):
         return "lft_cond_kernel<SchedCond,13,4,float>", "fp64"  # fp32 blocks, fp64 arithmetic
     if (s, m) in SMALL_SHAPES[dtype]:

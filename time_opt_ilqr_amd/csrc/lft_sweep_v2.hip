@@ -2325,17 +2325,15 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
                         v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, variant == 40);
     if (variant == 24 || opt(HOP_OPT_STAMPS))  // section stamps (tools/stamps.py --traj)
       return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlTrajStamped, 13, 4>, bytes, a);
-    if (variant == 61)  // closed-form kernel + a separate rerun launch (round-2 default)
-      return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
-                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
-#endif
-    // default: closed-form stage inverses, flagged problems recomputed in the same
-    // launch (fused hand-over)
-    {
+    if (variant == 61) {  // the fused hand-over (measured slower)
       LftArgs<double> c = a;
       c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
       return launch(v2::lft_cond_cf_kernel<v2::SchedCondTrajF, 13, 4>, bytes, c);
     }
+#endif
+    // default: closed-form stage inverses + rerun
+    return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
+                      v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
   }
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
   constexpr size_t bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
@@ -2374,9 +2372,13 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
     case 58:  // round-2 default (halved symmetric sums) without the rerun launch
       return launch(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>, bytes, a);
-    case 60:  // the default's kernel + a separate rerun launch (unfused hand-over)
-      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
-                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
+    case 60: {  // fused hand-over: flagged problems recomputed at the end of the same
+                // launch (lft_v2_body); the kernel then carries the LFT body's scratch and
+                // measured 0.7-2 % slower than the default's second launch
+      LftArgs<double> c = a;
+      c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+      return launch(v2::lft_cond_kernel<v2::SchedCondLSymF, 13, 4>, bytes, c);
+    }
     case 2: return launch(v2::lft_sweep_v2_kernel<v2::Select, 13, 4>, bytes, a);
     case 8: return launch(v2::lft_sweep_v2_kernel<v2::Chain, 13, 4>, bytes, a);
     case 10: return launch(v2::lft_sweep_v2_kernel<v2::Sched, 13, 4>, bytes, a);
@@ -2389,13 +2391,11 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (opt(HOP_OPT_STAMPS))
     return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
 #endif
-  // default (variant 40): conditioned prefix, the problems it flagged recomputed with
-  // the reference association at the end of the same launch (fused hand-over); the
+  // default (variant 40): conditioned prefix + rerun of the problems it flagged; the
   // stage / terminal inverses of the unhalved symmetric sums (SYM2: 1-2 % faster than
-  // the halved sums, profiles/r03_ab1_cond_schedules.txt)
-  LftArgs<double> c = a;
-  c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
-  return launch(v2::lft_cond_kernel<v2::SchedCondLSymF, 13, 4>, bytes, c);
+  // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_ab_pe.txt)
+  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
+                    v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
 }
 
 }  // namespace hop
