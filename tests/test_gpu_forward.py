@@ -584,8 +584,9 @@ def test_integration_md_ctypes_stubs_run(dev):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     text = open(os.path.join(repo, "INTEGRATION.md")).read()
     blocks = [b for b in re.findall(r"```python\n(.*?)```", text, re.S)
-              if "hop_lft_sweep_f64" in b or "hop_bruteforce_jcurve_f64" in b]
-    assert len(blocks) == 2
+              if "hop_lft_sweep_f64" in b or "hop_bruteforce_jcurve_f64" in b
+              or "hop_bruteforce_jcurve_legacy_f64" in b]
+    assert len(blocks) == 3
     ns = {}
     code = "\n".join(blocks).replace("/path/to/time_opt_ilqr_amd/libhop_amd.so", _lib.LIB_PATH)
     exec(compile(code, "INTEGRATION.md", "exec"), ns)
@@ -602,6 +603,13 @@ def test_integration_md_ctypes_stubs_run(dev):
                                       _t(ur, dev), _t(Q, dev), _t(R, dev), _t(Qf, dev), N,
                                       w_stage=0.1)
     assert np.array_equal(J, _np(Je)) and np.array_equal(st, _np(se)) and (st == 0).all()
+    # the legacy twin's brute force (ilqr_propagator.py:426-454), Qf = alpha I
+    Jg, sg = ns["legacy_bruteforce_all_Jt_batched"](A, Bm, X, U, xg, ur, Q, R, 10.0, N, 0.1)
+    Jge, sge = engine.bruteforce_jcurve(_t(A, dev), _t(Bm, dev), _t(X, dev), _t(U, dev),
+                                        _t(xg, dev), _t(ur, dev), _t(Q, dev), _t(R, dev),
+                                        _t(10.0 * np.eye(n), dev), N, w_stage=0.1, legacy=True)
+    assert np.array_equal(Jg, _np(Jge)) and np.array_equal(sg, _np(sge))
+    assert np.allclose(Jg, J, rtol=1e-9)  # well-conditioned: the legacy solve is the same
     from oracle import hop_oracle as orc
     Aa, Ba, Qa, Ra, Ri, z0, QT = orc.synth_lft_batch(40, 2, 5, 1, 16)
     Jl, stl, tsl = ns["propagator_all_Jt_aug_batched"](Aa, Ba, Qa, Ri[0], z0[0], QT, 16, 3, 16)
