@@ -860,10 +860,21 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
 // the same jc_tmax + 1 steps (11 % faster than one horizon per workgroup, longest
 // first) and a block's horizons sit in adjacent workgroups (its A, B, x, u re-reads
 // meet in the caches)
+// XCD: workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
+// dispatch), so consecutive ids -- one problem block's horizons -- land on 8 different
+// L2s and each re-reads the block's A, B, x, u from HBM.  The remap gives the ids an
+// XCD receives (w = x, x + 8, x + 16, ...) consecutive logical ids, so a block's
+// horizons share one L2.
+template <bool XCD>
 __global__ __launch_bounds__(256, 1) void riccati_fast_jcurve_kernel(RiccatiArgs<double> a) {
   const unsigned P = (unsigned)((a.jc_tmax + 1) / 2);
-  const int h = (int)(blockIdx.x % P);
-  const long long blk = (long long)(blockIdx.x / P);
+  unsigned w = blockIdx.x;
+  if constexpr (XCD) {
+    const unsigned G8 = gridDim.x / 8u * 8u;  // a remainder keeps its ids
+    if (w < G8) w = (w % 8u) * (G8 / 8u) + w / 8u;
+  }
+  const int h = (int)(w % P);
+  const long long blk = (long long)(w / P);
   ric_body<1, false, false, 0, true>(a, blk, a.jc_tmax - h);
   if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true>(a, blk, h + 1);
 }
@@ -907,9 +918,15 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
   if (4 * (NA + 1) * ricf::NX * ricf::NX * 8 >= 0x7FFF0000ll) return hipErrorNotSupported;
   if (a.jc_J) {  // the J-curve form: one launch, ceil(jc_tmax / 2) workgroups per block
     const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
-    hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel,
-                       dim3((unsigned)(blocks * ((a.jc_tmax + 1) / 2))), dim3(256),
-                       (size_t)kWavesPerBlock * ricf::WAVE_BYTES, stream, a);
+    const dim3 grid((unsigned)(blocks * ((a.jc_tmax + 1) / 2)));
+    const size_t lds = (size_t)kWavesPerBlock * ricf::WAVE_BYTES;
+#ifdef HOP_DEV
+    if (g_opt_variant == 83) {  // XCD-grouped horizons (A/B)
+      hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel<true>, grid, dim3(256), lds, stream, a);
+      return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel<false>, grid, dim3(256), lds, stream, a);
     return hipGetLastError();
   }
   if (a.mode == 1) return ricf::launch<1, true>(a, stream);
