@@ -456,7 +456,9 @@ def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default per workload: about 2-5 s of GPU time, so the "
+                         "run's GPU phase is long enough to observe; 20 when N > 1)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="lft")
     ap.add_argument("--batch", type=int, default=None,
@@ -512,6 +514,9 @@ def main(argv=None):
             "config5": (16384, 13, 4, 128, "f32"),
             "select_gains": (4096, 13, 4, 100, "f64"),
             "bruteforce": (4096, 13, 4, 100, "f64")}[wl]
+    if args.steps is None:  # ~2-5 s of timed GPU work at N = 1 (config 2: 10,000 x 0.48 ms)
+        args.steps = 20 if world > 1 else {"lft": 10000, "config3": 5000, "config5": 3000,
+                                           "select_gains": 10000, "bruteforce": 300}[wl]
     args.batch_given = args.batch
     args.batch = args.batch or dflt[0]
     args.s = args.s or dflt[1]
@@ -638,7 +643,7 @@ def main(argv=None):
         for _ in range(3):
             launch_a()
         sync()
-        ka = max(3, K // 4)
+        ka = min(max(3, K // 4), 50)
         ta = time.perf_counter()
         for _ in range(ka):
             launch_a()
