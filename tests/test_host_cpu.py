@@ -727,3 +727,45 @@ def test_mfma_predict_lane_maps_emulated():
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import emu_mfma_predict as emu
     assert emu.main() < 5e-7
+
+
+def test_packed_sweep_colchain_block_emulated():
+    """SweepQColChainOff<4, 12, 12> (the Riccati kernel's packed [Qux | Quu] rows: the
+    4 x 4 block on lanes 12..15 in offset form, the RHS Qux on lanes 0..11): one
+    Gauss-Jordan sweep leaves (M + eps I)^-1 Qux on lanes 0..11 and I - (M + eps I)^-1
+    on lanes 12..15, and the fused column chains acc[r] += sum_j x[j]@r * y[j]
+    (CPU emulation of the instruction strings, tools/emu_dpp.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(41)
+    M = rng.standard_normal((4, 4))
+    M = M @ M.T + 4 * np.eye(4)
+    Y = rng.standard_normal((4, 12))
+    eps = 1e-9
+    regs = {}
+    for r in range(4):
+        v = np.empty(16)
+        v[:12] = Y[r]
+        v[12:] = M[r]
+        v[12 + r] += eps - 1.0
+        regs[r] = v
+    regs[4] = np.ones(16)
+    for j in range(7):
+        regs[5 + j] = np.full(16, np.nan)
+    acc0 = rng.standard_normal((12, 16))
+    X = rng.standard_normal((12, 16))
+    Yc = rng.standard_normal((12, 16))
+    for j in range(12):
+        regs[12 + j], regs[24 + j], regs[36 + j] = acc0[j].copy(), X[j], Yc[j]
+    E.run(E.extract(inc, "SweepQColChainOff", "4, 12, 12"), regs)
+    Mi = np.linalg.inv(M + eps * np.eye(4))
+    got_y = np.array([regs[r][:12] for r in range(4)])
+    got_i = np.array([regs[r][12:] for r in range(4)])
+    assert np.abs(got_y - Mi @ Y).max() < 1e-12
+    assert np.abs(got_i - (np.eye(4) - Mi)).max() < 1e-12
+    assert regs[4][0] > 0
+    for r in range(12):
+        want = acc0[r] + sum(X[j][r] * Yc[j] for j in range(12))
+        assert np.abs(regs[12 + r] - want).max() < 1e-12

@@ -385,6 +385,55 @@ __device__ __forceinline__ double diag_sum4(const double (&x)[4]) {
   return acc;
 }
 
+// Packed rows (PK): P[r] = [Qux row r (lanes 0..11) | Quu row r (lanes 12..15)].  The
+// transpose of the 4 x 4 block for _sym(Quu), in ONE asm statement: the rows are
+// written a second time with lane 12 + x's entries at row 12 + x, column r (an
+// immediate stride of 8; lanes < 12 write into row 0, which the plain row writes that
+// follow overwrite), then read back with a stride of 136: lanes < 12 see their own
+// Qux entries, lanes 12 + j see P[j][12 + r], the transpose.
+__device__ __forceinline__ void lds_sym_packed4(const double (&x)[4], double (&t)[4], unsigned wa,
+                                                unsigned wt, unsigned rt) {
+  asm volatile(
+      "ds_write_b64 %5, %7 offset:0\n\t"
+      "ds_write_b64 %5, %8 offset:8\n\t"
+      "ds_write_b64 %5, %9 offset:16\n\t"
+      "ds_write_b64 %5, %10 offset:24\n\t"
+      "ds_write_b64 %4, %7 offset:0\n\t"
+      "ds_write_b64 %4, %8 offset:136\n\t"
+      "ds_write_b64 %4, %9 offset:272\n\t"
+      "ds_write_b64 %4, %10 offset:408\n\t"
+      "ds_read_b64 %0, %6 offset:0\n\t"
+      "ds_read_b64 %1, %6 offset:136\n\t"
+      "ds_read_b64 %2, %6 offset:272\n\t"
+      "ds_read_b64 %3, %6 offset:408\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
+      : "v"(wa), "v"(wt), "v"(rt), "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3])
+      : "memory");
+}
+// sum of lanes [OFF, OFF + N) of x on every lane of the row
+template <int N, int OFF>
+__device__ __forceinline__ double lane_sum_off(double x) {
+  double acc = 0.0, one[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) one[j] = 1.0;
+  LaneDotOff<N, OFF>::fma(acc, x, one);
+  return acc;
+}
+// sum_r x[r] at lane 12 + r (the trace of the packed 4 x 4 block)
+__device__ __forceinline__ double diag_sum4_off12(const double (&x)[4]) {
+  double acc = 0.0;
+  const double one = 1.0;
+  asm(HOP_NOP2
+      "v_fmac_f64_dpp %0, %1, %5 row_newbcast:12" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %0, %2, %5 row_newbcast:13" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %0, %3, %5 row_newbcast:14" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:15" HOP_DPP_TAIL
+      : "+&v"(acc)
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(one));
+  return acc;
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   const unsigned nrec = bytes > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)(bytes > 0 ? bytes : 0);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec,
@@ -403,7 +452,12 @@ __device__ unsigned long long g_ricf_stamp[16];
 // the stores, 2 the per-step LDS-DMA.  JC: the J-curve form (mode 1 at horizon jl for
 // the whole wave, no K / k / V stores; RiccatiArgs::jc_J).  blk: the workgroup's
 // problem block.
-template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC>
+// PK (packed rows, default): [Qux | Quu] of row r of B^T V [A|B] + R share one 16-lane
+// register (Quu on lanes 12..15), so the offset-form 4 x 4 sweep leaves
+// (Quu_reg + eps I)^-1 Qux = -K on lanes 0..11 directly: no K product, no lane
+// rotations of Quu, no inverse rebuilt from the sweep's offset form; Qu, k and R du
+// live on lanes 12..15 likewise.  PK = false keeps the round-2 form (developer A/B).
+template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC, bool PK = true>
 __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long blk, int jl) {
   constexpr int S = NX, MM = MU;
   unsigned long long sec[12] = {};
@@ -471,11 +525,11 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     ad[j] = wlds + (c < S ? OFF_A + 1152 * g + 8 * c + 96 * j
                           : OFF_B + 384 * g + 8 * (c - S) + 32 * j);
   const unsigned xa = wlds + OFF_X + 96 * g + 8 * (c < S ? c : 0);
-  const unsigned ua = wlds + OFF_U + 32 * g + 8 * (c < MM ? c : 0);
+  const unsigned ua = wlds + OFF_U + 32 * g + 8 * (c < MM ? c : ((PK && c >= S) ? c - S : 0));
   // per-lane store offsets (problem part; the step part is the scalar offset)
   const unsigned pofs = (unsigned)(pb - pb0);
   const unsigned voK = pofs * (unsigned)pK + 8u * (c < S ? c : 0);
-  const unsigned vok = pofs * (unsigned)pk + 8u * (c < MM ? c : 0);
+  const unsigned vok = pofs * (unsigned)pk + 8u * (c < MM ? c : ((PK && c >= S) ? c - S : 0));
 
   const double* xgp = a.xg + pb * a.xg_bstride;
   const double* urp = a.u_ref + pb * a.uref_bstride;
@@ -508,7 +562,20 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     rrow[i] = c < MM ? Rp[cr * MM + i] : ((i == c) ? 1.0 : 0.0);
   }
   const double xg_c = c < S ? xgp[cq] : 0.0;
-  const double ur_c = c < MM ? urp[cr] : 0.0;
+  // PK: u and u_ref ride on lanes 12..15 as well (du, R du, Qu, k of the packed rows)
+  const double ur_c = c < MM ? urp[cr] : ((PK && c >= S) ? urp[c - S] : 0.0);
+  double rpk[PK ? MM : 1], rrow12[PK ? MM : 1], dgc[PK ? MM : 1];
+  if constexpr (PK) {
+    const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+    const int cs = c >= S ? c - S : 0;
+#pragma unroll
+    for (int r = 0; r < MM; ++r) {
+      rpk[r] = c >= S ? Rp[r * MM + cs] : 0.0;     // lanes 12..15: row r of R
+      rrow12[r] = c >= S ? Rp[cs * MM + r] : 0.0;  // lanes 12..15: column r of R
+      // the offset-form diagonal of Quu_reg + eps I (chol_solve's first try)
+      dgc[r] = (c == S + r) ? lam1 + (1e-9 - 1.0) : 0.0;
+    }
+  }
   const bool wrap_c = (c < S) && ((a.wrap_mask >> c) & 1u);
 
   unsigned st = 0;
@@ -557,6 +624,10 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   const unsigned voV0 = pofs * (unsigned)pV0;
   const unsigned twa = (unsigned)(uintptr_t)tile + 8u * c;         // (i, c): + 136 i
   const unsigned tra = (unsigned)(uintptr_t)tile + 8u * kLdsRow * c;  // (c, i): + 8 i
+  // PK: the packed 4 x 4 block's transpose through tile rows 12..15 (lds_sym_packed4)
+  const unsigned tbase = (unsigned)(uintptr_t)tile;
+  const unsigned tw2 = c < S ? twa : tbase + 136u * c;
+  const unsigned tr2 = c < S ? twa : tbase + 136u * S + 8u * (c - S);
   constexpr unsigned OOB = 0x80000000u;
 
   // Deferred symmetrisation: step i parks its value update Vn in the tile and
@@ -607,7 +678,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     const bool act = alive && (i < L);
     double e = c < S ? xi - xg_c : 0.0;
     if (wrap_c) e = wrap_angle(e);
-    const double du = c < MM ? ui - ur_c : 0.0;
+    const double du = (c < MM || (PK && c >= S)) ? ui - ur_c : 0.0;
     // the brute-force curve (solver.py:326-356) checks nothing itself: only its
     // chol_solve raises, so a non-finite e at t = 0 only feeds V_0 (inf/NaN in J)
     const bool e_ok = (JC && i == 0) || finite_val(e);
@@ -617,16 +688,21 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     // lx = Q e, lu = R du (lanes < n / < m)
     double lx = 0.0, lu = 0.0;
     LaneDot<S>::fma(lx, e, qrow);
-    LaneDot<MM>::fma(lu, du, rrow);
+    if constexpr (PK) LaneDotOff<MM, S>::fma(lu, du, rrow12);  // R du on lanes 12..15
+    else LaneDot<MM>::fma(lu, du, rrow);
     double l0 = 0.0;
-    if constexpr (MODE == 1)
-      l0 = 0.5 * lane_sum<S>(e * lx) + 0.5 * lane_sum<MM>(du * lu) +
-           a.w_stage;
+    if constexpr (MODE == 1) {
+      if constexpr (PK)
+        l0 = 0.5 * lane_sum<S>(e * lx) + 0.5 * lane_sum_off<MM, S>(du * lu) + a.w_stage;
+      else
+        l0 = 0.5 * lane_sum<S>(e * lx) + 0.5 * lane_sum<MM>(du * lu) + a.w_stage;
+    }
     // Q-function: qab = [A|B]^T Vx; VA = V [A|B]; [A|B]^T V [A|B]
     double qab = 0.0;
     LaneDot<S>::fma(qab, vx, ab);
-    const double qx = lx + qab;                          // Qx = lx + A^T Vx (lanes < n)
-    const double qu = lu + ror_row<kRowLanes - S>(qab);  // Qu = lu + B^T Vx (lanes < m)
+    const double qx = lx + qab;  // Qx = lx + A^T Vx (lanes < n)
+    // Qu = lu + B^T Vx: lanes < m, or (PK) lanes 12..15 where B^T Vx already is
+    const double qu = PK ? lu + qab : lu + ror_row<kRowLanes - S>(qab);
     stamp(3);
     // products as one dependent DPP chain per output row (accumulator forwarded)
     double VA[S];
@@ -634,126 +710,246 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     static_for<S>([&](auto I) { LaneDot<S>::fma(VA[I], V[I], ab); });  // V [A|B]
     stamp(4);
     // Q + A^T V A is accumulated into Qxx under the Quu^-1 sweep below
-    double QB[MM];
-    zero(QB);
-    static_for<MM>([&](auto R) {  // B^T V [A|B]
-      ColChain<S>::template fmaq<S + R>(QB[R], ab, VA);
-    });
-    double Qux[MM], Quu[MM];
-#pragma unroll
-    for (int r = 0; r < MM; ++r) {
-      Qux[r] = QB[r];                                    // B^T V A   (lanes < n)
-      Quu[r] = rcol[r] + ror_row<kRowLanes - S>(QB[r]);  // R + B^T V B (lanes < m)
-    }
-    // regularised solve
-    stamp(5);
-    double QuuT[MM];
-    lds_transpose<MM>(Quu, QuuT, twa, tra);
-    stamp(6);
-    // First attempt as one offset-form asm sweep (SweepQ, the hot LFT kernel's
-    // block): the diagonal carries (value - 1), the sweep returns -(M+eps I)^-1 + I
-    // and its minimum pivot -- chol_solve's first try (eps = 1e-9; mode 1 at
-    // lam = max(lm, 1e-12)).  Mode 0's jitter-free cholesky(Quu_reg) check
-    // (solver.py:211-219) follows from the same sweep whenever
-    // trace((M + eps I)^-1) < 1e6: then lambda_min(M) > 1e-6 - eps > 0.  Rows
-    // outside that bound get the exact check (a second sweep without jitter), rows
-    // whose first try fails the generic jitter / lambda ladders (hop_device.hpp);
-    // both rare, wave-uniform branches.
-    double Qi[MM], Qs[MM];
-    bool solved;
-    {
-      const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
-      double rj[MM];
-#pragma unroll
-      for (int r = 0; r < MM; ++r) {
-        Qs[r] = 0.5 * (Quu[r] + QuuT[r]);
-        rj[r] = Qs[r] + ((c == r) ? lam1 + (1e-9 - 1.0) : 0.0);
-      }
-      double dj = 1.0;
-      // the sweep fused with Qxx = Q + A^T V A (lanes < n; A^T V B on lanes n..):
-      // the 144 chain FMAs fill the pivots' rcp / Newton latency
-      SweepQColChain<MM, S>::run(rj, dj, Qxx, ab, VA);
-      const bool okj = (dj > 0.0) && (bcast<0>(rj[0]) == bcast<0>(rj[0]));
-#pragma unroll
-      for (int r = 0; r < MM; ++r) Qi[r] = ((c == r) ? 1.0 : 0.0) - rj[r];  // +(M+eps I)^-1
-      bool ok0 = true;
-      if constexpr (MODE == 0) {
-        const double tr = diag_sum4(Qi);  // trace((M + eps I)^-1)
-        const bool sure = okj && (tr < 1e6);
-        if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
-          double rc[MM];
-#pragma unroll
-          for (int r = 0; r < MM; ++r) rc[r] = Qs[r] + ((c == r) ? lam1 - 1.0 : 0.0);
-          double dc = 1.0;
-          SweepQ<MM>::run(rc, dc);
-          const bool okc = (dc > 0.0) && (bcast<0>(rc[0]) == bcast<0>(rc[0]));
-          ok0 = sure || okc;
-        }
-      }
-      solved = okj && ok0;
-      if (__any(!okj && ok0 && act)) {  // the jitter / lambda ladders for the rows that need them
-        const bool ladder = !okj && ok0;
-        if constexpr (MODE == 0) {
-          double Ql[MM];
-#pragma unroll
-          for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam0 : 0.0);
-          bool okc = true;
-          const bool good = spd_inverse_nofallback_chk(Ql, tile, c, 8, st, okc) && okc;
-#pragma unroll
-          for (int r = 0; r < MM; ++r) Qi[r] = ladder ? Ql[r] : Qi[r];
-          solved = ladder ? good : solved;
-        } else {
-          double lam = lam1;
-          int tries = 0;
-          bool okr = false;
-          double Ql[MM];
-#pragma unroll 1
-          while (true) {
-#pragma unroll
-            for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam : 0.0);
-            okr = spd_inverse_nofallback(Ql, tile, c, 8, st);
-            ++tries;
-            const bool done = okr || tries >= a.reg_max_tries;
-            if (!__any(!done && act && ladder)) break;
-            if (!done) lam *= 10.0;
-          }
-#pragma unroll
-          for (int r = 0; r < MM; ++r) Qi[r] = ladder ? Ql[r] : Qi[r];
-          solved = ladder ? okr : solved;
-        }
-      }
-    }
-    const bool fail_row = act && (bad || !solved);
-    stamp(7);
-    // gains
-    double K[MM];
-    zero(K);
-    static_for<MM>([&](auto R) { LaneDot<MM>::fma_neg(K[R], Qi[R], Qux); });  // -Quu_reg^-1 Qux
-    double kv = 0.0;
-    LaneDot<MM>::fma_neg(kv, qu, Qi);          // k = -Quu_reg^-1 Qu  (lanes < m)
-    stamp(8);
-    // value update
+    double Uq[MM];  // Qux rows (lanes < n): P under PK
+    double Kq[MM];  // K rows (lanes < n); under PK -K (the sweep's lanes 0..11)
+    double kvq;     // k (lanes < m; under PK lanes 12..15)
+    bool fail_row;
     double(&Vn)[S] = Qxx;  // the value update accumulates into Qxx in place
     double vxn = qx, v0n = v0;
-    if constexpr (MODE == 0) {
-      LaneDot<MM>::fma(vxn, qu, K);    // + K^T Qu
-      LaneDot<MM>::fma(vxn, kv, Qux);  // + Qux^T k
-      double qk = 0.0;
-      LaneDot<MM>::fma(qk, kv, QuuT);  // (Quu k)[c]
-      LaneDot<MM>::fma(vxn, qk, K);    // + K^T Quu k
-      double QK[MM];
-      copy(QK, Qux);
-      static_for<MM>([&](auto R) { LaneDot<MM>::fma(QK[R], Quu[R], K); });  // Qux + Quu K
-      static_for<S>([&](auto R) {
-        ColChain<MM>::template fmaq<R>(Vn[R], K, QK);    // + K^T (Qux + Quu K)
-        ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);   // + Qux^T K
-      });
+    if constexpr (PK) {
+      // P[R] = R row R (lanes 12..15) + B^T V [A|B] row R: [Qux | Quu] on one register
+      double P[MM], PT[MM];
+#pragma unroll
+      for (int r = 0; r < MM; ++r) P[r] = rpk[r];
+      static_for<MM>([&](auto R) { ColChain<S>::template fmaq<S + R>(P[R], ab, VA); });
+      stamp(5);
+      lds_sym_packed4(P, PT, twa, tw2, tr2);  // lanes 12..15 of PT: Quu^T; lanes < 12: Qux
+      stamp(6);
+      bool solved;
+      double rj[MM];
+      {
+        // lanes < 12 stay Qux exactly (0.5 (Qux + Qux)); lanes 12..15: _sym(Quu) + the
+        // offset-form lam + eps diagonal
+#pragma unroll
+        for (int r = 0; r < MM; ++r) rj[r] = __builtin_fma(0.5, P[r] + PT[r], dgc[r]);
+        double dj = 1.0;
+        SweepQColChainOff<MM, S, S>::run(rj, dj, Qxx, ab, VA);
+        const bool okj = (dj > 0.0) && (bcast<S>(rj[0]) == bcast<S>(rj[0]));
+        const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+        bool ok0 = true;
+        if constexpr (MODE == 0) {
+          const double tr = 4.0 - diag_sum4_off12(rj);  // trace((M + eps I)^-1)
+          const bool sure = okj && (tr < 1e6);
+          if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
+            double rc[MM];
+#pragma unroll
+            for (int r = 0; r < MM; ++r)
+              rc[r] = ror_row<kRowLanes - S>(0.5 * (P[r] + PT[r])) + ((c == r) ? lam1 - 1.0 : 0.0);
+            double dc = 1.0;
+            SweepQ<MM>::run(rc, dc);
+            const bool okc = (dc > 0.0) && (bcast<0>(rc[0]) == bcast<0>(rc[0]));
+            ok0 = sure || okc;
+          }
+        }
+        solved = okj && ok0;
+        if (__any(!okj && ok0 && act)) {  // the jitter / lambda ladders (rare), on lanes 0..3
+          const bool ladder = !okj && ok0;
+          double Qs[MM], Ql[MM];
+#pragma unroll
+          for (int r = 0; r < MM; ++r) Qs[r] = ror_row<kRowLanes - S>(0.5 * (P[r] + PT[r]));
+          bool good;
+          if constexpr (MODE == 0) {
+#pragma unroll
+            for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam0 : 0.0);
+            bool okc = true;
+            good = spd_inverse_nofallback_chk(Ql, tile, c, 8, st, okc) && okc;
+          } else {
+            double lam = lam1;
+            int tries = 0;
+#pragma unroll 1
+            while (true) {
+#pragma unroll
+              for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam : 0.0);
+              good = spd_inverse_nofallback(Ql, tile, c, 8, st);
+              ++tries;
+              const bool done = good || tries >= a.reg_max_tries;
+              if (!__any(!done && act && ladder)) break;
+              if (!done) lam *= 10.0;
+            }
+          }
+          // back to the packed form: lanes 0..11 Ql Qux, lanes 12..15 I - Ql
+#pragma unroll
+          for (int r = 0; r < MM; ++r) {
+            double y = 0.0;
+            LaneDot<MM>::fma(y, Ql[r], P);
+            const double il = ror_row<S>(Ql[r]);
+            const double rl = c < S ? y : (((c == S + r) ? 1.0 : 0.0) - il);
+            rj[r] = ladder ? rl : rj[r];
+          }
+          solved = ladder ? good : solved;
+        }
+      }
+      fail_row = act && (bad || !solved);
+      stamp(7);
+      // gains: K = -rj (lanes < 12); k = -(M + eps I)^-1 Qu on lanes 12..15 from the
+      // offset form: -Qu + sum_j Qu_j rj[j]
+      double kv = -qu;
+      LaneDotOff<MM, S>::fma(kv, qu, rj);
+      stamp(8);
+      if constexpr (MODE == 0) {
+        LaneDotOff<MM, S>::fma_neg(vxn, qu, rj);  // + K^T Qu
+        LaneDotOff<MM, S>::fma(vxn, kv, P);       // + Qux^T k
+        double qk = 0.0;
+        LaneDotOff<MM, S>::fma(qk, kv, PT);       // (Quu k) on lanes 12..15
+        LaneDotOff<MM, S>::fma_neg(vxn, qk, rj);  // + K^T Quu k
+        double QK[MM];
+        copy(QK, P);
+        static_for<MM>([&](auto R) { LaneDotOff<MM, S>::fma_neg(QK[R], P[R], rj); });  // Qux + Quu K
+        static_for<S>([&](auto R) {
+          ColChain<MM>::template fma_negq<R>(Vn[R], rj, QK);  // + K^T (Qux + Quu K)
+          ColChain<MM>::template fma_negq<R>(Vn[R], P, rj);   // + Qux^T K
+        });
+      } else {
+        static_for<S>([&](auto R) {  // Qxx - Qux^T Quu^-1 Qux
+          ColChain<MM>::template fma_negq<R>(Vn[R], P, rj);
+        });
+        LaneDotOff<MM, S>::fma(vxn, kv, P);  // Qx - Qux^T Quu^-1 Qu
+        v0n = l0 + v0 + 0.5 * lane_sum_off<MM, S>(qu * kv);
+      }
+#pragma unroll
+      for (int r = 0; r < MM; ++r) {
+        Uq[r] = P[r];
+        Kq[r] = rj[r];
+      }
+      kvq = kv;
     } else {
-      static_for<S>([&](auto R) {  // Qxx - Qux^T Quu^-1 Qux
-        ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);
+      // Q + A^T V A is accumulated into Qxx under the Quu^-1 sweep below
+      double QB[MM];
+      zero(QB);
+      static_for<MM>([&](auto R) {  // B^T V [A|B]
+        ColChain<S>::template fmaq<S + R>(QB[R], ab, VA);
       });
-      LaneDot<MM>::fma(vxn, kv, Qux);             // Qx - Qux^T Quu^-1 Qu
-      v0n = l0 + v0 + 0.5 * lane_sum<MM>(qu * kv);
+      double Qux[MM], Quu[MM];
+#pragma unroll
+      for (int r = 0; r < MM; ++r) {
+        Qux[r] = QB[r];                                    // B^T V A   (lanes < n)
+        Quu[r] = rcol[r] + ror_row<kRowLanes - S>(QB[r]);  // R + B^T V B (lanes < m)
+      }
+      // regularised solve
+      stamp(5);
+      double QuuT[MM];
+      lds_transpose<MM>(Quu, QuuT, twa, tra);
+      stamp(6);
+      // First attempt as one offset-form asm sweep (SweepQ, the hot LFT kernel's
+      // block): the diagonal carries (value - 1), the sweep returns -(M+eps I)^-1 + I
+      // and its minimum pivot -- chol_solve's first try (eps = 1e-9; mode 1 at
+      // lam = max(lm, 1e-12)).  Mode 0's jitter-free cholesky(Quu_reg) check
+      // (solver.py:211-219) follows from the same sweep whenever
+      // trace((M + eps I)^-1) < 1e6: then lambda_min(M) > 1e-6 - eps > 0.  Rows
+      // outside that bound get the exact check (a second sweep without jitter), rows
+      // whose first try fails the generic jitter / lambda ladders (hop_device.hpp);
+      // both rare, wave-uniform branches.
+      double Qi[MM], Qs[MM];
+      bool solved;
+      {
+        const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+        double rj[MM];
+#pragma unroll
+        for (int r = 0; r < MM; ++r) {
+          Qs[r] = 0.5 * (Quu[r] + QuuT[r]);
+          rj[r] = Qs[r] + ((c == r) ? lam1 + (1e-9 - 1.0) : 0.0);
+        }
+        double dj = 1.0;
+        // the sweep fused with Qxx = Q + A^T V A (lanes < n; A^T V B on lanes n..):
+        // the 144 chain FMAs fill the pivots' rcp / Newton latency
+        SweepQColChain<MM, S>::run(rj, dj, Qxx, ab, VA);
+        const bool okj = (dj > 0.0) && (bcast<0>(rj[0]) == bcast<0>(rj[0]));
+#pragma unroll
+        for (int r = 0; r < MM; ++r) Qi[r] = ((c == r) ? 1.0 : 0.0) - rj[r];  // +(M+eps I)^-1
+        bool ok0 = true;
+        if constexpr (MODE == 0) {
+          const double tr = diag_sum4(Qi);  // trace((M + eps I)^-1)
+          const bool sure = okj && (tr < 1e6);
+          if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
+            double rc[MM];
+#pragma unroll
+            for (int r = 0; r < MM; ++r) rc[r] = Qs[r] + ((c == r) ? lam1 - 1.0 : 0.0);
+            double dc = 1.0;
+            SweepQ<MM>::run(rc, dc);
+            const bool okc = (dc > 0.0) && (bcast<0>(rc[0]) == bcast<0>(rc[0]));
+            ok0 = sure || okc;
+          }
+        }
+        solved = okj && ok0;
+        if (__any(!okj && ok0 && act)) {  // the jitter / lambda ladders for the rows that need them
+          const bool ladder = !okj && ok0;
+          if constexpr (MODE == 0) {
+            double Ql[MM];
+#pragma unroll
+            for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam0 : 0.0);
+            bool okc = true;
+            const bool good = spd_inverse_nofallback_chk(Ql, tile, c, 8, st, okc) && okc;
+#pragma unroll
+            for (int r = 0; r < MM; ++r) Qi[r] = ladder ? Ql[r] : Qi[r];
+            solved = ladder ? good : solved;
+          } else {
+            double lam = lam1;
+            int tries = 0;
+            bool okr = false;
+            double Ql[MM];
+#pragma unroll 1
+            while (true) {
+#pragma unroll
+              for (int r = 0; r < MM; ++r) Ql[r] = Qs[r] + ((c == r) ? lam : 0.0);
+              okr = spd_inverse_nofallback(Ql, tile, c, 8, st);
+              ++tries;
+              const bool done = okr || tries >= a.reg_max_tries;
+              if (!__any(!done && act && ladder)) break;
+              if (!done) lam *= 10.0;
+            }
+#pragma unroll
+            for (int r = 0; r < MM; ++r) Qi[r] = ladder ? Ql[r] : Qi[r];
+            solved = ladder ? okr : solved;
+          }
+        }
+      }
+      fail_row = act && (bad || !solved);
+      stamp(7);
+      // gains
+      double K[MM];
+      zero(K);
+      static_for<MM>([&](auto R) { LaneDot<MM>::fma_neg(K[R], Qi[R], Qux); });  // -Quu_reg^-1 Qux
+      double kv = 0.0;
+      LaneDot<MM>::fma_neg(kv, qu, Qi);          // k = -Quu_reg^-1 Qu  (lanes < m)
+      stamp(8);
+      // value update
+      if constexpr (MODE == 0) {
+        LaneDot<MM>::fma(vxn, qu, K);    // + K^T Qu
+        LaneDot<MM>::fma(vxn, kv, Qux);  // + Qux^T k
+        double qk = 0.0;
+        LaneDot<MM>::fma(qk, kv, QuuT);  // (Quu k)[c]
+        LaneDot<MM>::fma(vxn, qk, K);    // + K^T Quu k
+        double QK[MM];
+        copy(QK, Qux);
+        static_for<MM>([&](auto R) { LaneDot<MM>::fma(QK[R], Quu[R], K); });  // Qux + Quu K
+        static_for<S>([&](auto R) {
+          ColChain<MM>::template fmaq<R>(Vn[R], K, QK);    // + K^T (Qux + Quu K)
+          ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);   // + Qux^T K
+        });
+      } else {
+        static_for<S>([&](auto R) {  // Qxx - Qux^T Quu^-1 Qux
+          ColChain<MM>::template fmaq<R>(Vn[R], Qux, K);
+        });
+        LaneDot<MM>::fma(vxn, kv, Qux);             // Qx - Qux^T Quu^-1 Qu
+        v0n = l0 + v0 + 0.5 * lane_sum<MM>(qu * kv);
+      }
+
+#pragma unroll
+      for (int r = 0; r < MM; ++r) {
+        Uq[r] = Qux[r];
+        Kq[r] = K[r];
+      }
+      kvq = kv;
     }
     stamp(9);
     lds_park12(Vn, twa);  // its transpose is read with the next step's image
@@ -768,7 +964,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     if (JC && i == 0) {
       z = 0.0;
 #pragma unroll
-      for (int r = 0; r < MM; ++r) z = __builtin_fma(Qux[r], 0.0, z);
+      for (int r = 0; r < MM; ++r) z = __builtin_fma(Uq[r], 0.0, z);
     }
     const unsigned long long vbm = __ballot(!(z == z) && c < S);
     const bool vfail = act && (((vbm >> (16 * g)) & 0xffffull) != 0ull);
@@ -797,8 +993,8 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
       const bool wr = commit && c < S;
       const unsigned so = (unsigned)i * (MM * S * 8), vo = wr ? voK : OOB;
 #pragma unroll
-      for (int r = 0; r < MM; ++r) st64(K[r], rK, vo + 8u * S * r, so);
-      st64(kv, rk, (commit && c < MM) ? vok : OOB, (unsigned)i * (MM * 8));
+      for (int r = 0; r < MM; ++r) st64(PK ? -Kq[r] : Kq[r], rK, vo + 8u * S * r, so);
+      st64(kvq, rk, (commit && (PK ? c >= S : c < MM)) ? vok : OOB, (unsigned)i * (MM * 8));
       if constexpr (WANTV) {
         st64(vxn, rVx, wr ? voVx : OOB, (unsigned)i * (S * 8));
         st64(v0n, rV0, (commit && c == 0) ? voV0 : OOB, (unsigned)i * 8);
@@ -850,9 +1046,9 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   }
 }
 
-template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0>
+template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool PK = true>
 __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
-  ric_body<MODE, WANTV, STAMP, EXP, false>(a, (long long)blockIdx.x, 0);
+  ric_body<MODE, WANTV, STAMP, EXP, false, PK>(a, (long long)blockIdx.x, 0);
 }
 
 // The J-curve form: workgroups [b * P, (b+1) * P), P = ceil(jc_tmax / 2), run problem
@@ -865,7 +1061,7 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
 // L2s and each re-reads the block's A, B, x, u from HBM.  The remap gives the ids an
 // XCD receives (w = x, x + 8, x + 16, ...) consecutive logical ids, so a block's
 // horizons share one L2.
-template <bool XCD>
+template <bool XCD, bool PK = true>
 __global__ __launch_bounds__(256, 1) void riccati_fast_jcurve_kernel(RiccatiArgs<double> a) {
   const unsigned P = (unsigned)((a.jc_tmax + 1) / 2);
   unsigned w = blockIdx.x;
@@ -875,8 +1071,8 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_jcurve_kernel(RiccatiArgs
   }
   const int h = (int)(w % P);
   const long long blk = (long long)(w / P);
-  ric_body<1, false, false, 0, true>(a, blk, a.jc_tmax - h);
-  if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true>(a, blk, h + 1);
+  ric_body<1, false, false, 0, true, PK>(a, blk, a.jc_tmax - h);
+  if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true, PK>(a, blk, h + 1);
 }
 
 template <int MODE, bool WANTV>
@@ -896,6 +1092,11 @@ hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
     else
       hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 2>), dim3((unsigned)blocks),
                          dim3(256), lds, stream, a);
+    return hipGetLastError();
+  }
+  if (g_opt_variant == 84) {  // separate Qux / Quu rows (the round-3 schedule, A/B)
+    hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 0, false>), dim3((unsigned)blocks),
+                       dim3(256), lds, stream, a);
     return hipGetLastError();
   }
 #endif
@@ -923,6 +1124,11 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
 #ifdef HOP_DEV
     if (g_opt_variant == 83) {  // XCD-grouped horizons (A/B)
       hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel<true>, grid, dim3(256), lds, stream, a);
+      return hipGetLastError();
+    }
+    if (g_opt_variant == 84) {  // separate Qux / Quu rows (A/B)
+      hipLaunchKernelGGL((ricf::riccati_fast_jcurve_kernel<false, false>), grid, dim3(256), lds,
+                         stream, a);
       return hipGetLastError();
     }
 #endif
