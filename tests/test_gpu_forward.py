@@ -424,6 +424,37 @@ def test_bruteforce_jcurve_equals_per_horizon_riccati(dev, sid, N, T_max):
     assert (st[4, 6:] & _lib.ST_NONFINITE).all() and not (st[4, :6] & _lib.ST_FAIL).any()
 
 
+def test_bruteforce_jcurve_shared_q_two_wave_kernel_bitwise(dev):
+    """a batch-shared Q runs the J curve at two waves per SIMD (one step image, one Q
+    image per wave, Q's rows re-read from LDS); a per-problem Q (the same matrix
+    repeated) the one-wave layout: bit-identical curves and status.  Quadrotor sizes
+    (the exact-size kernel), ragged B = 37, odd T_max, a NaN state, and a
+    non-symmetric Q so lx = Q e and the Qxx start (Q's rows vs columns) are told apart"""
+    import torch
+    from time_opt_ilqr_amd import engine
+    n, m = dyn.DIMS[2]
+    rng = np.random.default_rng(29)
+    Bn, N, T_max = 37, 40, 31
+    X = rng.standard_normal((Bn, N + 1, n)) * 0.3
+    U = rng.standard_normal((Bn, N, m)) * 0.1
+    lin = engine.linearize(2, _t(X, dev), _t(U, dev), 0.05, central=False)
+    X[5, 9, 3] = np.nan
+    Xd, Ud = _t(X, dev), _t(U, dev)
+    xg, ur = _t(rng.standard_normal(n) * 0.2, dev), _t(rng.standard_normal(m) * 0.1, dev)
+    Qn = np.diag(rng.uniform(0.5, 2, n)) + 0.05 * rng.standard_normal((n, n))
+    Q = _t(Qn, dev)
+    R = _t(np.diag(rng.uniform(0.5, 2, m)), dev)
+    Qf = _t(np.diag(rng.uniform(2, 10, n)), dev)
+    kw = dict(lm_lambda=1e-6, w_stage=0.4)
+    J1, s1 = engine.bruteforce_jcurve(lin.A, lin.B, Xd, Ud, xg, ur, Q, R, Qf, T_max, **kw)
+    Qb = Q.unsqueeze(0).repeat(Bn, 1, 1).contiguous()
+    J2, s2 = engine.bruteforce_jcurve(lin.A, lin.B, Xd, Ud, xg, ur, Qb, R, Qf, T_max, **kw)
+    assert torch.equal(s1, s2)
+    assert torch.equal(J1.nan_to_num(7.0), J2.nan_to_num(7.0))
+    # horizon T reads X[0..T]: T >= 9 (column 8 on) sees the NaN
+    assert torch.isnan(J1[5, 8:]).all() and torch.isfinite(J1[5, :8]).all()
+
+
 def test_bruteforce_jcurve_oracle_and_limits(dev):
     """against the oracle's bruteforce_J on a DI problem, and the entry's checks"""
     from time_opt_ilqr_amd import _lib, engine

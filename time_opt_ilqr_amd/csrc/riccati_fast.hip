@@ -37,6 +37,13 @@ constexpr int OFF_T = 2 * BUF;              // transpose tiles
 constexpr int OFF_Q = OFF_T + kProbPerWave * kLdsTile * 8;  // Q rows: problem g, row r, lane c
 constexpr int Q_PROB = NX * 16 * 8;                         // at OFF_Q + 1536 g + 128 r + 8 c
 constexpr int WAVE_BYTES = OFF_Q + kProbPerWave * Q_PROB;
+// the two-waves-per-SIMD J-curve layout (OCC2): ONE step image (its DMA is issued
+// after the step's reads, still one step ahead), the tiles, and one Q image shared by
+// the wave's problems (a batch-shared Q): 19,456 B, so two 4-wave workgroups fit a CU
+constexpr int OFF_T2 = BUF;
+constexpr int OFF_Q2 = OFF_T2 + kProbPerWave * kLdsTile * 8;
+constexpr int WAVE_BYTES2 = OFF_Q2 + Q_PROB;
+static_assert(2 * kWavesPerBlock * WAVE_BYTES2 <= 160 * 1024, "OCC2 needs two workgroups per CU");
 
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
@@ -262,6 +269,113 @@ __device__ __forceinline__ void read_step_vt_q(const unsigned (&ad)[NX], unsigne
       : "memory");
 }
 
+// OCC2: ... and Q's rows for lx = Q e (row c on lane c at qra + 8 i), re-read each step
+// instead of held in 24 VGPRs
+template <int IMG>
+__device__ __forceinline__ void read_step_q_qr(const unsigned (&ad)[NX], unsigned xa, unsigned ua, unsigned qa, unsigned qra, double (&ab)[NX], double& x, double& u, double (&q)[NX], double (&qr)[NX]) {
+  asm volatile(
+      "ds_read_b64 %0, %38 offset:%c54\n\t"
+      "ds_read_b64 %1, %39 offset:%c54\n\t"
+      "ds_read_b64 %2, %40 offset:%c54\n\t"
+      "ds_read_b64 %3, %41 offset:%c54\n\t"
+      "ds_read_b64 %4, %42 offset:%c54\n\t"
+      "ds_read_b64 %5, %43 offset:%c54\n\t"
+      "ds_read_b64 %6, %44 offset:%c54\n\t"
+      "ds_read_b64 %7, %45 offset:%c54\n\t"
+      "ds_read_b64 %8, %46 offset:%c54\n\t"
+      "ds_read_b64 %9, %47 offset:%c54\n\t"
+      "ds_read_b64 %10, %48 offset:%c54\n\t"
+      "ds_read_b64 %11, %49 offset:%c54\n\t"
+      "ds_read_b64 %12, %50 offset:%c54\n\t"
+      "ds_read_b64 %13, %51 offset:%c54\n\t"
+      "ds_read_b64 %14, %52 offset:0\n\t"
+      "ds_read_b64 %15, %52 offset:128\n\t"
+      "ds_read_b64 %16, %52 offset:256\n\t"
+      "ds_read_b64 %17, %52 offset:384\n\t"
+      "ds_read_b64 %18, %52 offset:512\n\t"
+      "ds_read_b64 %19, %52 offset:640\n\t"
+      "ds_read_b64 %20, %52 offset:768\n\t"
+      "ds_read_b64 %21, %52 offset:896\n\t"
+      "ds_read_b64 %22, %52 offset:1024\n\t"
+      "ds_read_b64 %23, %52 offset:1152\n\t"
+      "ds_read_b64 %24, %52 offset:1280\n\t"
+      "ds_read_b64 %25, %52 offset:1408\n\t"
+      "ds_read_b64 %26, %53 offset:0\n\t"
+      "ds_read_b64 %27, %53 offset:8\n\t"
+      "ds_read_b64 %28, %53 offset:16\n\t"
+      "ds_read_b64 %29, %53 offset:24\n\t"
+      "ds_read_b64 %30, %53 offset:32\n\t"
+      "ds_read_b64 %31, %53 offset:40\n\t"
+      "ds_read_b64 %32, %53 offset:48\n\t"
+      "ds_read_b64 %33, %53 offset:56\n\t"
+      "ds_read_b64 %34, %53 offset:64\n\t"
+      "ds_read_b64 %35, %53 offset:72\n\t"
+      "ds_read_b64 %36, %53 offset:80\n\t"
+      "ds_read_b64 %37, %53 offset:88\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]), "=&v"(ab[7]), "=&v"(ab[8]), "=&v"(ab[9]), "=&v"(ab[10]), "=&v"(ab[11]), "=&v"(x), "=&v"(u), "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11]), "=&v"(qr[0]), "=&v"(qr[1]), "=&v"(qr[2]), "=&v"(qr[3]), "=&v"(qr[4]), "=&v"(qr[5]), "=&v"(qr[6]), "=&v"(qr[7]), "=&v"(qr[8]), "=&v"(qr[9]), "=&v"(qr[10]), "=&v"(qr[11])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(xa), "v"(ua), "v"(qa), "v"(qra), "i"(IMG)
+      : "memory");
+}
+template <int IMG>
+__device__ __forceinline__ void read_step_vt_q_qr(const unsigned (&ad)[NX], unsigned xa, unsigned ua, unsigned ra, unsigned qa, unsigned qra, double (&ab)[NX], double& x, double& u, double (&t)[NX], double (&q)[NX], double (&qr)[NX]) {
+  asm volatile(
+      "ds_read_b64 %0, %50 offset:%c67\n\t"
+      "ds_read_b64 %1, %51 offset:%c67\n\t"
+      "ds_read_b64 %2, %52 offset:%c67\n\t"
+      "ds_read_b64 %3, %53 offset:%c67\n\t"
+      "ds_read_b64 %4, %54 offset:%c67\n\t"
+      "ds_read_b64 %5, %55 offset:%c67\n\t"
+      "ds_read_b64 %6, %56 offset:%c67\n\t"
+      "ds_read_b64 %7, %57 offset:%c67\n\t"
+      "ds_read_b64 %8, %58 offset:%c67\n\t"
+      "ds_read_b64 %9, %59 offset:%c67\n\t"
+      "ds_read_b64 %10, %60 offset:%c67\n\t"
+      "ds_read_b64 %11, %61 offset:%c67\n\t"
+      "ds_read_b64 %12, %62 offset:%c67\n\t"
+      "ds_read_b64 %13, %63 offset:%c67\n\t"
+      "ds_read_b64 %14, %64 offset:0\n\t"
+      "ds_read_b64 %15, %64 offset:8\n\t"
+      "ds_read_b64 %16, %64 offset:16\n\t"
+      "ds_read_b64 %17, %64 offset:24\n\t"
+      "ds_read_b64 %18, %64 offset:32\n\t"
+      "ds_read_b64 %19, %64 offset:40\n\t"
+      "ds_read_b64 %20, %64 offset:48\n\t"
+      "ds_read_b64 %21, %64 offset:56\n\t"
+      "ds_read_b64 %22, %64 offset:64\n\t"
+      "ds_read_b64 %23, %64 offset:72\n\t"
+      "ds_read_b64 %24, %64 offset:80\n\t"
+      "ds_read_b64 %25, %64 offset:88\n\t"
+      "ds_read_b64 %26, %65 offset:0\n\t"
+      "ds_read_b64 %27, %65 offset:128\n\t"
+      "ds_read_b64 %28, %65 offset:256\n\t"
+      "ds_read_b64 %29, %65 offset:384\n\t"
+      "ds_read_b64 %30, %65 offset:512\n\t"
+      "ds_read_b64 %31, %65 offset:640\n\t"
+      "ds_read_b64 %32, %65 offset:768\n\t"
+      "ds_read_b64 %33, %65 offset:896\n\t"
+      "ds_read_b64 %34, %65 offset:1024\n\t"
+      "ds_read_b64 %35, %65 offset:1152\n\t"
+      "ds_read_b64 %36, %65 offset:1280\n\t"
+      "ds_read_b64 %37, %65 offset:1408\n\t"
+      "ds_read_b64 %38, %66 offset:0\n\t"
+      "ds_read_b64 %39, %66 offset:8\n\t"
+      "ds_read_b64 %40, %66 offset:16\n\t"
+      "ds_read_b64 %41, %66 offset:24\n\t"
+      "ds_read_b64 %42, %66 offset:32\n\t"
+      "ds_read_b64 %43, %66 offset:40\n\t"
+      "ds_read_b64 %44, %66 offset:48\n\t"
+      "ds_read_b64 %45, %66 offset:56\n\t"
+      "ds_read_b64 %46, %66 offset:64\n\t"
+      "ds_read_b64 %47, %66 offset:72\n\t"
+      "ds_read_b64 %48, %66 offset:80\n\t"
+      "ds_read_b64 %49, %66 offset:88\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(ab[0]), "=&v"(ab[1]), "=&v"(ab[2]), "=&v"(ab[3]), "=&v"(ab[4]), "=&v"(ab[5]), "=&v"(ab[6]), "=&v"(ab[7]), "=&v"(ab[8]), "=&v"(ab[9]), "=&v"(ab[10]), "=&v"(ab[11]), "=&v"(x), "=&v"(u), "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3]), "=&v"(t[4]), "=&v"(t[5]), "=&v"(t[6]), "=&v"(t[7]), "=&v"(t[8]), "=&v"(t[9]), "=&v"(t[10]), "=&v"(t[11]), "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7]), "=&v"(q[8]), "=&v"(q[9]), "=&v"(q[10]), "=&v"(q[11]), "=&v"(qr[0]), "=&v"(qr[1]), "=&v"(qr[2]), "=&v"(qr[3]), "=&v"(qr[4]), "=&v"(qr[5]), "=&v"(qr[6]), "=&v"(qr[7]), "=&v"(qr[8]), "=&v"(qr[9]), "=&v"(qr[10]), "=&v"(qr[11])
+      : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(xa), "v"(ua), "v"(ra), "v"(qa), "v"(qra), "i"(IMG)
+      : "memory");
+}
+
 // park x (column c per lane) in the problem's tile: row i at wa + 136 i (no wait:
 // the wave's LDS operations execute in order, the next reads see these writes)
 __device__ __forceinline__ void lds_park12(const double (&x)[NX], unsigned wa) {
@@ -457,7 +571,7 @@ __device__ unsigned long long g_ricf_stamp[16];
 // (Quu_reg + eps I)^-1 Qux = -K on lanes 0..11 directly: no K product, no lane
 // rotations of Quu, no inverse rebuilt from the sweep's offset form; Qu, k and R du
 // live on lanes 12..15 likewise.  PK = false keeps the round-2 form (developer A/B).
-template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC, bool PK = true>
+template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC, bool PK = true, bool OCC2 = false>
 __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long blk, int jl) {
   constexpr int S = NX, MM = MU;
   unsigned long long sec[12] = {};
@@ -475,9 +589,10 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  unsigned char* wbase = smem_raw + w * WAVE_BYTES;
+  static_assert(!OCC2 || JC, "the shared-Q single-image layout is the J curve's");
+  unsigned char* wbase = smem_raw + w * (OCC2 ? WAVE_BYTES2 : WAVE_BYTES);
   const unsigned wlds = (unsigned)(uintptr_t)wbase;
-  double* tile = reinterpret_cast<double*>(wbase + OFF_T) + g * kLdsTile;
+  double* tile = reinterpret_cast<double*>(wbase + (OCC2 ? OFF_T2 : OFF_T)) + g * kLdsTile;
 #pragma unroll 1
   for (int i = c; i < kLdsTile; i += kRowLanes) tile[i] = 0.0;
 
@@ -548,13 +663,16 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   const int cq = c < S ? c : 0, cr = c < MM ? c : 0;
   // Q row r on lane c (the Qxx accumulator start) lives in the wave's Q image and
   // is re-read each step with the step's [A|B]; only Q's rows (for lx) stay in VGPRs
-  double qrow[S], rcol[MM], rrow[MM];
-  const unsigned qa = wlds + OFF_Q + Q_PROB * g + 8 * c;
+  double qrow_r[S], rcol[MM], rrow[MM];
+  // (OCC2: one image for the wave; its 4 problems write the same batch-shared Q; Q's
+  // rows are read from it per step, lanes 12..15 reading row 0: their lx is never used)
+  const unsigned qa = wlds + (OCC2 ? OFF_Q2 : OFF_Q + Q_PROB * g) + 8 * c;
+  const unsigned qra = wlds + OFF_Q2 + 128 * cq;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const double qv = c < S ? Qp[i * S + cq] : 0.0;
     asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(qa), "v"(qv), "i"(128 * i) : "memory");
-    qrow[i] = c < S ? Qp[cq * S + i] : 0.0;
+    if constexpr (!OCC2) qrow_r[i] = c < S ? Qp[cq * S + i] : 0.0;
   }
 #pragma unroll
   for (int i = 0; i < MM; ++i) {
@@ -643,29 +761,38 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   auto step = [&](int i, auto IMGc, auto FIRSTc) {
     constexpr int IMG = decltype(IMGc)::value;
     constexpr bool FIRST = decltype(FIRSTc)::value;
-    constexpr int NEXT = IMG == 0 ? BUF : 0;
+    constexpr int NEXT = OCC2 ? 0 : (IMG == 0 ? BUF : 0);
     // this step's pieces landed; the previous step's NST stores may still be in flight
     stamp(-1);
     if constexpr (FIRST) vm_wait();
     else vm_wait_n<EXP == 1 ? 0 : NST>();
     stamp(0);
-    if (EXP != 2 && i > 0)
-      dma9<NEXT>(va, vb, vx_, vu_, rA, rB, rX, rU, wlds, (unsigned)(i - 1) * (S * S * 8),
-                 (unsigned)(i - 1) * (S * MM * 8), (unsigned)(i - 1) * (S * 8),
-                 (unsigned)(i - 1) * (MM * 8));
+    auto dma_prev = [&]() {
+      if (EXP != 2 && i > 0)
+        dma9<NEXT>(va, vb, vx_, vu_, rA, rB, rX, rU, wlds, (unsigned)(i - 1) * (S * S * 8),
+                   (unsigned)(i - 1) * (S * MM * 8), (unsigned)(i - 1) * (S * 8),
+                   (unsigned)(i - 1) * (MM * 8));
+    };
+    if constexpr (!OCC2) dma_prev();
     stamp(1);
     double ab[S], xi, ui;
     double Qxx[S];  // Q (the accumulator start of Qxx = Q + A^T V A)
+    double qrow[S];  // Q row c (lx = Q e): loop-invariant registers, or (OCC2) LDS
+    if constexpr (!OCC2) copy(qrow, qrow_r);
     if constexpr (FIRST) {
-      read_step_q<IMG>(ad, xa, ua, qa, ab, xi, ui, Qxx);
+      if constexpr (OCC2) read_step_q_qr<IMG>(ad, xa, ua, qa, qra, ab, xi, ui, Qxx, qrow);
+      else read_step_q<IMG>(ad, xa, ua, qa, ab, xi, ui, Qxx);
     } else {
       double t[S];
-      read_step_vt_q<IMG>(ad, xa, ua, tra, qa, ab, xi, ui, t, Qxx);
+      if constexpr (OCC2) read_step_vt_q_qr<IMG>(ad, xa, ua, tra, qa, qra, ab, xi, ui, t, Qxx, qrow);
+      else read_step_vt_q<IMG>(ad, xa, ua, tra, qa, ab, xi, ui, t, Qxx);
       // _sym of step i+1's Vxx; a row that did not commit carried (and parked) its
       // old, exactly symmetric V, for which this is V itself
 #pragma unroll
       for (int r = 0; r < S; ++r) V[r] = 0.5 * (Vp[r] + t[r]);
     }
+    // OCC2: the single image is free once its reads have waited (lgkmcnt(0) above)
+    if constexpr (OCC2) dma_prev();
     // Vxx of step i+1 (mode 1 / requested): NST counts 12 stores here every step
     // (the first step's are out of range) so vm_wait_n stays exact
     if constexpr (WANTV && EXP != 1) {
@@ -1004,7 +1131,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   };
 
   using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, BUF>;
+  using I1 = std::integral_constant<int, OCC2 ? 0 : BUF>;
   if (Lw > 0) {
     const int i0 = Lw - 1;
     dma9<0>(va, vb, vx_, vu_, rA, rB, rX, rU, wlds, (unsigned)i0 * (S * S * 8),
@@ -1061,8 +1188,12 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double
 // L2s and each re-reads the block's A, B, x, u from HBM.  The remap gives the ids an
 // XCD receives (w = x, x + 8, x + 16, ...) consecutive logical ids, so a block's
 // horizons share one L2.
-template <bool XCD, bool PK = true>
-__global__ __launch_bounds__(256, 1) void riccati_fast_jcurve_kernel(RiccatiArgs<double> a) {
+// OCC2 (the default for a batch-shared Q): 247 VGPRs and 19,456 B of LDS per wave
+// (one step image, one Q image, Q's rows re-read from it per step), so two 4-wave
+// workgroups share a CU and each SIMD interleaves two waves' dependent DPP chains:
+// 1.31x the one-wave layout at the bench shape, bit-identical (round 3).
+template <bool XCD, bool PK = true, bool OCC2 = false>
+__global__ __launch_bounds__(256, OCC2 ? 2 : 1) void riccati_fast_jcurve_kernel(RiccatiArgs<double> a) {
   const unsigned P = (unsigned)((a.jc_tmax + 1) / 2);
   unsigned w = blockIdx.x;
   if constexpr (XCD) {
@@ -1071,8 +1202,8 @@ __global__ __launch_bounds__(256, 1) void riccati_fast_jcurve_kernel(RiccatiArgs
   }
   const int h = (int)(w % P);
   const long long blk = (long long)(w / P);
-  ric_body<1, false, false, 0, true, PK>(a, blk, a.jc_tmax - h);
-  if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true, PK>(a, blk, h + 1);
+  ric_body<1, false, false, 0, true, PK, OCC2>(a, blk, a.jc_tmax - h);
+  if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true, PK, OCC2>(a, blk, h + 1);
 }
 
 template <int MODE, bool WANTV>
@@ -1131,7 +1262,16 @@ hipError_t dispatch_riccati_fast(const RiccatiArgs<double>& a, hipStream_t strea
                          stream, a);
       return hipGetLastError();
     }
+    if (g_opt_variant == 86) {  // one wave per SIMD with a batch-shared Q (A/B)
+      hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel<false>, grid, dim3(256), lds, stream, a);
+      return hipGetLastError();
+    }
 #endif
+    if (a.q_bstride == 0) {  // a batch-shared Q: two waves per SIMD (OCC2)
+      hipLaunchKernelGGL((ricf::riccati_fast_jcurve_kernel<false, true, true>), grid, dim3(256),
+                         (size_t)kWavesPerBlock * ricf::WAVE_BYTES2, stream, a);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL(ricf::riccati_fast_jcurve_kernel<false>, grid, dim3(256), lds, stream, a);
     return hipGetLastError();
   }
