@@ -589,7 +589,6 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   const int tid = threadIdx.x;
   const int lane = tid & 63, c = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  static_assert(!OCC2 || JC, "the shared-Q single-image layout is the J curve's");
   unsigned char* wbase = smem_raw + w * (OCC2 ? WAVE_BYTES2 : WAVE_BYTES);
   const unsigned wlds = (unsigned)(uintptr_t)wbase;
   double* tile = reinterpret_cast<double*>(wbase + (OCC2 ? OFF_T2 : OFF_T)) + g * kLdsTile;
@@ -1173,9 +1172,11 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   }
 }
 
-template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool PK = true>
-__global__ __launch_bounds__(256, 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
-  ric_body<MODE, WANTV, STAMP, EXP, false, PK>(a, (long long)blockIdx.x, 0);
+// OCC2: the two-waves-per-SIMD layout of the J curve (below) for batches that give a
+// SIMD more than one wave (a batch-shared Q; launch() picks it)
+template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool PK = true, bool OCC2 = false>
+__global__ __launch_bounds__(256, OCC2 ? 2 : 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
+  ric_body<MODE, WANTV, STAMP, EXP, false, PK, OCC2>(a, (long long)blockIdx.x, 0);
 }
 
 // The J-curve form: workgroups [b * P, (b+1) * P), P = ceil(jc_tmax / 2), run problem
@@ -1208,6 +1209,21 @@ __global__ __launch_bounds__(256, OCC2 ? 2 : 1) void riccati_fast_jcurve_kernel(
   if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true, PK, OCC2>(a, blk, h + 1);
 }
 
+// compute units of the current device (cached per device id)
+inline long long simd_units_cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
 template <int MODE, bool WANTV>
 hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
@@ -1232,7 +1248,22 @@ hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
                        dim3(256), lds, stream, a);
     return hipGetLastError();
   }
+  const bool force1 = g_opt_variant == 89, force2 = g_opt_variant == 90;  // layouts (A/B)
+#else
+  constexpr bool force1 = false, force2 = false;
 #endif
+  // mode 0 (K, k only), more waves than SIMDs and a batch-shared Q: two waves per SIMD
+  // (OCC2), which hides the dependent chains' latency the one-wave layout exposes (B =
+  // 32,768: 1.818 -> 1.540 ms).  Mode 1 streams Vxx and is HBM-bound: two waves were
+  // 4 % slower there (2.376 -> 2.476 ms), so it keeps one wave per SIMD.
+  constexpr bool occ2_mode = MODE == 0 && !WANTV;
+  if (occ2_mode && a.q_bstride == 0 && !force1 &&
+      (force2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * simd_units_cu_count())) {
+    hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 0, true, occ2_mode>),
+                       dim3((unsigned)blocks), dim3(256),
+                       (size_t)kWavesPerBlock * (occ2_mode ? WAVE_BYTES2 : WAVE_BYTES), stream, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV>), dim3((unsigned)blocks), dim3(256), lds,
                      stream, a);
   return hipGetLastError();
