@@ -146,6 +146,16 @@ struct SchedCondL2Stamped : SchedCondL2 {
 struct SchedCondLSym : SchedCondL {  // the default since round 3
   static constexpr int SYM2 = 1, NEWT = 0, PEPS = 0;
 };
+// the default at two waves per SIMD: packed images (Geo PACK), 2 workgroups per CU
+// (batches above one wave per SIMD)
+struct SchedCondLSymP : SchedCondLSym {
+  static constexpr int PACK = 1;
+};
+template <class C>
+constexpr bool has_pack() {
+  if constexpr (requires { C::PACK; }) return C::PACK != 0;
+  return false;
+}
 struct SchedCondLSymStamped : SchedCondLSym {
   static constexpr int STAMP = 1;
 };
@@ -754,6 +764,52 @@ __device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsign
 // block: M0 saved once and set per piece from the wave's LDS base plus an
 // immediate (no per-piece SGPR, no readlane of spilled addresses, no save /
 // restore pair per piece).
+// PACK: dma_step20 with the images back to back.  The full pieces first, then the
+// last piece of Q, A, QT (LM lanes) and of B (LB lanes) under a narrowed EXEC, so no
+// lane past an image's data writes into the next image; EXEC restored at the end.
+template <int OQ, int OA, int OB, int OT, int LM, int LB>
+__device__ __forceinline__ void dma_step20p(const unsigned (&vm)[6], const unsigned (&vb)[2],
+                                            __amdgpu_buffer_rsrc_t rQ, __amdgpu_buffer_rsrc_t rA,
+                                            __amdgpu_buffer_rsrc_t rB, __amdgpu_buffer_rsrc_t rT,
+                                            unsigned wlds, unsigned soM, unsigned soB) {
+  static_assert(LM > 0 && LM <= 32 && LB > 32 && LB <= 64, "partial-piece masks");
+  unsigned keep;
+  unsigned long long ex;
+#define HOP_P(R, V, OFF, SO)                                                  \
+  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
+  "], %[" #SO "] offen lds\n\t"
+  asm volatile(
+      ".p2align 3\n\t"
+      "s_mov_b32 %[keep], m0\n\t"
+      "s_mov_b64 %[ex], exec\n\t"
+      HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
+      HOP_P(rq, v3, %[q3], sm) HOP_P(rq, v4, %[q4], sm)
+      HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
+      HOP_P(ra, v3, %[a3], sm) HOP_P(ra, v4, %[a4], sm)
+      HOP_P(rb, u0, %[b0], sb)
+      HOP_P(rt, v0, %[t0], sm) HOP_P(rt, v1, %[t1], sm) HOP_P(rt, v2, %[t2], sm)
+      HOP_P(rt, v3, %[t3], sm) HOP_P(rt, v4, %[t4], sm)
+      "s_mov_b32 exec_lo, %[mlo]\n\t"
+      "s_mov_b32 exec_hi, 0\n\t"
+      HOP_P(rq, v5, %[q5], sm) HOP_P(ra, v5, %[a5], sm) HOP_P(rt, v5, %[t5], sm)
+      "s_mov_b32 exec_lo, -1\n\t"
+      "s_mov_b32 exec_hi, %[bhi]\n\t"
+      HOP_P(rb, u1, %[b1], sb)
+      "s_mov_b64 exec, %[ex]\n\t"
+      "s_mov_b32 m0, %[keep]"
+      : [keep] "=&s"(keep), [ex] "=&s"(ex)
+      : [w] "s"(wlds), [sm] "s"(soM), [sb] "s"(soB), [rq] "s"(rQ), [ra] "s"(rA), [rb] "s"(rB),
+        [rt] "s"(rT), [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]),
+        [v4] "v"(vm[4]), [v5] "v"(vm[5]), [u0] "v"(vb[0]), [u1] "v"(vb[1]),
+        [q0] "i"(OQ), [q1] "i"(OQ + 1024), [q2] "i"(OQ + 2048), [q3] "i"(OQ + 3072),
+        [q4] "i"(OQ + 4096), [q5] "i"(OQ + 5120), [a0] "i"(OA), [a1] "i"(OA + 1024),
+        [a2] "i"(OA + 2048), [a3] "i"(OA + 3072), [a4] "i"(OA + 4096), [a5] "i"(OA + 5120),
+        [b0] "i"(OB), [b1] "i"(OB + 1024), [t0] "i"(OT), [t1] "i"(OT + 1024),
+        [t2] "i"(OT + 2048), [t3] "i"(OT + 3072), [t4] "i"(OT + 4096), [t5] "i"(OT + 5120),
+        [mlo] "i"((int)((1ull << LM) - 1ull)), [bhi] "i"((int)((1ull << (LB - 32)) - 1ull))
+      : "memory", "scc");
+#undef HOP_P
+}
 template <int OQ, int OA, int OB, int OT>
 __device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsigned (&vb)[2],
                                            __amdgpu_buffer_rsrc_t rQ, __amdgpu_buffer_rsrc_t rA,
@@ -842,19 +898,28 @@ __device__ __forceinline__ void dma_stepAB(const unsigned (&vm)[6], const unsign
 #undef HOP_P
 }
 
-template <int S, int MM, int ES = 8>  // ES: bytes per element of the streamed blocks
+// PACK (the conditioned kernel at two waves per SIMD, SchedCondLSymP): the images
+// packed back to back (the last DMA piece of each block type runs on the lanes that
+// carry data only, so nothing is written past an image) and the tile slot cut to the
+// zero area the lanes past s - 1 read: 19,400 B per wave at s = 13 fp64, so two 4-wave
+// workgroups fit a CU's 160 KiB
+template <int S, int MM, int ES = 8, bool PACK = false>  // ES: bytes per streamed element
 struct Geo {
   static constexpr int SS = S * S;
   static constexpr int CHM = (SS * ES + 15) / 16;     // 16-B chunks per S x S block
   static constexpr int IMGM = CHM * 16;               // bytes per problem image (16-aligned)
   static constexpr int NJM = (kProbPerWave * CHM + 63) / 64;  // DMA instrs per block type
-  static constexpr int IMGM_W = NJM * 1024;           // bytes per wave image (DMA writes 1 KiB)
+  // bytes per wave image (a full DMA piece writes 1 KiB)
+  static constexpr int IMGM_W = PACK ? kProbPerWave * IMGM : NJM * 1024;
   static constexpr int SM = S * MM;
   static constexpr int CHB = (SM * ES + 15) / 16;
   static constexpr int IMGB = CHB * 16;
   static constexpr int NJB = (kProbPerWave * CHB + 63) / 64;
-  static constexpr int IMGB_W = NJB * 1024;
-  static constexpr int TILE_W = kProbPerWave * kLdsTile * 8;
+  static constexpr int IMGB_W = PACK ? kProbPerWave * IMGB : NJB * 1024;
+  // lanes of the last piece that carry data (PACK masks the rest)
+  static constexpr int LASTM = kProbPerWave * CHM - 64 * (NJM - 1);
+  static constexpr int LASTB = kProbPerWave * CHB - 64 * (NJB - 1);
+  static constexpr int TILE_W = PACK ? 8 * (SS + 8) : kProbPerWave * kLdsTile * 8;
   // per-wave layout: [Q][A][QT][B][tiles]
   static constexpr int OFF_Q = 0, OFF_A = IMGM_W, OFF_QT = 2 * IMGM_W, OFF_B = 3 * IMGM_W;
   static constexpr int OFF_T = 3 * IMGM_W + IMGB_W;
@@ -1521,10 +1586,13 @@ struct CondTraj {
 // reads; the arithmetic stays fp64 (fp32 DPP FMAs issue no faster at one wave
 // per SIMD) and J / J* are rounded to fp32 on the store.
 template <class C, int S, int MM, class T = double>
-__global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
+__global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(LftArgs<T> a) {
   constexpr int ES = (int)sizeof(T);
   constexpr bool F32 = ES == 4;
-  using G = Geo<S, MM, ES>;
+  using G = Geo<S, MM, ES, has_pack<C>()>;
+  static_assert(!has_pack<C>() || (!F32 && !has_traj<C>() && G::NJM == 6 && G::NJB == 2 &&
+                                   2 * kWavesPerBlock * G::WAVE_BYTES <= 160 * 1024),
+                "packed images: s = 13 fp64 blocks, two workgroups per CU");
   constexpr bool TRAJ = has_traj<C>();
   static_assert(!F32 || (!TRAJ && !has_ldspipe<C>()), "fp32 blocks: augmented form, plain reads");
   constexpr int NN = G::NN;
@@ -1561,7 +1629,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
   // SYM2: eps I rows for the predict, read as element 15 + I - c of a zero-padded
   // vector holding eps at element 15 (after the zero area)
   constexpr int EPSV = 192;  // doubles from the zero area's start
-  static_assert(G::TILE_W >= 8 * (EPSV + 32), "eps vector in the tile slot");
+  static_assert(!has_peps<C>() || G::TILE_W >= 8 * (EPSV + 32), "eps vector in the tile slot");
   if constexpr (has_peps<C>()) {
     if (lane < 32) zarea[EPSV + lane] = lane == 15 ? 1e-9 : 0.0;
   }
@@ -1628,8 +1696,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_kernel(LftArgs<T> a) {
           soV + NN * 8, soV, soU);
     } else if constexpr (G::NJM == 6 && G::NJB == 2) {
       const unsigned soM = (unsigned)(k * SS * ES), soB = (unsigned)(k * SM * ES);
-      dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
-                                                         soB);
+      if constexpr (has_pack<C>())
+        dma_step20p<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT, G::LASTM, G::LASTB>(
+            voM, voB, rQ, rA, rB, rT, wlds, soM, soB);
+      else
+        dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
+                                                           soB);
     } else {
       const unsigned soM = (unsigned)(k * SS * ES), soB = (unsigned)(k * SM * ES);
 #pragma unroll
@@ -2293,6 +2365,21 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
 // the reference association alone; HOP_OPT_FORCE_HANDOVER: every problem handed
 // over).  Developer builds (HOP_DEV) add the A/B schedules of DESIGN.md 3.2 by
 // number (hop_set_options variant).
+// compute units of the current device (cached per device id)
+static long long cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv) return hipErrorNotSupported;
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
@@ -2391,6 +2478,23 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (opt(HOP_OPT_STAMPS))
     return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
 #endif
+  // more waves than SIMDs: the packed-image layout at two waves per SIMD (the rerun
+  // launch keeps the LFT kernel's own layout)
+#ifdef HOP_DEV
+  const bool pack1 = variant == 92, pack2 = variant == 91;  // forced layouts (A/B)
+#else
+  constexpr bool pack1 = false, pack2 = false;
+#endif
+  if (!pack1 && (pack2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count())) {
+    LftArgs<double> c = a;
+    c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+    hipError_t e = launch(v2::lft_cond_kernel<v2::SchedCondLSymP, 13, 4>,
+                          (size_t)v2::Geo<13, 4, 8, true>::WAVE_BYTES * kWavesPerBlock, c);
+    if (e != hipSuccess) return e;
+    LftArgs<double> r = a;
+    r.cond = 1;
+    return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, r);
+  }
   // default (variant 40): conditioned prefix + rerun of the problems it flagged; the
   // stage / terminal inverses of the unhalved symmetric sums (SYM2: 1-2 % faster than
   // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_ab_pe.txt)
