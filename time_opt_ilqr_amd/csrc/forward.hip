@@ -88,6 +88,29 @@ __device__ inline void wrap_err(const double* a, const double* b, unsigned mask,
 // running-cost increment of step k (solver.py:87-95); false if e or du is not finite
 // SH: every cost block is shared by the batch (all batch strides 0), so the block
 // addresses are wave-uniform and the compiler reads them through the scalar cache
+// (stage_inc_e: the same with the wrapped error e given)
+template <int n, int m, bool SH = false>
+__device__ inline bool stage_inc_e(const CostArgs& c, long long b_, const double* x,
+                                   const double* e, const double* u, double& acc, bool diag) {
+  const long long b = SH ? 0 : b_;
+  double du[m];
+  const double* ur = c.u_ref + b * c.ur_bs;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < n; ++i) ok = ok && fin(e[i]);
+#pragma unroll
+  for (int i = 0; i < m; ++i) {
+    du[i] = u[i] - ur[i];
+    ok = ok && fin(du[i]);
+  }
+  const double q = diag ? half_quad_diag<n>(c.Q + b * c.q_bs, e) : half_quad<n>(c.Q + b * c.q_bs, e);
+  const double r =
+      diag ? half_quad_diag<m>(c.R + b * c.r_bs, du) : half_quad<m>(c.R + b * c.r_bs, du);
+  acc += (q + r) + c.w[b * c.w_bs];
+  if (c.obs) acc += obstacle_c(c.obs, c.n_obs, x[0], x[1]);
+  return ok;
+}
+
 template <int n, int m, bool SH = false, int WM = -1>
 __device__ inline bool stage_inc(const CostArgs& c, long long b_, const double* x,
                                  const double* u, double& acc, bool diag = false) {
@@ -197,9 +220,26 @@ __global__ __launch_bounds__(TPB) void cost_kernel(CostArgs c, const double* X, 
 // batch * n_alpha + b computes problem b's J_old.
 // Step k+1's rows of X, U, K, k are loaded at the top of step k (register double
 // buffer), so their latency hides under step k's dynamics and cost.
-template <int SYS, bool SH, int WM>
+// the two lanes of a (problem, alpha) pair exchange values through a DPP quad
+// permutation [1, 0, 3, 2] (lanes 2j and 2j + 1 swap)
+__device__ inline double pair_swap(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+// PAIR (quadrotor, the default there): two lanes per (problem, alpha) rollout.  Lane h
+// forms controls 2h, 2h + 1 (its two rows of K_k: half the K.dx chains, half the
+// prefetched rows and their registers) and one of the two independent sin/cos pairs
+// (h = 0: roll, h = 1: yaw); the partner's values arrive by pair_swap.  Everything
+// else -- the error, the cost, the pitch's sin/cos/tan, the dynamics -- both lanes
+// evaluate with the same operations in the same order, so the rollout, J and the
+// rows written are bit-identical to the one-lane form.  Lane h writes half of each
+// X', U' row.
+template <int SYS, bool SH, int WM, bool PAIR = false>
 __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   constexpr int n = state_dim(SYS), m = control_dim(SYS);
+  static_assert(!PAIR || (n == 12 && m == 4), "two-lane rollouts: the quadrotor");
   // shared cost blocks staged in LDS once per workgroup (every lane reads the same
   // address: a broadcast, no bank conflicts); per-problem blocks stay in HBM
   constexpr int NQ = n * n, NR = m * m;
@@ -239,12 +279,15 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   // lanes [0, batch * n_alpha): (problem, step size) rollouts; the J_old lanes of
   // every problem come after them, so no wave mixes the two loops (a mixed wave
   // runs both, one after the other)
-  const int S = a.n_alpha + 1;
+  constexpr int LP = PAIR ? 2 : 1;  // lanes per (problem, alpha) rollout
   const long long q = (long long)blockIdx.x * TPB + threadIdx.x;
-  if (q >= a.batch * S) return;
   const long long nr = a.batch * a.n_alpha;
-  const long long b = q < nr ? q / a.n_alpha : q - nr;
-  const int slot = q < nr ? (int)(q - b * a.n_alpha) : a.n_alpha;
+  if (q >= LP * nr + a.batch) return;
+  const bool roll = q < LP * nr;
+  const long long pr = roll ? q / LP : 0;
+  const int h = PAIR ? (int)(q & 1) : 0;
+  const long long b = roll ? pr / a.n_alpha : q - LP * nr;
+  const int slot = roll ? (int)(pr - b * a.n_alpha) : a.n_alpha;
   const int N = a.N;
   const double* X = a.X + b * (long long)(N + 1) * n;
   const double* U = a.U + b * (long long)N * m;
@@ -256,7 +299,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   }
   double* J = a.Jc + b * a.n_alpha + slot;
   if (!active) {
-    *J = NAN;
+    if (h == 0) *J = NAN;
     return;
   }
   const double alpha = a.alphas[slot];
@@ -265,6 +308,96 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
   const long long row = (long long)(N + 1) * n + (long long)N * m;
   double* Xc = a.ws + (b * a.n_alpha + slot) * row;
   double* Uc = Xc + (long long)(N + 1) * n;
+  if constexpr (PAIR) {
+    constexpr int HN = n / 2, HM = m / 2;
+    double x[n];
+#pragma unroll
+    for (int i = 0; i < n; ++i) x[i] = X[i];
+#pragma unroll
+    for (int i = 0; i < HN; ++i) Xc[HN * h + i] = h ? x[HN + i] : x[i];
+    double acc = 0.0;
+    bool ok = true;
+    double nu[HM], nk[HM], nx[n], nK[HM * n];  // this lane's rows of the next step
+    auto load = [&](int k) {
+#pragma unroll
+      for (int j = 0; j < HM; ++j) nu[j] = U[k * m + HM * h + j], nk[j] = kf[k * m + HM * h + j];
+#pragma unroll
+      for (int i = 0; i < n; ++i) nx[i] = X[k * n + i];
+#pragma unroll
+      for (int i = 0; i < HM * n; ++i) nK[i] = K[(long long)k * m * n + HM * h * n + i];
+    };
+    if (N > 0) load(0);
+    for (int k = 0; k < N; ++k) {
+      if constexpr (SH) asm volatile("" ::: "memory");
+      double uh[HM];
+      double e[n];  // the stage cost's error x - xg (k < T)
+      if (k < T) {
+        // the wrapped components split over the pair: lane 0 wraps dx = x - x_ref,
+        // lane 1 the cost's e = x - xg (same operations, exchanged)
+        static_assert(WM >= 0, "two-lane rollouts: the default wrap mask");
+        const double* xgp = cl.xg + (SH ? 0 : b * cl.xg_bs);
+        double dx[n];
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          if ((WM >> i) & 1) {
+            const double wv = wrap_angle(x[i] - (h ? xgp[i] : nx[i]));
+            const double o = pair_swap(wv);
+            dx[i] = h ? o : wv;
+            e[i] = h ? wv : o;
+          } else {
+            dx[i] = x[i] - nx[i];
+            e[i] = x[i] - xgp[i];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < HM; ++j) {
+          double r = 0.0;
+#pragma unroll
+          for (int i = 0; i < n; ++i) r = fma(nK[j * n + i], dx[i], r);
+          uh[j] = nu[j] + (r + alpha * nk[j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < HM; ++j) uh[j] = nu[j];
+      }
+      double u[m];
+#pragma unroll
+      for (int j = 0; j < HM; ++j) {
+        const double o = pair_swap(uh[j]);
+        u[j] = h ? o : uh[j];
+        u[HM + j] = h ? uh[j] : o;
+      }
+      if (k + 1 < N) load(k + 1);
+      if (k < T) ok = stage_inc_e<n, m, SH>(cl, b, x, e, u, acc, diag) && ok;
+#pragma unroll
+      for (int j = 0; j < HM; ++j) Uc[k * m + HM * h + j] = uh[j];
+      // trigonometry: roll (h = 0) or yaw (h = 1) on this lane, the pitch on both
+      QuadTrig t;
+      const double ang = h ? x[8] : x[6];
+      const double sa = sin(ang), ca = cos(ang);
+      const double so = pair_swap(sa), co = pair_swap(ca);
+      t.sphi = h ? so : sa, t.cphi = h ? co : ca;
+      t.spsi = h ? sa : so, t.cpsi = h ? ca : co;
+      quad_trig_th(x[7], t);
+      double xn[n];
+      f_quadrotor_t(x, u, a.dt, t, xn);
+      bool f = true;
+#pragma unroll
+      for (int i = 0; i < n; ++i) f = f && fin(xn[i]);
+      if (!f) {  // rejected step size (both lanes see the same xn)
+        if (h == 0) *J = NAN;
+        return;
+      }
+#pragma unroll
+      for (int i = 0; i < HN; ++i) Xc[(k + 1) * n + HN * h + i] = h ? xn[HN + i] : xn[i];
+#pragma unroll
+      for (int i = 0; i < n; ++i) x[i] = xn[i];
+      if (k + 1 == T) acc += terminal_cost<n, SH, WM>(cl, b, x, ok, diag);
+    }
+    if (T == 0) ok = false;
+    if (h == 0) *J = ok ? acc : INFINITY;
+    return;
+  }
   double x[n];
 #pragma unroll
   for (int i = 0; i < n; ++i) Xc[i] = x[i] = X[i];
@@ -461,13 +594,30 @@ hipError_t launch_all(int which, const void* args, hipStream_t st) {
     }
     default: {
       const FwdArgs& a = *(const FwdArgs*)args;
-      const long long lanes = a.batch * (a.n_alpha + 1);
+      long long lanes = a.batch * (a.n_alpha + 1);
       const CostArgs& c = a.c;
       const bool shared = !c.xg_bs && !c.ur_bs && !c.q_bs && !c.r_bs && !c.qf_bs && !c.w_bs;
       // the reference's wrap_idx of each system (systems.py:48, 110, 228, 263, 347)
       constexpr int WD = SYS == kCartpole || SYS == kSegway ? (1 << 2)
                          : SYS == kQuadrotor                ? (7 << 6)
                                                             : 0;
+#ifdef HOP_DEV
+      const bool one_lane = g_opt_variant == 93;  // the one-lane quadrotor rollout (A/B)
+#else
+      constexpr bool one_lane = false;
+#endif
+      if constexpr (SYS == kQuadrotor) {
+        if (shared && c.wrap_mask == (unsigned)WD && !one_lane) {  // two lanes per rollout
+          lanes = 2 * a.batch * a.n_alpha + a.batch;
+          hipLaunchKernelGGL((linesearch_kernel<SYS, true, WD, true>),
+                             dim3((unsigned)((lanes + TPB - 1) / TPB)), dim3(TPB), 0, st, a);
+          hipError_t e = hipGetLastError();
+          if (e != hipSuccess) return e;
+          hipLaunchKernelGGL((linesearch_pick_kernel<SYS>), dim3((unsigned)a.batch), dim3(256), 0,
+                             st, a);
+          break;
+        }
+      }
       const dim3 grid((unsigned)((lanes + TPB - 1) / TPB));
       if (shared && c.wrap_mask == (unsigned)WD)
         hipLaunchKernelGGL((linesearch_kernel<SYS, true, WD>), grid, dim3(TPB), 0, st, a);
