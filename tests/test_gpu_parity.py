@@ -442,6 +442,32 @@ def test_cond_forced_handover_is_the_lft_kernel(dev):
     assert int(r.status[4]) & orc.ST_LU
 
 
+def test_cond_packed_layout_handover_large_batch(dev):
+    """B = 4101 (more waves than SIMDs): the conditioned kernel runs its packed-image
+    layout at two waves per SIMD.  Forced hand-over: the rerun launch (the LFT kernel in
+    its own layout) recomputes every problem, bitwise equal to HOP_OPT_REFERENCE_ASSOC;
+    default: the problem that needs chol_inv's LU slot is handed over (its status bits
+    and J the LFT kernel's, bitwise), the rest within 1e-9 of the reference association."""
+    import torch
+    from time_opt_ilqr_amd import _lib, engine
+    Bn, s, m, N = 4101, 13, 4, 24
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(5151, Bn, s, m, N)
+    Q = Q.copy()
+    Q[4099, 7] = -np.eye(s)  # LU slot, in the last workgroup
+    args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
+    with _lib.options(force_handover=True):
+        f = engine.propagate(*args, t_min=3, t_max=N)
+    with _lib.options(reference_assoc=True):
+        r = engine.propagate(*args, t_min=3, t_max=N)
+    d = engine.propagate(*args, t_min=3, t_max=N)
+    assert torch.equal(f.J, r.J) and torch.equal(f.status, r.status)
+    assert torch.equal(f.t_star, r.t_star)
+    assert int(r.status[4099]) & orc.ST_LU
+    assert torch.equal(d.status, r.status)
+    assert torch.equal(d.J[4099], r.J[4099])
+    assert float(((d.J - r.J).abs() / r.J.abs()).max()) <= 1e-9
+
+
 @pytest.mark.devbuild
 @pytest.mark.parametrize("s,m,dt", [(5, 1, "f32"), (3, 1, "f64"), (4, 2, "f64")])
 def test_small_cond_kernel(dev, s, m, dt):
