@@ -1210,7 +1210,7 @@ __global__ __launch_bounds__(256, OCC2 ? 2 : 1) void riccati_fast_jcurve_kernel(
 }
 
 // compute units of the current device (cached per device id)
-inline long long simd_units_cu_count() {
+inline long long cu_count() {
   static int cached[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
@@ -1258,7 +1258,7 @@ hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   // 4 % slower there (2.376 -> 2.476 ms), so it keeps one wave per SIMD.
   constexpr bool occ2_mode = MODE == 0 && !WANTV;
   if (occ2_mode && a.q_bstride == 0 && !force1 &&
-      (force2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * simd_units_cu_count())) {
+      (force2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count())) {
     hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 0, true, occ2_mode>),
                        dim3((unsigned)blocks), dim3(256),
                        (size_t)kWavesPerBlock * (occ2_mode ? WAVE_BYTES2 : WAVE_BYTES), stream, a);
