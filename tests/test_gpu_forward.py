@@ -165,6 +165,45 @@ def test_linesearch_mixed_batch_vs_oracle(dev, golden_dir):
     assert -1 in seen and 0 in seen and len(seen) >= 4, seen
 
 
+def test_linesearch_two_lane_and_one_lane_layouts_bitwise(dev, golden_dir):
+    """The quadrotor line search runs two lanes per (problem, alpha) rollout while the
+    launch fits one wave per SIMD (37 problems here) and one lane per rollout beyond
+    that (6,000 problems: 66,000 two-lane lanes would exceed the 65,536 of one wave per
+    SIMD).  The same problems at both sizes: J, the accepted index, X' and U' bitwise
+    equal; per-problem horizons, scaled feed-forwards (rejections, non-finite steps)."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    d, sid, wrap, obs = _case(golden_dir, "quadrotor")
+    g = lambda k: d[f"f1_{k}"]  # noqa: E731
+    N, T0 = int(d["N"]), int(g("T_star"))
+    nb = 37
+    scales = np.array([1, 3, 10, 30, 100, 300, -1, -10, 0.3])
+    sc = scales[np.arange(nb) % len(scales)]
+    X = np.stack([g("X")] * nb)
+    U = np.stack([g("U")] * nb)
+    K = np.zeros((nb, N, 4, 12))
+    k = np.zeros((nb, N, 4))
+    K[:, :T0] = g("K")
+    k[:, :T0] = g("k")[None] * sc[:, None, None]
+    T = np.full(nb, T0)
+    T[3], T[10:14] = 0, [1, 5, T0 // 2, N]
+    cost = _cost(d, wrap, obs, dev)
+    small = engine.forward_linesearch(2, _t(X, dev), _t(U, dev), torch.as_tensor(T), _t(K, dev),
+                                      _t(k, dev), cost, float(d["dt"]))
+    rep = (6000 + nb - 1) // nb
+    big = engine.forward_linesearch(2, _t(np.tile(X, (rep, 1, 1)), dev),
+                                    _t(np.tile(U, (rep, 1, 1)), dev),
+                                    torch.as_tensor(np.tile(T, rep)), _t(np.tile(K, (rep, 1, 1, 1)), dev),
+                                    _t(np.tile(k, (rep, 1, 1)), dev), cost, float(d["dt"]))
+    for j in (0, rep // 2, rep - 1):
+        sl = slice(j * nb, (j + 1) * nb)
+        assert torch.equal(big.accepted[sl], small.accepted)
+        assert torch.equal(big.J[sl].nan_to_num(7.0), small.J.nan_to_num(7.0))
+        assert torch.equal(big.X[sl].nan_to_num(7.0), small.X.nan_to_num(7.0))
+        assert torch.equal(big.U[sl].nan_to_num(7.0), small.U.nan_to_num(7.0))
+    assert len(set(small.accepted.tolist())) >= 3
+
+
 def test_obstacle_cost_kernel(dev):
     from time_opt_ilqr_amd import engine, systems
     rng = np.random.default_rng(5)

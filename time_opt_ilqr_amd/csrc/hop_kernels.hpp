@@ -10,6 +10,21 @@ namespace hop {
 extern unsigned g_opt_flags;
 extern int g_opt_variant;
 inline bool opt(unsigned f) { return (g_opt_flags & f) != 0u; }
+// compute units of the current device, cached per device id: the launches that pick
+// a layout by waves per SIMD (4 SIMDs per CU) compare against 4 x this
+inline long long cu_count() {
+  static int cached[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cached[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
 #ifdef HOP_DEV
 inline constexpr bool kDevBuild = true;
 #else

@@ -2365,21 +2365,6 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
 // the reference association alone; HOP_OPT_FORCE_HANDOVER: every problem handed
 // over).  Developer builds (HOP_DEV) add the A/B schedules of DESIGN.md 3.2 by
 // number (hop_set_options variant).
-// compute units of the current device (cached per device id)
-static long long cu_count() {
-  static int cached[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    cached[dev] = cus;
-  }
-  return cached[dev];
-}
-
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   if (a.dbg_efg || a.dbg_pre || a.r_kstride != 0 || !a.r_is_inv) return hipErrorNotSupported;
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;

@@ -1209,21 +1209,6 @@ __global__ __launch_bounds__(256, OCC2 ? 2 : 1) void riccati_fast_jcurve_kernel(
   if (h + 1 < a.jc_tmax - h) ric_body<1, false, false, 0, true, PK, OCC2>(a, blk, h + 1);
 }
 
-// compute units of the current device (cached per device id)
-inline long long cu_count() {
-  static int cached[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    cached[dev] = cus;
-  }
-  return cached[dev];
-}
-
 template <int MODE, bool WANTV>
 hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
