@@ -1594,7 +1594,8 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
                                    2 * kWavesPerBlock * G::WAVE_BYTES <= 160 * 1024),
                 "packed images: s = 13 fp64 blocks, two workgroups per CU");
   constexpr bool TRAJ = has_traj<C>();
-  static_assert(!F32 || (!TRAJ && !has_ldspipe<C>()), "fp32 blocks: augmented form, plain reads");
+  static_assert(!F32 || (!TRAJ && dstag<C>() == 0 && !has_sym2<C>() && !has_peps<C>()),
+                "fp32 blocks: augmented form, halved sums");
   constexpr int NN = G::NN;
   static_assert(S < kRowLanes, "m rides on lane S");
   static_assert(G::TILE_W >= 8 * S * S + 64, "zero area in the tile slot");
@@ -1808,7 +1809,38 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     double ar[has_arow<C>() ? S : 1];  // AROW: rows of A_k, read before the image is refilled
     float mb[MF ? 4 : 1][4], ma[MF ? 4 : 1][4];  // MFMA predict operands (likewise)
     stamp(1);
-    if constexpr (has_ldspipe<C>() && !TRAJ) {
+    if constexpr (has_ldspipe<C>() && !TRAJ && F32) {
+      // fp32 images: Q's converting reads, then QT's 4-byte reads under the E sweep
+      // and A_k / B_k's under the X sweep, converted after (the offset form in fp64)
+      const bool in = c < S;
+      const T* qc = in ? imQ + c : zareaT;
+      const T* qr = in ? imQ + S * c : zareaT;
+#pragma unroll
+      for (int i = 0; i < S; ++i) NE[i] = 0.5 * ((double)qc[S * i] + (double)qr[i]);
+      static_for<S>([&](auto I) { NE[I] += sel_lane<I>(0.0, 1e-9 - 1.0); });
+      stamp(2);
+      float o[2 * S];
+      const unsigned aq[2] = {in ? lds_addr(imT) + 4u * c : zaddr,
+                              in ? lds_addr(imT) + 4u * S * c : zaddr};
+      double d1 = 1.0, d2 = 1.0;
+      SweepQSymF<S>::run(NE, d1, o, aq);
+#pragma unroll
+      for (int i = 0; i < S; ++i) NX[i] = 0.5 * ((double)o[i] + (double)o[S + i]);
+      static_for<S>([&](auto I) { NX[I] += sel_lane<I>(0.0, 1e-9 - 1.0); });
+      float o2[2 * S + MM];
+      const unsigned ab[3] = {in ? lds_addr(imA) + 4u * S * c : zaddr, lds_addr(imA) + 4u * c,
+                              in ? lds_addr(imB) + 4u * MM * c : zaddr};
+      SweepQABF<S>::run(NX, d2, o2, ab);
+      bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        at[j] = (double)o2[j];
+        if constexpr (has_arow<C>()) ar[j] = (double)o2[S + j];
+      }
+#pragma unroll
+      for (int q = 0; q < MM; ++q) brow[q] = (double)o2[2 * S + q];
+      stamp(3);
+    } else if constexpr (has_ldspipe<C>() && !TRAJ) {
       // QT's sym reads ride under the E sweep, A_k / B_k's under the X sweep
       sym_from_z<C, S>(imQ, zaddr, c, NE);
       stamp(2);
@@ -2498,7 +2530,7 @@ hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
   const int var = g_opt_variant;
   if (opt(HOP_OPT_REFERENCE_ASSOC) ||
-      (var != 0 && var != 40 && var != 41 && (!kDevBuild || (var != 56 && var != 57))))
+      (var != 0 && var != 40 && var != 41 && (!kDevBuild || (var != 56 && var != 57 && var != 95))))
     return hipErrorNotSupported;
   using G = v2::Geo<13, 4, 4>;
   const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
@@ -2511,7 +2543,14 @@ hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
                        stream, c);
   else
 #endif
-  hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4, float>), dim3((unsigned)blocks),
+#ifdef HOP_DEV
+  if (var == 95)  // plain converting reads (the round-2 fp32-block kernel, A/B)
+    hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCond, 13, 4, float>), dim3((unsigned)blocks),
+                       dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
+  else
+#endif
+  // QT / A / B reads under the two sweeps (SchedCondL: the fp64 default's placement)
+  hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondL, 13, 4, float>), dim3((unsigned)blocks),
                      dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
   if (var == 41 || var == 57) return hipGetLastError();
   LftArgs<float> r = a;
