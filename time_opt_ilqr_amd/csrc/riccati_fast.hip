@@ -571,7 +571,11 @@ __device__ unsigned long long g_ricf_stamp[16];
 // (Quu_reg + eps I)^-1 Qux = -K on lanes 0..11 directly: no K product, no lane
 // rotations of Quu, no inverse rebuilt from the sweep's offset form; Qu, k and R du
 // live on lanes 12..15 likewise.  PK = false keeps the round-2 form (developer A/B).
-template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC, bool PK = true, bool OCC2 = false>
+// QL (default): the one-wave layout reads the step's Qxx accumulator start (the Q
+// image) inside the V [A|B] product's asm block (LaneRowsQ) instead of with the
+// step's other reads, so its LDS latency hides under the 144 FMAs
+template <int MODE, bool WANTV, bool STAMP, int EXP, bool JC, bool PK = true, bool OCC2 = false,
+          bool QL = true>
 __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long blk, int jl) {
   constexpr int S = NX, MM = MU;
   unsigned long long sec[12] = {};
@@ -778,12 +782,15 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     double Qxx[S];  // Q (the accumulator start of Qxx = Q + A^T V A)
     double qrow[S];  // Q row c (lx = Q e): loop-invariant registers, or (OCC2) LDS
     if constexpr (!OCC2) copy(qrow, qrow_r);
+    constexpr bool QLATE = QL && !OCC2;
     if constexpr (FIRST) {
       if constexpr (OCC2) read_step_q_qr<IMG>(ad, xa, ua, qa, qra, ab, xi, ui, Qxx, qrow);
+      else if constexpr (QLATE) read_step<IMG>(ad, xa, ua, ab, xi, ui);
       else read_step_q<IMG>(ad, xa, ua, qa, ab, xi, ui, Qxx);
     } else {
       double t[S];
       if constexpr (OCC2) read_step_vt_q_qr<IMG>(ad, xa, ua, tra, qa, qra, ab, xi, ui, t, Qxx, qrow);
+      else if constexpr (QLATE) read_step_vt<IMG>(ad, xa, ua, tra, ab, xi, ui, t);
       else read_step_vt_q<IMG>(ad, xa, ua, tra, qa, ab, xi, ui, t, Qxx);
       // _sym of step i+1's Vxx; a row that did not commit carried (and parked) its
       // old, exactly symmetric V, for which this is V itself
@@ -833,7 +840,8 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
     // products as one dependent DPP chain per output row (accumulator forwarded)
     double VA[S];
     zero(VA);
-    static_for<S>([&](auto I) { LaneDot<S>::fma(VA[I], V[I], ab); });  // V [A|B]
+    if constexpr (QLATE) LaneRowsQ<S>::run(VA, Qxx, V, ab, qa);  // V [A|B], Q's rows
+    else static_for<S>([&](auto I) { LaneDot<S>::fma(VA[I], V[I], ab); });  // V [A|B]
     stamp(4);
     // Q + A^T V A is accumulated into Qxx under the Quu^-1 sweep below
     double Uq[MM];  // Qux rows (lanes < n): P under PK
@@ -1174,9 +1182,10 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
 
 // OCC2: the two-waves-per-SIMD layout of the J curve (below) for batches that give a
 // SIMD more than one wave (a batch-shared Q; launch() picks it)
-template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool PK = true, bool OCC2 = false>
+template <int MODE, bool WANTV, bool STAMP = false, int EXP = 0, bool PK = true, bool OCC2 = false,
+          bool QL = true>
 __global__ __launch_bounds__(256, OCC2 ? 2 : 1) void riccati_fast_kernel(RiccatiArgs<double> a) {
-  ric_body<MODE, WANTV, STAMP, EXP, false, PK, OCC2>(a, (long long)blockIdx.x, 0);
+  ric_body<MODE, WANTV, STAMP, EXP, false, PK, OCC2, QL>(a, (long long)blockIdx.x, 0);
 }
 
 // The J-curve form: workgroups [b * P, (b+1) * P), P = ceil(jc_tmax / 2), run problem
@@ -1231,6 +1240,11 @@ hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   if (g_opt_variant == 84) {  // separate Qux / Quu rows (the round-3 schedule, A/B)
     hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 0, false>), dim3((unsigned)blocks),
                        dim3(256), lds, stream, a);
+    return hipGetLastError();
+  }
+  if (g_opt_variant == 96) {  // Q image read with the step's other reads (A/B)
+    hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 0, true, false, false>),
+                       dim3((unsigned)blocks), dim3(256), lds, stream, a);
     return hipGetLastError();
   }
   const bool force1 = g_opt_variant == 89, force2 = g_opt_variant == 90;  // layouts (A/B)
