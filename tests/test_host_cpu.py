@@ -769,3 +769,35 @@ def test_packed_sweep_colchain_block_emulated():
     for r in range(12):
         want = acc0[r] + sum(X[j][r] * Yc[j] for j in range(12))
         assert np.abs(regs[12 + r] - want).max() < 1e-12
+
+
+def test_lane_rows_q_block_emulated():
+    """LaneRowsQ<12> (the Riccati step's V [A|B] product with the Q image's 12 reads
+    riding in it): every output row is the same j-ordered chain as LaneDot<12>::fma
+    (bitwise in the emulation), and q[r] is LDS row r at the lane's address + 128 r
+    (CPU emulation of the instruction strings, tools/emu_dpp.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(43)
+    n = 12
+    acc0 = rng.standard_normal((n, 16))
+    X = rng.standard_normal((n, 16))
+    Y = rng.standard_normal((n, 16))
+    lds = rng.standard_normal(4096)
+    base = 8 * 100 + 8 * np.arange(16)  # lane c reads Q image row r at base + 128 r
+    regs = {}
+    for i in range(n):
+        regs[i] = acc0[i].copy()
+        regs[n + i] = np.full(16, np.nan)
+        regs[2 * n + i] = X[i]
+        regs[3 * n + i] = Y[i]
+    regs[4 * n] = base.astype(float)
+    E.run(E.extract(inc, "LaneRowsQ", "12"), regs, lds=lds)
+    for i in range(n):
+        want = acc0[i].copy()
+        for j in range(n):  # LaneDot<12>::fma's order: acc += bcast_j(x) * y[j], j = 0..11
+            want = want + np.full(16, X[i][j]) * Y[j]
+        assert np.array_equal(regs[i], want)
+        assert np.array_equal(regs[n + i], lds[(base + 128 * i) // 8])
