@@ -13,7 +13,10 @@ synthetic blocks resident in HBM before timing.  Rank 0 prints ONE JSON line.
 Workloads (BASELINE.json configs):
   lft (default)  N=1: config 2 -- Quadrotor shape s=13, m=4, N=100, 4096 problems, fp64.
                  N>1: config 4 -- the same shape, 32768 problems per GPU (262144 on 8
-                 GPUs), contiguous shards, weak scaling.
+                 GPUs), contiguous shards, weak scaling.  --scaling strong keeps config
+                 4's global batch of 262144 for every N (--global-batch to change it);
+                 the N=1 default line carries both config-4 anchors (32768 and 262144
+                 problems on one GPU).
   config3        Cartpole shape s=5, m=1, N=200, 65536 problems, fp32 (small-s kernel),
                  blocks in the kernel's native tile64 layout (include/hop.h; --layout
                  batch for batch-major blocks, which is also timed as a side figure).
@@ -345,7 +348,7 @@ def _select_gains_workload(args, world, lo, hi, dev):
 
     def launch():
         sel = engine.propagate_traj(A, Bm, a_res, X, U, xg, ur, Q, Rinv, P, w, t_min=t_min,
-                                    t_max=N, rho_reg=1.0)
+                                    t_max=N, rho_reg=args.rho_reg)
         ric = engine.riccati(A, Bm, X, U, xg, ur, Q, R, P, sel.t_star, 1e-3, mode=0)
         sel.riccati_status = ric.status
         return sel
@@ -358,7 +361,7 @@ def _select_gains_workload(args, world, lo, hi, dev):
                 executed=cf_flops(N, n + 1, m) + riccati_flops(n, m, N),
                 flops_fn=lambda tbar: lft_flops(N, n + 1, m) + riccati_flops(n, m, 1) * tbar,
                 executed_fn=lambda tbar: cf_flops(N, n + 1, m) + riccati_flops(n, m, 1) * tbar,
-                t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None)
+                t_min=t_min, t_max=N, s=n + 1, m=m, N=N, host=None, rho_reg=args.rho_reg)
     return launch, info
 
 
@@ -486,7 +489,17 @@ def main(argv=None):
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the side timing of the other layout (profiling passes)")
     ap.add_argument("--no-anchor", action="store_true",
-                    help="N=1 lft: skip the config-4-shard anchor (32,768 problems)")
+                    help="N=1 lft: skip the config-4 anchors (the 32,768-problem shard and the "
+                         "262,144-problem global batch on one GPU)")
+    ap.add_argument("--rho-reg", type=float, default=1e-12,
+                    help="select_gains: the terminal/stage regulariser of the augmented "
+                         "builders (the reference's default 1e-12, augmented.py:14, 64)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak (default): --batch problems per GPU; strong: a fixed global "
+                         "batch (--global-batch) sharded over the N GPUs")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="--scaling strong: problems over all GPUs (default: 8 x the "
+                         "workload's per-GPU size; lft: config 4's 262,144)")
     args = ap.parse_args(argv)
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
@@ -555,15 +568,27 @@ def main(argv=None):
             return _Ev()
         return torch.cuda.Event(enable_timing=True)
 
-    Bn = args.batch
-    lo, hi = hd.shard_bounds(Bn * world, rank, world)
+    strong = args.scaling == "strong"
+    if strong:  # config 4: a fixed global batch over N GPUs
+        if args.global_batch is not None:
+            total_b = args.global_batch
+        elif dry:  # the rehearsal's stand-in problems are slow: --batch per GPU
+            total_b = args.batch * world
+        else:  # lft: 8 x 32,768 = 262,144 (BASELINE config 4)
+            total_b = 8 * (32768 if wl == "lft" else dflt[0])
+        if total_b < 1:
+            raise SystemExit("bench.py: --global-batch must be >= 1")
+    else:
+        total_b = args.batch * world
+    lo, hi = hd.shard_bounds(total_b, rank, world)
+    Bn = hi - lo  # this rank's problems (weak: args.batch on every rank)
     launch, info = (_dry_workload if dry else WORKLOADS[wl])(args, world, lo, hi, dev)
     s, m, N = info["s"], info["m"], info["N"]
 
     def step():
         r = launch()
         if world > 1:
-            hd.gather_selection(r.t_star, r.j_star, Bn * world)
+            hd.gather_selection(r.t_star, r.j_star, total_b)
         return r
 
     gathered = None
@@ -595,7 +620,7 @@ def main(argv=None):
         r = launch()
         ev[i][1].record()
         if world > 1:
-            gathered = hd.gather_selection(r.t_star, r.j_star, Bn * world)
+            gathered = hd.gather_selection(r.t_star, r.j_star, total_b)
     sync()
     if world > 1:
         dist.barrier()
@@ -626,8 +651,9 @@ def main(argv=None):
                      j_star=gathered[1].cpu().numpy())
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "steps": K,
-                              "ms_per_step": elapsed / K * 1e3,
-                              "config": {"batch_per_gpu": Bn, "global_batch": Bn * world,
+                              "ms_per_step": elapsed / K * 1e3, "scaling": args.scaling,
+                              "config": {"batch_per_gpu": Bn, "global_batch": total_b,
+                                         "scaling": args.scaling,
                                          "parallelism": f"dp{world}"},
                               "status_ok": status_ok}), flush=True)
         if world > 1:
@@ -636,25 +662,39 @@ def main(argv=None):
 
     # the config-4-shard anchor at N=1: the per-GPU batch of the N>1 lines (32,768),
     # so a 1->N curve can compare equal per-GPU work (a side figure, not `value`)
-    anchor = None
+    # and the config-4 global batch (262,144) on one GPU: the N = 1 point of the
+    # strong-scaling curve (`--scaling strong --gpus N` shards that same batch)
+    anchor = anchor_g = None
     if (rank == 0 and world == 1 and wl == "lft" and Bn != 32768 and not args.no_anchor
-            and args.batch_given is None):
-        launch_a, _ = WORKLOADS[wl](args_with_batch(args, 32768), 1, 0, 32768, dev)
-        for _ in range(3):
-            launch_a()
-        sync()
+            and args.batch_given is None and not strong):
+        def time_batch(nb, ka):
+            launch_a, _ = WORKLOADS[wl](args_with_batch(args, nb), 1, 0, nb, dev)
+            for _ in range(2):
+                launch_a()
+            sync()
+            ta = time.perf_counter()
+            for _ in range(ka):
+                ra = launch_a()
+            sync()
+            ms_a = (time.perf_counter() - ta) / ka * 1e3
+            ok_a = int(ra.status.abs().sum().item()) == 0
+            del launch_a, ra
+            torch.cuda.empty_cache()
+            return ms_a, ok_a
+
         ka = min(max(3, K // 4), 50)
-        ta = time.perf_counter()
-        for _ in range(ka):
-            launch_a()
-        sync()
-        ms_a = (time.perf_counter() - ta) / ka * 1e3
+        ms_a, ok_a = time_batch(32768, ka)
         anchor = {"workload": "config 4 shard: LFT sweep + fused argmin (32,768 problems on "
-                  "one GPU, the per-GPU batch of the N>1 lines)", "batch_per_gpu": 32768,
-                  "steps": ka, "ms_per_step": ms_a, "value": 32768 / ms_a * 1e3,
-                  "unit": "sweeps/s"}
-        del launch_a
-        torch.cuda.empty_cache()
+                  "one GPU, the per-GPU batch of the N>1 weak-scaling lines)",
+                  "batch_per_gpu": 32768, "steps": ka, "ms_per_step": ms_a,
+                  "value": 32768 / ms_a * 1e3, "unit": "sweeps/s", "status_ok": ok_a}
+        kg = min(ka, 10)
+        ms_g, ok_g = time_batch(262144, kg)
+        anchor_g = {"workload": "config 4 global batch: LFT sweep + fused argmin (262,144 "
+                    "problems on one GPU, the N = 1 point of --scaling strong)",
+                    "global_batch": 262144, "steps": kg, "ms_per_step": ms_g,
+                    "value": 262144 / ms_g * 1e3, "unit": "sweeps/s", "scaling": "strong",
+                    "status_ok": ok_g}
 
     # PCIe-inclusive side figure (never `value`): the step's inputs start in pinned
     # host memory and are copied H2D inside the timed region
@@ -691,7 +731,7 @@ def main(argv=None):
         alt_ms = sum(a_.elapsed_time(b_) for a_, b_ in ea) / len(ea)
 
     if rank == 0:
-        total = Bn * world * K
+        total = total_b * K
         value = total / elapsed
         per_launch = hi - lo
         if info["bound"] == "hbm":
@@ -742,7 +782,9 @@ def main(argv=None):
             roof["batch_major_kernel_ms"] = alt_ms
             roof["batch_major_frac"] = (info["bytes"] * per_launch / (alt_ms * 1e-3) / 1e9
                                         / PEAK_HBM_GBS)
-        names = {"lft": ("config 2: LFT sweep + fused argmin" if world == 1 and Bn != 32768
+        names = {"lft": ("config 4: LFT sweep + fused argmin, a fixed global batch sharded "
+                         "over the GPUs" if strong else
+                         "config 2: LFT sweep + fused argmin" if world == 1 and Bn != 32768
                          else "config 4 shard: LFT sweep + fused argmin"),
                  "config3": "config 3: LFT sweep + fused argmin (small-s kernel)",
                  "config5": "config 5: mixed Segway/Cartpole/Quadrotor (i mod 3), "
@@ -761,19 +803,22 @@ def main(argv=None):
             "prewarm_launches": prewarm,
             "ms_per_step": elapsed / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (device RNG, well-conditioned SPD blocks; SURVEY.md 8(d))",
             "config": {"workload": f"{names[wl]}, s={s} m={m} N={N}",
-                       "batch_per_gpu": Bn, "global_batch": Bn * world, "s": s, "m": m,
+                       "batch_per_gpu": Bn, "global_batch": total_b,
+                       "scaling": args.scaling, "s": s, "m": m,
                        "N": N, "t_min": info["t_min"], "t_max": info["t_max"],
                        "layout": info.get("layout", "batch-major"),
+                       **({"rho_reg": info["rho_reg"]} if "rho_reg" in info else {}),
                        "parallelism": f"dp{world}"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d,
             "config4_shard_anchor": anchor,
+            "config4_global_1gpu": anchor_g,
             "status_ok": status_ok,
         }
         print(json.dumps(line), flush=True)

@@ -54,8 +54,9 @@ const char* hop_last_error(void);
 /*
  * Test / diagnostic controls.  Not part of any reference interface and never
  * needed by a caller: every entry point runs its default kernels with all flags
- * 0.  Process-wide, read by the dispatchers at launch time (no environment
- * variables are consulted); set from one host thread between launches.
+ * 0.  Per host thread: the dispatchers read the calling thread's setting at
+ * launch time (no environment variables are consulted), so two threads may
+ * launch with different options at once.
  *   HOP_OPT_FORCE_GENERIC   every sweep / Riccati pass on the generic kernels
  *                           (lft_sweep.hip, riccati.hip): the fast paths'
  *                           cross-check
@@ -65,6 +66,10 @@ const char* hop_last_error(void);
  *                           kernel (no conditioned prefix)
  *   HOP_OPT_TRAJ_UNFUSED    trajectory form through hop_augment + the sweep
  *   HOP_OPT_STAMPS          section-stamped instantiations (developer builds)
+ *   HOP_OPT_NO_RERUN        the conditioned-prefix kernels run without their
+ *                           rerun launch: a problem they hand over keeps
+ *                           HOP_ST_HANDOVER in status and its J is not valid
+ *                           (counts hand-overs; tests and tools only)
  * `variant` selects an A/B schedule; only developer builds (HOP_DEV_BUILD=1 at
  * build time, hop_build_flags() & 1) compile them -- product builds return
  * HOP_E_ARG for variant != 0 or HOP_OPT_STAMPS.
@@ -74,8 +79,12 @@ const char* hop_last_error(void);
 #define HOP_OPT_REFERENCE_ASSOC 4u
 #define HOP_OPT_TRAJ_UNFUSED 8u
 #define HOP_OPT_STAMPS 16u
+#define HOP_OPT_NO_RERUN 32u
+#define HOP_ST_HANDOVER 16 /* status bit, set only under HOP_OPT_NO_RERUN */
 int hop_set_options(uint32_t flags, int32_t variant);
+int hop_get_options(uint32_t* flags, int32_t* variant); /* the calling thread's; nullable */
 int hop_build_flags(void); /* bit 0: developer build (A/B schedules and stamps compiled) */
+int hop_cu_fallbacks(void); /* CU-count queries that failed and assumed 256 (layout only) */
 
 /*
  * hop_lft_sweep_f64 / _f32
@@ -332,14 +341,18 @@ int hop_bruteforce_jcurve_f32(const float* A, const float* Bm, const float* X, c
  *   backward_pass_truncated (ilqr_propagator.py:375-400), mode 1 its
  *   value_expansions_and_gains_prefix (ilqr_propagator.py:237-287), the J-curve
  *   entry its bruteforce_all_Jt_backward_expansion (ilqr_propagator.py:426-454).
- *   Every solve is the legacy chol_solve (ilqr_propagator.py:33-43): 4 jitters,
- *   then np.linalg.lstsq of sym(Quu_reg) -- the minimum-norm pinv solve, marked
- *   HOP_ST_LU -- instead of a failure; Quu_reg = _sym(Quu) + lm I (no floor, no
- *   lambda ladder); no finiteness checks (NaN propagates; a non-finite Quu_reg
- *   that reaches lstsq fails the row, as numpy's lstsq raises).  The terminal
- *   weight is Qf = alpha I (the legacy passes take a scalar alpha).  Arguments as
- *   hop_riccati_f64 / hop_bruteforce_jcurve_f64 without the extra stage cost and
- *   reg_max_tries; m <= 11 (HOP_E_SIZE otherwise).
+ *   Mode 1 and the J curve solve with the legacy chol_solve
+ *   (ilqr_propagator.py:33-43): 4 jitters, then np.linalg.lstsq of sym(Quu_reg)
+ *   -- the minimum-norm pinv solve, marked HOP_ST_LU -- instead of a failure.
+ *   Mode 0 is the legacy backward_pass_truncated: a Cholesky gate on Quu_reg
+ *   without jitter fails the row (HOP_ST_FAIL, the reference's ok=False) before
+ *   any solve, so its solves succeed at the first 1e-9 jitter and never reach
+ *   lstsq.  Quu_reg = _sym(Quu) + lm I (no floor, no lambda ladder); no
+ *   finiteness checks (NaN propagates; a non-finite Quu_reg that reaches lstsq
+ *   fails the row, as numpy's lstsq raises).  The terminal weight is Qf = alpha I
+ *   (the legacy passes take a scalar alpha).  Arguments as hop_riccati_f64 /
+ *   hop_bruteforce_jcurve_f64 without the extra stage cost and reg_max_tries;
+ *   mode 1 and the J curve need m <= 11 (HOP_E_SIZE otherwise).
  */
 int hop_riccati_legacy_f64(const double* A, const double* Bm, const double* X, const double* U,
                            const double* xg, int64_t xg_batch_stride, const double* u_ref,

@@ -473,6 +473,70 @@ def chol_solve_legacy(A, B, jitter=JITTER0, max_tries=4):
     return np.linalg.lstsq(A, B, rcond=None)[0], ST_LU
 
 
+def riccati_truncated_legacy(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_star,
+                             lm_lambda=1e-3, wrap_idx=None):
+    """ilqr_propagator.py:375-400 (the legacy backward_pass_truncated): Qf = alpha I,
+    a Cholesky gate on Quu_reg without jitter ((None, None, False) when it fails),
+    then the legacy chol_solve; no finiteness checks."""
+    T = int(T_star)
+    n, m = X.shape[1], U.shape[1]
+    ks, Ks = [None] * T, [None] * T
+    eT = wrap_angles(np.asarray(X[T] - xg, dtype=np.float64), wrap_idx).reshape(-1)
+    Vx, Vxx = float(alpha) * eT, float(alpha) * np.eye(n)
+    for k in range(T - 1, -1, -1):
+        e = wrap_angles(np.asarray(X[k] - xg, dtype=np.float64), wrap_idx).reshape(-1)
+        du = np.atleast_1d(U[k] - u_ref).reshape(-1)
+        A, B = A_list[k], B_list[k]
+        Qx, Qu = Q @ e + A.T @ Vx, R @ du + B.T @ Vx
+        Qxx, Quu, Qux = Q + A.T @ Vxx @ A, R + B.T @ Vxx @ B, B.T @ Vxx @ A
+        Quu_reg = sym(Quu) + float(lm_lambda) * np.eye(m)
+        try:
+            np.linalg.cholesky(Quu_reg)
+        except np.linalg.LinAlgError:
+            return None, None, False
+        kap = -chol_solve_legacy(Quu_reg, Qu)[0]
+        Kk = -chol_solve_legacy(Quu_reg, Qux)[0]
+        ks[k], Ks[k] = kap, Kk
+        Vx = Qx + Kk.T @ Qu + Qux.T @ kap + Kk.T @ Quu @ kap
+        Vxx = sym(Qxx + Kk.T @ Qux + Qux.T @ Kk + Kk.T @ Quu @ Kk)
+    return ks, Ks, True
+
+
+def riccati_expand_legacy(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
+                          lm_lambda=1e-6, w_stage=0.0, wrap_idx=None):
+    """ilqr_propagator.py:237-287 (the legacy value_expansions_and_gains_prefix):
+    Qf = alpha I, Quu_reg = _sym(Quu) + lm I, the legacy chol_solve (4 jitters,
+    then lstsq; never raises for finite data).  Returns (Vxx, Vx, V0, K, k, status)
+    with index i = t + S_right; status has ST_LU where lstsq ran."""
+    n, m = X.shape[1], U.shape[1]
+    L = int(T_bar) + int(S_right)
+    Vxx = [np.zeros((n, n)) for _ in range(L + 1)]
+    Vx = [np.zeros(n) for _ in range(L + 1)]
+    V0 = [0.0] * (L + 1)
+    K, kk, st = [None] * L, [None] * L, 0
+    eT = wrap_angles(np.asarray(X[L] - xg, dtype=np.float64), wrap_idx).reshape(-1)
+    Vxx[L], Vx[L], V0[L] = float(alpha) * np.eye(n), float(alpha) * eT, \
+        0.5 * float(alpha) * float(eT @ eT)
+    for i in range(L - 1, -1, -1):
+        e = wrap_angles(np.asarray(X[i] - xg, dtype=np.float64), wrap_idx).reshape(-1)
+        du = np.atleast_1d(U[i] - u_ref).reshape(-1)
+        l0 = 0.5 * float(e @ (Q @ e)) + 0.5 * float(du @ (R @ du)) + float(w_stage)
+        A, B = A_list[i], B_list[i]
+        Qx, Qu = Q @ e + A.T @ Vx[i + 1], R @ du + B.T @ Vx[i + 1]
+        Qxx = Q + A.T @ Vxx[i + 1] @ A
+        Quu = R + B.T @ Vxx[i + 1] @ B
+        Qux = B.T @ Vxx[i + 1] @ A
+        Quu_reg = sym(Quu) + float(lm_lambda) * np.eye(m)
+        a, s1 = chol_solve_legacy(Quu_reg, Qu)
+        b, s2 = chol_solve_legacy(Quu_reg, Qux)
+        st |= s1 | s2
+        kk[i], K[i] = -a, -b
+        Vxx[i] = sym(Qxx - Qux.T @ b)
+        Vx[i] = Qx - Qux.T @ a
+        V0[i] = l0 + V0[i + 1] - 0.5 * float(Qu.T @ a)
+    return Vxx, Vx, V0, K, kk, st
+
+
 def bruteforce_J(A_list, B_list, X, U, xg, u_ref, Q, R, alpha, w, T_max,
                  lm_lambda=1e-6, wrap_idx=None, extra=None, legacy=False, want_status=False):
     """solver.py:293-358: J[T-1] = V0[0] of a fresh Riccati sweep of length T.

@@ -4,7 +4,7 @@ Run in the build container only (the reference tree is not on the GPU box):
 
     cd /tmp && PYTHONDONTWRITEBYTECODE=1 python /root/repo/tests/golden/make_golden.py [FLAG]
 
-FLAG selects one group: --r3, --r2, --legacy, --traj, --lin, --ilqr (propagator outer loop),
+FLAG selects one group: --r4, --r3, --r2, --legacy, --traj, --lin, --ilqr (propagator outer loop),
 --ilqr-bf (ilqr_timeopt(method="bruteforce"), ilqr_bf_*.npz), --summary (the
 plots/summary.csv comparison runs, summary_*.npz); none runs the base groups.
 
@@ -800,6 +800,62 @@ def lu_pivot_cases(seed=9900):
     print("lu_pivot_cases:", sorted(d))
 
 
+def legacy_riccati_cases(seed=9950):
+    """Round 4: the legacy twin's Riccati passes with its chol_solve
+    (ilqr_propagator.py:33-43): backward_pass_truncated (ilqr_propagator.py:375-400,
+    Cholesky gate without jitter, then chol_solve) and
+    value_expansions_and_gains_prefix (ilqr_propagator.py:237-287, chol_solve's
+    4 jitters then np.linalg.lstsq).  Per shape, problem 0 is clean and problem 1
+    has R[0, 0] = -1: Quu_reg is indefinite, mode 0 returns (None, None, False)
+    and mode 1 takes the least-squares fallback at every step."""
+    import ilqr_propagator as leg
+    d = {}
+    for n, m, N in ((4, 2, 10), (12, 4, 10)):
+        tag = f"n{n}_m{m}"
+        T_star, T_bar, S_right, lm = 8, 7, 2, 1e-6
+        for i in range(2):
+            A, B, X, U, xg, u_ref, Q, R, alpha = orc.synth_riccati_problem(seed + i, n, m, N)
+            if i == 1:
+                R = R.copy()
+                R[0, 0] = -1.0
+            k0, K0, ok = leg.backward_pass_truncated(list(A), list(B), X, U, xg, u_ref, Q, R,
+                                                     alpha, T_star, lm_lambda=lm)
+            d[f"{tag}_p{i}_R"] = R
+            d[f"{tag}_p{i}_m0_ok"] = bool(ok)
+            if ok:
+                d[f"{tag}_p{i}_m0_K"] = np.array(K0)
+                d[f"{tag}_p{i}_m0_k"] = np.array(k0).reshape(T_star, m)
+            calls = []
+            real = leg.np.linalg.lstsq
+
+            def spy(*a, **k):
+                calls.append(1)
+                return real(*a, **k)
+
+            leg.np.linalg.lstsq = spy
+            try:
+                Vxx, Vx, V0, K, k = leg.value_expansions_and_gains_prefix(
+                    list(A), list(B), X, U, xg, u_ref, Q, R, alpha, T_bar, S_right,
+                    lm_lambda=lm, w_stage=0.5)
+            finally:
+                leg.np.linalg.lstsq = real
+            d[f"{tag}_p{i}_m1_Vxx"] = np.array(Vxx)
+            d[f"{tag}_p{i}_m1_Vx"] = np.array(Vx)
+            d[f"{tag}_p{i}_m1_V0"] = np.array(V0)
+            d[f"{tag}_p{i}_m1_K"] = np.array(K)
+            d[f"{tag}_p{i}_m1_k"] = np.array(k).reshape(len(k), m)
+            d[f"{tag}_p{i}_m1_lstsq_calls"] = len(calls)
+            print(f"legacy_riccati {tag} p{i}: mode0 ok={ok} mode1 lstsq calls {len(calls)}")
+        d[f"{tag}_seed"] = seed
+        d[f"{tag}_params"] = np.array([T_star, T_bar, S_right, lm])
+    np.savez_compressed(os.path.join(HERE, "legacy_riccati_cases.npz"), **d)
+
+
+def main_r4():
+    np.seterr(all="ignore")
+    legacy_riccati_cases()
+
+
 def main_r3():
     np.seterr(all="ignore")
     bruteforce_edge_cases()
@@ -821,7 +877,9 @@ def main_r2():
 
 
 if __name__ == "__main__":
-    if "--r3" in sys.argv:  # round-3 fixtures only
+    if "--r4" in sys.argv:  # round-4 fixtures only
+        main_r4()
+    elif "--r3" in sys.argv:  # round-3 fixtures only
         main_r3()
     elif "--r2" in sys.argv:  # round-2 fixtures only
         main_r2()

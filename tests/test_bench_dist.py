@@ -78,3 +78,25 @@ def test_bench_more_gpus_than_devices_fails():
     assert p.returncode == 2, p.stdout + p.stderr
     assert "HIP device" in p.stderr
     assert '"n_gpus"' not in p.stdout
+
+
+@pytest.mark.parametrize("gpus,total", [(2, 7), (3, 5)])
+def test_bench_strong_scaling_dry_run_shards_the_global_batch(tmp_path, gpus, total):
+    """--scaling strong: the global batch stays fixed and is split into contiguous
+    shards (sizes differ by at most one); the line names the mode and every
+    problem's (T*, J*) comes back in order"""
+    out = tmp_path / "s.npz"
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--dry-run",
+           "--scaling", "strong", "--global-batch", str(total), "--steps", "2", "--warmup", "1",
+           "--prewarm-s", "0", "--no-cpu-baseline", "--dry-out", str(out)]
+    p = subprocess.run(cmd, env=_env(), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = _json_line(p.stdout)
+    assert line["n_gpus"] == gpus and line["scaling"] == "strong"
+    assert line["config"]["global_batch"] == total and line["config"]["scaling"] == "strong"
+    assert line["config"]["batch_per_gpu"] == -(-total // gpus)  # rank 0's shard
+    got = np.load(out)
+    import bench_dry_standin as sd
+    ref = [sd.select_for(i) for i in range(total)]
+    assert got["t_star"].tolist() == [r[0] for r in ref]
+    assert np.array_equal(got["j_star"], np.array([r[1] for r in ref]))

@@ -137,3 +137,32 @@ def test_gloo_sharded_outer_loop(tmp_path, world, total, method):
     J_last = np.array([ref["J_hist"][b, nh[b] - 1].item() for b in range(total)])
     assert np.array_equal(got["J_star"], J_last)
     assert not got["crashed"].any()
+
+
+def test_sharded_inputs_broadcast_leading_one(monkeypatch):
+    """ilqr_timeopt_sharded's per-problem slicing: a batch-form input with a leading
+    dimension of 1 (one shared U_init [1, N', m], which ilqr_timeopt_batch
+    broadcasts) passes through whole; [B, ...] is sliced; any other leading size
+    is refused"""
+    from time_opt_ilqr_amd import distributed as hd
+    from time_opt_ilqr_amd import solver
+    seen = {}
+
+    def standin(system, x0, xg, u_ref, Q, R, Qf, w, N, T_min, T_max, *, U_init=None, **kw):
+        seen["U_init"], seen["xg"] = U_init, xg
+        return _oracle_batch(0, x0, np.zeros(2) + 2.0, u_ref, Q, R, Qf, w, N, T_min, T_max,
+                             max_iter=1)
+
+    monkeypatch.setattr(solver, "ilqr_timeopt_batch", standin)
+    F, x0, xg, u_ref, Q, R, Qf, w = _case_di()
+    X0 = np.stack([x0] * 3)
+    U1 = np.zeros((1, 30, 1))
+    hd.ilqr_timeopt_sharded(0, X0, xg, u_ref, Q, R, Qf, w, 30, 8, 30, U_init=U1,
+                            device=torch.device("cpu"))
+    assert seen["U_init"].shape == (1, 30, 1)
+    hd.ilqr_timeopt_sharded(0, X0, np.stack([xg] * 3), u_ref, Q, R, Qf, w, 30, 8, 30,
+                            U_init=np.zeros((3, 30, 1)), device=torch.device("cpu"))
+    assert seen["U_init"].shape == (3, 30, 1) and seen["xg"].shape == (3, 2)
+    with pytest.raises(ValueError):
+        hd.ilqr_timeopt_sharded(0, X0, xg, u_ref, Q, R, Qf, w, 30, 8, 30,
+                                U_init=np.zeros((2, 30, 1)), device=torch.device("cpu"))

@@ -779,3 +779,47 @@ def test_legacy_bruteforce_lstsq_vs_reference(dev, golden_dir, n, m):
                                               _t(alpha * np.eye(n), dev), N, lm_lambda=1e-6,
                                               w_stage=0.5)
             assert (_np(sm)[0] & _lib.ST_FAIL).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,m", [(4, 2), (12, 4)])
+def test_legacy_riccati_passes_vs_reference(dev, golden_dir, n, m):
+    """The legacy twin's Riccati passes (hop_riccati_legacy_f64) against the
+    reference's own (legacy_riccati_cases.npz): mode 0 = backward_pass_truncated
+    (ilqr_propagator.py:375-400: no-jitter Cholesky gate, then chol_solve), mode 1 =
+    value_expansions_and_gains_prefix (ilqr_propagator.py:237-287: chol_solve's 4
+    jitters, then lstsq).  Problem 1's R[0, 0] = -1 makes Quu_reg indefinite:
+    mode 0 fails the row (ok=False), mode 1 takes the least-squares fallback
+    (ST_LU) at the steps where the reference calls lstsq.  n=4/m=2 and n=12/m=4
+    both run the generic kernel (the legacy passes have no exact-size form)."""
+    from time_opt_ilqr_amd import _lib, engine
+    from oracle import hop_oracle as orc
+    d = np.load(os.path.join(golden_dir, "legacy_riccati_cases.npz"))
+    tag, N = f"n{n}_m{m}", 10
+    T_star, T_bar, S_right, lm = d[f"{tag}_params"]
+    T_star, T_bar, S_right = int(T_star), int(T_bar), int(S_right)
+    L = T_bar + S_right
+    for i in range(2):
+        A, B, X, U, xg, ur, Q, R, alpha = orc.synth_riccati_problem(int(d[f"{tag}_seed"]) + i, n,
+                                                                   m, N)
+        R = d[f"{tag}_p{i}_R"]
+        args = (_t(A[None], dev), _t(B[None], dev), _t(X[None], dev), _t(U[None], dev),
+                _t(xg, dev), _t(ur, dev), _t(Q, dev), _t(R, dev), _t(alpha * np.eye(n), dev))
+        r0 = engine.riccati(*args, T_star, float(lm), mode=0, legacy=True)
+        st0 = int(_np(r0.status)[0])
+        if bool(d[f"{tag}_p{i}_m0_ok"]):
+            assert st0 & _lib.ST_FAIL == 0 and st0 & _lib.ST_LU == 0, st0
+            assert _rel(_np(r0.K)[0, :T_star], d[f"{tag}_p{i}_m0_K"]) <= 1e-10
+            assert _rel(_np(r0.k)[0, :T_star], d[f"{tag}_p{i}_m0_k"]) <= 1e-10
+        else:  # (None, None, False): the gate fails the row, no lstsq
+            assert st0 & _lib.ST_FAIL and not st0 & _lib.ST_LU, st0
+        r1 = engine.riccati(*args, L, float(lm), mode=1, w_stage=0.5, legacy=True)
+        st1 = int(_np(r1.status)[0])
+        assert st1 & _lib.ST_FAIL == 0, st1
+        assert bool(st1 & _lib.ST_LU) == (int(d[f"{tag}_p{i}_m1_lstsq_calls"]) > 0), st1
+        tol = 1e-10 if i == 0 else 1e-8  # the pinv solve: Jacobi vs LAPACK's SVD
+        assert _rel(_np(r1.K)[0, :L], d[f"{tag}_p{i}_m1_K"]) <= tol
+        assert _rel(_np(r1.k)[0, :L], d[f"{tag}_p{i}_m1_k"]) <= tol
+        assert _rel(_np(r1.Vxx)[0, :L + 1], d[f"{tag}_p{i}_m1_Vxx"]) <= tol
+        assert _rel(_np(r1.Vx)[0, :L + 1], d[f"{tag}_p{i}_m1_Vx"]) <= tol
+        assert _rel(_np(r1.V0)[0, :L + 1], d[f"{tag}_p{i}_m1_V0"]) <= tol

@@ -30,7 +30,7 @@ def _header_functions():
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 34
+    assert len(names) == 36
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:
@@ -69,12 +69,42 @@ def test_options_are_explicit_and_product_build_has_no_ab_schedules(lib):
     assert lib.hop_set_options(_lib.OPT_STAMPS, 0) == -1
     assert lib.hop_set_options(1 << 9, 0) == -1
     with _lib.options(force_generic=True):
-        with _lib.options(traj_unfused=True):
-            assert _lib._opts == (_lib.OPT_FORCE_GENERIC | _lib.OPT_TRAJ_UNFUSED, 0)
-        assert _lib._opts == (_lib.OPT_FORCE_GENERIC, 0)
-    assert _lib._opts == (0, 0)
+        with _lib.options(traj_unfused=True, no_rerun=True):
+            assert _lib.get_options() == (_lib.OPT_FORCE_GENERIC | _lib.OPT_TRAJ_UNFUSED |
+                                          _lib.OPT_NO_RERUN, 0)
+        assert _lib.get_options() == (_lib.OPT_FORCE_GENERIC, 0)
+    assert _lib.get_options() == (0, 0)
     out = os.popen(f"nm -D {_lib.LIB_PATH}").read()
     assert not re.search(r"\bU getenv\b", out)
+
+
+def test_options_are_per_host_thread(lib):
+    """SURVEY.md 8(b) re-entrancy: hop_set_options from one host thread does not
+    change the options another thread's launches read (thread-local state)."""
+    import threading
+    from time_opt_ilqr_amd import _lib
+    seen, go, done = {}, threading.Barrier(2), threading.Barrier(2)
+
+    def worker(name, kw):
+        with _lib.options(**kw):
+            go.wait()          # both threads hold their own setting at once
+            seen[name] = _lib.get_options()
+            done.wait()
+        seen[name + "_after"] = _lib.get_options()
+
+    ts = [threading.Thread(target=worker, args=("a", dict(force_generic=True))),
+          threading.Thread(target=worker, args=("b", dict(reference_assoc=True, no_rerun=True)))]
+    with _lib.options(force_handover=True):  # the main thread's own setting
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert _lib.get_options() == (_lib.OPT_FORCE_HANDOVER, 0)
+    assert seen["a"] == (_lib.OPT_FORCE_GENERIC, 0)
+    assert seen["b"] == (_lib.OPT_REFERENCE_ASSOC | _lib.OPT_NO_RERUN, 0)
+    assert seen["a_after"] == seen["b_after"] == (0, 0)
+    assert _lib.get_options() == (0, 0)
+    assert lib.hop_cu_fallbacks() == 0  # no launch has asked for the CU count here
 
 
 def test_library_is_gfx950_code_object(lib):

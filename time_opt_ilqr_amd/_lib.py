@@ -61,7 +61,9 @@ SIGNATURES = {
     "hop_abi_version": (C.c_int, []),
     "hop_last_error": (C.c_char_p, []),
     "hop_set_options": (C.c_int, [_U32, _I32]),
+    "hop_get_options": (C.c_int, [_P, _P]),
     "hop_build_flags": (C.c_int, []),
+    "hop_cu_fallbacks": (C.c_int, []),
     "hop_lft_sweep_f64": (C.c_int, _LFT),
     "hop_lft_sweep_f32": (C.c_int, _LFT),
     "hop_lft_sweep_tile64_f64": (C.c_int, _LFT_T64),
@@ -141,6 +143,8 @@ OPT_FORCE_HANDOVER = 2
 OPT_REFERENCE_ASSOC = 4
 OPT_TRAJ_UNFUSED = 8
 OPT_STAMPS = 16
+OPT_NO_RERUN = 32
+ST_HANDOVER = 16  # status bit left by the conditioned kernels under OPT_NO_RERUN
 
 
 def dev_build() -> bool:
@@ -150,30 +154,35 @@ def dev_build() -> bool:
 
 @contextlib.contextmanager
 def options(*, force_generic=None, force_handover=None, reference_assoc=None,
-            traj_unfused=None, stamps=None, variant=None):
+            traj_unfused=None, stamps=None, no_rerun=None, variant=None):
     """Set hop_set_options for the duration of a `with` block (tests, tools).
     Arguments left at None keep the enclosing block's setting; the previous
-    controls are restored afterwards.  The library reads them at launch."""
-    global _opts
-    prev = _opts
+    controls are restored afterwards.  The library keeps them per host thread
+    and reads them at launch, so the block affects only this thread's calls."""
+    lib = load()
+    f0, v0 = C.c_uint32(), C.c_int32()
+    check(lib.hop_get_options(C.byref(f0), C.byref(v0)))
+    prev = (f0.value, v0.value)
     flags, var = prev
     for on, bit in ((force_generic, OPT_FORCE_GENERIC), (force_handover, OPT_FORCE_HANDOVER),
                     (reference_assoc, OPT_REFERENCE_ASSOC), (traj_unfused, OPT_TRAJ_UNFUSED),
-                    (stamps, OPT_STAMPS)):
+                    (stamps, OPT_STAMPS), (no_rerun, OPT_NO_RERUN)):
         if on is not None:
             flags = (flags | bit) if on else (flags & ~bit)
     if variant is not None:
         var = int(variant)
-    check(load().hop_set_options(flags, var))
-    _opts = (flags, var)
+    check(lib.hop_set_options(flags, var))
     try:
         yield
     finally:
-        load().hop_set_options(*prev)
-        _opts = prev
+        lib.hop_set_options(*prev)
 
 
-_opts = (0, 0)
+def get_options() -> tuple:
+    """(flags, variant) of the calling host thread."""
+    f, v = C.c_uint32(), C.c_int32()
+    check(load().hop_get_options(C.byref(f), C.byref(v)))
+    return f.value, v.value
 
 
 def check(rc: int):

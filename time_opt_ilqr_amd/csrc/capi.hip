@@ -1,6 +1,7 @@
 // extern "C" boundary of libhop_amd.so (include/hop.h): argument validation,
 // kernel dispatch, the horizon argmin kernel.
 #include <algorithm>
+#include <atomic>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -11,8 +12,11 @@
 #include "dynamics.hpp"
 
 namespace hop {
-unsigned g_opt_flags = 0u;
-int g_opt_variant = 0;
+// per host thread (re-entrant across host threads): a thread's
+// hop_set_options changes only the launches that thread issues
+thread_local unsigned g_opt_flags = 0u;
+thread_local int g_opt_variant = 0;
+std::atomic<int> g_cu_fallbacks{0};
 }  // namespace hop
 
 namespace {
@@ -193,7 +197,10 @@ int riccati_entry(const T* A, const T* Bm, const T* X, const T* U, const T* xg, 
   a.reg_max_tries = reg_max_tries; a.max_tries = 8; a.wrap_mask = wrap_mask; a.w_stage = w_stage;
   a.K = K; a.k = k; a.Vxx = Vxx; a.Vx = Vx; a.V0 = V0; a.status = status;
   a.legacy = legacy;
-  if (legacy && m > 11) return fail(HOP_E_SIZE, "legacy lstsq fallback: m must be <= 11");
+  // mode 0 never reaches the lstsq fallback (the no-jitter Cholesky gate fails the
+  // row first, ilqr_propagator.py:387-390), so only mode 1 carries the m limit
+  if (legacy && mode == 1 && m > 11)
+    return fail(HOP_E_SIZE, "legacy lstsq fallback: m must be <= 11");
   return hip_status(hop::dispatch_riccati<T>(a, (hipStream_t)stream));
 }
 
@@ -343,7 +350,7 @@ extern "C" {
 
 int hop_set_options(uint32_t flags, int32_t variant) {
   if (flags & ~(HOP_OPT_FORCE_GENERIC | HOP_OPT_FORCE_HANDOVER | HOP_OPT_REFERENCE_ASSOC |
-                HOP_OPT_TRAJ_UNFUSED | HOP_OPT_STAMPS))
+                HOP_OPT_TRAJ_UNFUSED | HOP_OPT_STAMPS | HOP_OPT_NO_RERUN))
     return fail(HOP_E_ARG, "unknown option flag");
   if (!hop::kDevBuild && (variant != 0 || (flags & HOP_OPT_STAMPS)))
     return fail(HOP_E_ARG, "A/B schedules and stamps exist only in developer builds "
@@ -353,7 +360,15 @@ int hop_set_options(uint32_t flags, int32_t variant) {
   return HOP_OK;
 }
 
+int hop_get_options(uint32_t* flags, int32_t* variant) {
+  if (flags) *flags = hop::g_opt_flags;
+  if (variant) *variant = hop::g_opt_variant;
+  return HOP_OK;
+}
+
 int hop_build_flags(void) { return hop::kDevBuild ? 1 : 0; }
+
+int hop_cu_fallbacks(void) { return hop::g_cu_fallbacks.load(std::memory_order_relaxed); }
 
 int hop_abi_version(void) { return HOP_ABI_VERSION; }
 const char* hop_last_error(void) { return g_err; }

@@ -611,7 +611,7 @@ hipError_t launch_all(int which, const void* args, hipStream_t st) {
         // (beyond that the SIMDs are full and the duplicated half of the work costs)
         const long long lanes2 = 2 * a.batch * a.n_alpha + a.batch;
         if (shared && c.wrap_mask == (unsigned)WD && !one_lane &&
-            (lanes2 + 63) / 64 <= 4 * cu_count()) {
+            (lanes2 + 63) / 64 <= 4 * cu_count(st)) {
           lanes = lanes2;
           hipLaunchKernelGGL((linesearch_kernel<SYS, true, WD, true>),
                              dim3((unsigned)((lanes + TPB - 1) / TPB)), dim3(TPB), 0, st, a);

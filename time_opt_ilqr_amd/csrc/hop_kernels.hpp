@@ -3,27 +3,41 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/hop.h"
 
 namespace hop {
-// test / diagnostic controls (hop_set_options, include/hop.h); 0 = product defaults
-extern unsigned g_opt_flags;
-extern int g_opt_variant;
+// test / diagnostic controls (hop_set_options, include/hop.h); 0 = product defaults.
+// Per host thread: a launch sees the options of the thread that issues it.
+extern thread_local unsigned g_opt_flags;
+extern thread_local int g_opt_variant;
 inline bool opt(unsigned f) { return (g_opt_flags & f) != 0u; }
-// compute units of the current device, cached per device id: the launches that pick
-// a layout by waves per SIMD (4 SIMDs per CU) compare against 4 x this
-inline long long cu_count() {
-  static int cached[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cached[dev] == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    cached[dev] = cus;
+// queries that could not read the device's CU count (hop_cu_fallbacks)
+extern std::atomic<int> g_cu_fallbacks;
+// compute units of the device `stream` belongs to, cached per device id (atomics:
+// launches from several host threads may fill the cache at once); the launches
+// that pick a layout by waves per SIMD (4 SIMDs per CU) compare against 4 x this.
+// A failed query counts in hop_cu_fallbacks() and assumes MI355X's 256 CUs; that
+// changes only the layout choice (the results are bit-identical either way).
+inline long long cu_count(hipStream_t stream) {
+  static std::atomic<int> cached[64] = {};
+  int dev = -1;
+  if (hipStreamGetDevice(stream, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess)
+    dev = -1;
+  if (dev < 0 || dev >= 64) {
+    g_cu_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    return 256;
   }
-  return cached[dev];
+  int cus = cached[dev].load(std::memory_order_relaxed);
+  if (cus > 0) return cus;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0) {
+    g_cu_fallbacks.fetch_add(1, std::memory_order_relaxed);
+    return 256;  // not cached: the next launch asks again
+  }
+  cached[dev].store(cus, std::memory_order_relaxed);
+  return cus;
 }
 #ifdef HOP_DEV
 inline constexpr bool kDevBuild = true;

@@ -585,7 +585,7 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
     hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
-    if (cmode == 2) return hipGetLastError();
+    if (cmode == 2 || opt(HOP_OPT_NO_RERUN)) return hipGetLastError();
     LftArgs<T> r = a;
     r.cond = 1;
     hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
@@ -640,6 +640,7 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
     hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
+    if (opt(HOP_OPT_NO_RERUN)) return hipGetLastError();  // flags left in status (tests)
     LftArgs<T> r = a;
     r.cond = 1;
     hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);

@@ -767,21 +767,23 @@ __device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsign
 // PACK: dma_step20 with the images back to back.  The full pieces first, then the
 // last piece of Q, A, QT (LM lanes) and of B (LB lanes) under a narrowed EXEC, so no
 // lane past an image's data writes into the next image; EXEC restored at the end.
+// The narrowed masks are ANDed with the caller's EXEC, so a lane the caller turned
+// off stays off (the kernel calls this with full EXEC; the AND keeps it safe if not).
 template <int OQ, int OA, int OB, int OT, int LM, int LB>
 __device__ __forceinline__ void dma_step20p(const unsigned (&vm)[6], const unsigned (&vb)[2],
                                             __amdgpu_buffer_rsrc_t rQ, __amdgpu_buffer_rsrc_t rA,
                                             __amdgpu_buffer_rsrc_t rB, __amdgpu_buffer_rsrc_t rT,
                                             unsigned wlds, unsigned soM, unsigned soB) {
   static_assert(LM > 0 && LM <= 32 && LB > 32 && LB <= 64, "partial-piece masks");
-  unsigned keep;
-  unsigned long long ex;
+  unsigned keep, elo, ehi;
 #define HOP_P(R, V, OFF, SO)                                                  \
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
       ".p2align 3\n\t"
       "s_mov_b32 %[keep], m0\n\t"
-      "s_mov_b64 %[ex], exec\n\t"
+      "s_mov_b32 %[elo], exec_lo\n\t"
+      "s_mov_b32 %[ehi], exec_hi\n\t"
       HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
       HOP_P(rq, v3, %[q3], sm) HOP_P(rq, v4, %[q4], sm)
       HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
@@ -789,15 +791,16 @@ __device__ __forceinline__ void dma_step20p(const unsigned (&vm)[6], const unsig
       HOP_P(rb, u0, %[b0], sb)
       HOP_P(rt, v0, %[t0], sm) HOP_P(rt, v1, %[t1], sm) HOP_P(rt, v2, %[t2], sm)
       HOP_P(rt, v3, %[t3], sm) HOP_P(rt, v4, %[t4], sm)
-      "s_mov_b32 exec_lo, %[mlo]\n\t"
+      "s_and_b32 exec_lo, %[elo], %[mlo]\n\t"
       "s_mov_b32 exec_hi, 0\n\t"
       HOP_P(rq, v5, %[q5], sm) HOP_P(ra, v5, %[a5], sm) HOP_P(rt, v5, %[t5], sm)
-      "s_mov_b32 exec_lo, -1\n\t"
-      "s_mov_b32 exec_hi, %[bhi]\n\t"
+      "s_mov_b32 exec_lo, %[elo]\n\t"
+      "s_and_b32 exec_hi, %[ehi], %[bhi]\n\t"
       HOP_P(rb, u1, %[b1], sb)
-      "s_mov_b64 exec, %[ex]\n\t"
+      "s_mov_b32 exec_lo, %[elo]\n\t"
+      "s_mov_b32 exec_hi, %[ehi]\n\t"
       "s_mov_b32 m0, %[keep]"
-      : [keep] "=&s"(keep), [ex] "=&s"(ex)
+      : [keep] "=&s"(keep), [elo] "=&s"(elo), [ehi] "=&s"(ehi)
       : [w] "s"(wlds), [sm] "s"(soM), [sb] "s"(soB), [rq] "s"(rQ), [ra] "s"(rA), [rb] "s"(rB),
         [rt] "s"(rT), [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]),
         [v4] "v"(vm[4]), [v5] "v"(vm[5]), [u0] "v"(vb[0]), [u1] "v"(vb[1]),
@@ -2410,7 +2413,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     LftArgs<double> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
     hipError_t e = launch(kc, bytes, c);
-    if (e != hipSuccess || !rerun) return e;
+    if (e != hipSuccess || !rerun || opt(HOP_OPT_NO_RERUN)) return e;
     LftArgs<double> r = a;
     r.cond = 1;
     return launch(kr, bytes, r);
@@ -2502,12 +2505,12 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
 #else
   constexpr bool pack1 = false, pack2 = false;
 #endif
-  if (!pack1 && (pack2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count())) {
+  if (!pack1 && (pack2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count(stream))) {
     LftArgs<double> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
     hipError_t e = launch(v2::lft_cond_kernel<v2::SchedCondLSymP, 13, 4>,
                           (size_t)v2::Geo<13, 4, 8, true>::WAVE_BYTES * kWavesPerBlock, c);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || opt(HOP_OPT_NO_RERUN)) return e;
     LftArgs<double> r = a;
     r.cond = 1;
     return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, r);
@@ -2552,7 +2555,7 @@ hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream) {
   // QT / A / B reads under the two sweeps (SchedCondL: the fp64 default's placement)
   hipLaunchKernelGGL((v2::lft_cond_kernel<v2::SchedCondL, 13, 4, float>), dim3((unsigned)blocks),
                      dim3(256), (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
-  if (var == 41 || var == 57) return hipGetLastError();
+  if (var == 41 || var == 57 || opt(HOP_OPT_NO_RERUN)) return hipGetLastError();
   LftArgs<float> r = a;
   r.cond = 1;
   return dispatch_lft<float>(r, stream);

@@ -1257,7 +1257,7 @@ hipError_t launch(const RiccatiArgs<double>& a, hipStream_t stream) {
   // 4 % slower there (2.376 -> 2.476 ms), so it keeps one wave per SIMD.
   constexpr bool occ2_mode = MODE == 0 && !WANTV;
   if (occ2_mode && a.q_bstride == 0 && !force1 &&
-      (force2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count())) {
+      (force2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count(stream))) {
     hipLaunchKernelGGL((riccati_fast_kernel<MODE, WANTV, false, 0, true, occ2_mode>),
                        dim3((unsigned)blocks), dim3(256),
                        (size_t)kWavesPerBlock * (occ2_mode ? WAVE_BYTES2 : WAVE_BYTES), stream, a);

@@ -125,8 +125,12 @@ def ilqr_timeopt_sharded(system, x0_all, xg, u_ref, Q, R, Qf, w, N: int, T_min: 
     dev = device or (torch.device("cuda", torch.cuda.current_device())
                      if torch.cuda.is_available() else torch.device("cpu"))
     def shard(a, batch_ndim, name):
-        """rows [lo, hi) of a per-problem input (leading dim == total), else a shared one"""
+        """rows [lo, hi) of a per-problem input (leading dim == total), else a shared one;
+        a leading dimension of 1 is one block in batch form, which ilqr_timeopt_batch
+        broadcasts (solver.py: U_init [1, N', m]), so it passes through whole"""
         if a is None or np.ndim(a) < batch_ndim:
+            return a
+        if np.ndim(a) == batch_ndim and np.shape(a)[0] == 1 and total != 1:
             return a
         if np.ndim(a) > batch_ndim or np.shape(a)[0] != total:
             raise ValueError(f"{name}: per-problem inputs need the leading dimension B={total} "

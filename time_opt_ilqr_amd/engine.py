@@ -386,8 +386,10 @@ def riccati(A, Bm, X, U, xg, u_ref, Q, R, Qf, horizon, lm, *, mode: int = 0,
     A [B,N,n,n], Bm [B,N,n,m], X [B,N+1,n], U [B,N,m]; xg/u_ref/Q/R/Qf shared or
     per problem; horizon [B] int (T* or T_bar+S_right); lm [B] or scalar.
     legacy=True: the legacy twin's passes (ilqr_propagator.py:375-400 / 237-287,
-    hop_riccati_legacy_f64): its chol_solve (4 jitters, then lstsq, ST_LU), no
-    finiteness checks, Qf = alpha I; fp64, no extra stage cost.
+    hop_riccati_legacy_f64): mode 1 solves with its chol_solve (4 jitters, then
+    lstsq, ST_LU); mode 0 fails a row at its no-jitter Cholesky gate first, so its
+    solves never reach lstsq; no finiteness checks, Qf = alpha I; fp64, no extra
+    stage cost.
     """
     torch = _torch()
     dt = A.dtype
