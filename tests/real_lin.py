@@ -100,7 +100,24 @@ def run(d, dev):
            for k, v in out.items()}
     res["handover_traj"] = int(((ho_traj & _lib.ST_HANDOVER) != 0).sum().item())
     res["handover_aug"] = int(((ho_aug & _lib.ST_HANDOVER) != 0).sum().item())
+    res["ho_status_traj"] = ho_traj.cpu().numpy()
+    res["ho_status_aug"] = ho_aug.cpu().numpy()
     return res
+
+
+REASONS = {1: "stage inverse pivot", 2: "stage sigma", 4: "update pivot", 8: "query sigma",
+           16: "query pivot", 32: "non-finite J"}
+
+
+def handover_reasons(ho_status, final_status):
+    """Developer builds: (reason, first failing horizon, the rerun's final status) of
+    every handed-over problem (status bits 5.. of the NO_RERUN launch)."""
+    out = []
+    for b in np.nonzero(ho_status & 16)[0]:
+        why = int(ho_status[b]) >> 5
+        out.append((int(b), REASONS.get(why & 255, str(why & 255)), why >> 8,
+                    int(final_status[b])))
+    return out
 
 
 def oracle_sample(d, idx):
@@ -134,7 +151,13 @@ def compare(Ja, ta, Jb, tb, ok, T_min, T_max):
     flips = [int(i) for i in np.nonzero(ok)[0] if ta[i] != tb[i]]
     gaps = [near_tie_tol(Jb[i], int(ta[i]), int(tb[i])) for i in flips]
     q = (lambda p: float(np.quantile(rel_max, p))) if rel_max.size else (lambda p: 0.0)
+    # J at b's selected horizon (J*): the value the select hands on
+    idx = np.nonzero(ok)[0]
+    js = np.array([abs(Ja[i, tb[i] - 1] - Jb[i, tb[i] - 1]) / max(abs(Jb[i, tb[i] - 1]), 1e-300)
+                   for i in idx]) if idx.size else np.zeros(0)
+    qs = (lambda p: float(np.quantile(js, p))) if js.size else (lambda p: 0.0)
     return dict(n=int(ok.sum()), t_equal=int(ok.sum()) - len(flips), flips=len(flips),
+                jstar_rel_p50=qs(0.5), jstar_rel_p99=qs(0.99), jstar_rel_max=qs(1.0),
                 flip_gap_max=max(gaps) if gaps else 0.0,
                 rel_p50=q(0.5), rel_p99=q(0.99), rel_max=q(1.0),
                 frac_rel_gt_1e6=float(np.mean(rel_max > 1e-6)) if rel_max.size else 0.0,
@@ -157,6 +180,14 @@ def stats(name, Bn, seed, dev, n_oracle=32):
         J, ts, st = r[k]
         out[f"{k}_vs_traj_ref"] = compare(J, ts, Jr, tr, ok, T_min, T_max)
         out[f"{k}_status_equal"] = bool(np.array_equal(st[ok], sr[ok]))
+    hist = lambda st: {int(v): int(c) for v, c in zip(*np.unique(st[ok], return_counts=True))}  # noqa
+    out["status_hist"] = {k: hist(r[k][2]) for k in ("traj", "traj_ref", "aug", "aug_ref")}
+    # hand-overs the reference association finishes with status 0 (no jitter
+    # escalation: a false positive of the conditioned form's own tests)
+    for k in ("traj", "aug"):
+        ho = (r[f"ho_status_{k}"] & 16) != 0
+        out[f"handover_{k}_clean_final"] = int((ho & (r[k][2] == 0)).sum())
+        out[f"handover_{k}_reasons"] = handover_reasons(r[f"ho_status_{k}"], r[k][2])[:40]
     # oracle spot check: evenly spread sample of the finite problems
     cand = np.nonzero(ok)[0]
     idx = cand[np.linspace(0, len(cand) - 1, min(n_oracle, len(cand))).astype(int)]

@@ -239,6 +239,56 @@ def test_hand_scheduled_blocks_emulated(n):
     assert abs(regs[n][n] - q) <= 1e-12 * abs(q)
 
 
+def test_elimq2_block_emulated():
+    """ElimQ2<13> (the closed-form query's elimination, dpp_blocks.inc): the bordered
+    LDL of A with the border columns m (lane 13) and u (lane 14) leaves m^T A^-1 m and
+    u^T A^-1 u on lanes 13 / 14 of acc and -m^T A^-1 u on lane 14 of accx, so
+    m^T (A + u u^T / sigma)^-1 m = a - b^2 / (sigma + c) (Sherman-Morrison) without
+    forming the 1/sigma ~ 1e9 entries (CPU emulation, tools/emu_dpp.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    n = 13
+    rng = np.random.default_rng(5)
+    M = rng.standard_normal((n, n))
+    M = M @ M.T / n + 1e-3 * np.eye(n)
+    m, u = rng.standard_normal(n), rng.standard_normal(n)
+    regs = {}
+    for i in range(n):
+        col = np.zeros(16)
+        col[:n] = M[i]
+        col[n], col[n + 1] = m[i], u[i]
+        regs[i] = col
+    regs[n], regs[n + 1], regs[n + 2] = np.zeros(16), np.zeros(16), np.ones(16)
+    for j in range(6):
+        regs[n + 3 + j] = np.full(16, np.nan)
+    E.run(E.extract(inc, "ElimQ2", n), regs)
+    a, c, b = regs[n][n], regs[n][n + 1], -regs[n + 1][n + 1]
+    Mi = np.linalg.inv(M)
+    assert abs(a - m @ Mi @ m) <= 1e-11 * abs(m @ Mi @ m)
+    assert abs(c - u @ Mi @ u) <= 1e-11 * abs(u @ Mi @ u)
+    assert abs(b - m @ Mi @ u) <= 1e-11 * abs(m @ Mi @ m)
+    assert regs[n + 2][0] > 0
+    # the identity itself, against an exact rational solve of the 1e9-scaled matrix
+    # (LAPACK's fp64 solve of it is only ~2e-6 accurate here)
+    from fractions import Fraction as Fr
+    sig = 1e-9
+    K = [[Fr(M[i, j]) + Fr(u[i]) * Fr(u[j]) / Fr(sig) for j in range(n)] for i in range(n)]
+    y = [Fr(v) for v in m]
+    for p in range(n):
+        for i in range(p + 1, n):
+            f = K[i][p] / K[p][p]
+            for j in range(p, n):
+                K[i][j] -= f * K[p][j]
+            y[i] -= f * y[p]
+    x = [Fr(0)] * n
+    for i in reversed(range(n)):
+        x[i] = (y[i] - sum(K[i][j] * x[j] for j in range(i + 1, n))) / K[i][i]
+    want = float(sum(Fr(m[i]) * x[i] for i in range(n)))
+    assert abs((a - b * b / (sig + c)) - want) <= 1e-12 * abs(want)
+
+
 @pytest.mark.parametrize("n", [3, 13])
 def test_query_ldl_block_emulated(n):
     """QueryLdl<n>: X0 = Ebar - H^T (Mt + eps I)^-1 H from the offset-form Mt

@@ -228,6 +228,17 @@ struct SchedCondLSymF : SchedCondLSym {
 struct SchedCondTrajF : SchedCondTraj {
   static constexpr int FUSE = 1;
 };
+// lft_cond_cf_kernel with the round-3 query: the elimination of Sigma_eps + X_t with
+// X_t's 1/sigma ~ 1e9 rank-1 part formed (A/B, developer variant 97); the default
+// takes the rank-1 part by Sherman-Morrison (ElimQ2)
+struct SchedCondTrajG : SchedCondTraj {
+  static constexpr int GJQ = 1;
+};
+template <class C>
+constexpr bool has_gjq() {
+  if constexpr (requires { C::GJQ; }) return C::GJQ != 0;
+  return false;
+}
 template <class C>
 constexpr bool has_fuse() {
   if constexpr (requires { C::FUSE; }) return C::FUSE != 0;
@@ -1745,6 +1756,10 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   X[S] = 0.0;
   const double e_s = (c == S) ? 1.0 : 0.0;  // row S of A~^T: carries m through the first product
   bool bad = (a.cond & 2) != 0;
+  int why = 0;  // developer builds: first failing test and horizon (see lft_cond_cf_kernel)
+  auto flag = [&](bool f, int bit, int t) {
+    if constexpr (kDevBuild) why = (f && why == 0) ? (bit | (t << 8)) : why;
+  };
   unsigned long long sec[8] = {};
   unsigned long long tprev = 0;
   auto stamp = [&](int j) {
@@ -1865,6 +1880,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
                               in ? lds_addr(imB) + 8u * MM * c : zaddr};
       SweepQAB<S>::run(NX, d2, o2, ab);
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
+      flag(!pivots_ok(NE, d1) || !pivots_ok(NX, d2), 1, k + 1);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         at[j] = o2[j];
@@ -1899,6 +1915,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       SweepQ<S>::run(NE, d1);
       SweepQ<S>::run(NX, d2);
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
+      flag(!pivots_ok(NE, d1) || !pivots_ok(NX, d2), 1, k + 1);
     }
     stamp(3);
     // MFMA: the A~ / A operands of the predict's two products, read here because the
@@ -1966,6 +1983,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       else CondLdl<S>::run(r, Ht, X, dmin);
       const double x = bcast<S - 1>(r[S - 1]);
       bad = bad || !(dmin > 0.0) || (x != x);
+      flag(!(dmin > 0.0) || (x != x), 4, k + 1);
     }
     if (dma_late) {  // DSTAG 1: the odd waves' pieces, half a step after the even waves'
       wave_sync();
@@ -2044,11 +2062,13 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       const double q = bcast<S>(acc);
       const double gam = bcast<S>(X[S]);
       bad = bad || !(dmin > 0.0) || (q != q);
+      flag(!(dmin > 0.0) || (q != q), 16, k + 1);
       jk = 0.5 * (q - gam);
     }
     stamp(7);
     if constexpr (TRAJ && !F32) tb.load_rows(cq, imT, c);
     bad = bad || !finite_val(jk);
+    flag(!finite_val(jk), 32, k + 1);
     if (fuse_argmin) {
       const int t = k + 1;
       if (t == a.t_min) {
@@ -2073,7 +2093,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   }
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = (T)jprev;
-    a.status[prob] = bad ? (int)ST_RERUN : 0;
+    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : 0) : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = (T)best;
@@ -2173,6 +2193,12 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   const int cc = in ? c : 0;
   const double eps = 1e-9;
   bool bad = (a.cond & 2) != 0;
+  // developer builds: the first failing test and its horizon (hand-over diagnosis,
+  // reported in status bits 5.. under a.cond & 4); product builds compile none of it
+  int why = 0;
+  auto flag = [&](bool f, int bit, int t) {
+    if constexpr (kDevBuild) why = (f && why == 0) ? (bit | (t << 8)) : why;
+  };
   // raw Q rows (Q e), (Qs + eps I)^-1 and (P + eps I)^-1 rows, parked per wave in
   // LDS as register images (row i of lane l at [i][l]; the Q / QT image areas
   // and the tile slot are free in this kernel) and re-read each step
@@ -2198,6 +2224,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     SweepQ<NN>::run(Qi, d1);
     SweepQ<NN>::run(Pi, d2);
     bad = bad || !pivots_ok(Qi, d1) || !pivots_ok(Pi, d2);
+    flag(bad, 1, 0);
     static_for<NN>([&](auto I) {
       Qi[I] = sel_lane<I>(0.0, 1.0) - Qi[I];
       Pi[I] = sel_lane<I>(0.0, 1.0) - Pi[I];
@@ -2244,6 +2271,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   static_for<S>([&](auto I) { X[I] = (c == S) ? (I == NN ? 1.0 : 0.0) : sel_lane<I>(0.0, eps); });
   X[S] = 0.0;
   const double e_s = (c == S) ? 1.0 : 0.0;
+  const double e_s1 = (c == S + 1) ? 1.0 : 0.0;  // the query's u border (ElimQ2)
   const double m1 = (c == NN) ? -1.0 : 0.0;  // lane NN of v' / u'
 
   double best = 0.0, jprev = 0.0;
@@ -2292,6 +2320,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       const double qv = lane_sum<NN>(qe_k * v);
       const double sig = (((eqe_k + w2) + t.rho_reg) + eps) - qv;
       bad = bad || !(sig > 0.0);
+      flag(!(sig > 0.0), 2, k + 1);
       const double vp = in ? v : m1;
       const double wp = vp * recip_nr(sig);
 #pragma unroll
@@ -2316,6 +2345,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       CondLdlN<S>::run(r, Ht, X, dmin);
       const double x = bcast<S - 1>(r[S - 1]);
       bad = bad || !(dmin > 0.0) || (x != x);
+      flag(!(dmin > 0.0) || (x != x), 4, k + 1);
     }
     // ---- predict
     {
@@ -2342,22 +2372,42 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       const double eu = lane_sum<NN>(e1 * u);
       const double sig = (t.rho_reg + eps) + eps * eu;
       bad = bad || !(sig > 0.0);
-      const double wq = u * recip_nr(sig);
+      flag(!(sig > 0.0), 8, k + 1);
       double rq[S];
 #pragma unroll
       for (int i = 0; i < NN; ++i) rq[i] = X[i] + Pi[i];
       rq[NN] = X[NN];
-      LaneB<S>::fma(rq, wq, u);
-      double acc = 0.0, dmin = 1.0;
-      ElimQ<S>::run(rq, acc, dmin, 0.0);
-      const double q = bcast<S>(acc);
+      double q;
+      if constexpr (has_gjq<C>()) {  // round 3: eliminate A + u u^T / sigma itself
+        const double wq = u * recip_nr(sig);
+        LaneB<S>::fma(rq, wq, u);
+        double acc = 0.0, dmin = 1.0;
+        ElimQ<S>::run(rq, acc, dmin, 0.0);
+        q = bcast<S>(acc);
+        bad = bad || !(dmin > 0.0) || (q != q);
+        flag(!(dmin > 0.0) || (q != q), 16, k + 1);
+      } else {
+        // m^T (A + u u^T / sigma)^-1 m = a - b^2 / (sigma + c) with A = Sigma_eps +
+        // Pi_ext and a, b, c = m^T A^-1 m, m^T A^-1 u, u^T A^-1 u from ONE bordered
+        // elimination of [A | m u] (u rides on lane S + 1): A's pivots stay O(|A|)
+        // while the 1/sigma ~ 1e9 entries of the round-3 form cancelled in them
+        // (measured false hand-overs on real quadrotor linearisations)
+        LaneB<S>::fma(rq, u, e_s1);  // lane S + 1 of row i: u_i
+        double acc = 0.0, accx = 0.0, dmin = 1.0;
+        ElimQ2<S>::run(rq, acc, accx, dmin);
+        const double qa = bcast<S>(acc), qc = bcast<S + 1>(acc), qb = bcast<S + 1>(accx);
+        const double den = sig + qc;
+        q = qa - qb * qb * recip_nr(den);
+        bad = bad || !(dmin > 0.0) || !(den > 0.0) || (q != q);
+        flag(!(dmin > 0.0) || !(den > 0.0) || (q != q), 16, k + 1);
+      }
       const double gam = bcast<S>(X[S]);
-      bad = bad || !(dmin > 0.0) || (q != q);
       jk = 0.5 * (q - gam);
     }
     qe_k = qe1;
     eqe_k = eqe1;
     bad = bad || !finite_val(jk);
+    flag(!finite_val(jk), 32, k + 1);
     if (fuse_argmin) {
       const int tt = k + 1;
       if (tt == a.t_min) {
@@ -2376,7 +2426,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   dma_wait();
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = jprev;
-    a.status[prob] = bad ? (int)ST_RERUN : 0;
+    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : 0) : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = best;
@@ -2409,9 +2459,12 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return hipGetLastError();
   };
   // conditioned kernel, then the rerun launch (cond = 1) of the flagged problems
+  // developer builds under HOP_OPT_NO_RERUN: the flagged problems' status also
+  // carries the first failing test and horizon (bits 5.., lft_cond_cf_kernel)
+  const int why_bit = (kDevBuild && opt(HOP_OPT_NO_RERUN)) ? 4 : 0;
   auto cond_rerun = [&](auto kc, auto kr, size_t bytes, bool rerun) {
     LftArgs<double> c = a;
-    c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+    c.cond = (opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0) | why_bit;
     hipError_t e = launch(kc, bytes, c);
     if (e != hipSuccess || !rerun || opt(HOP_OPT_NO_RERUN)) return e;
     LftArgs<double> r = a;
@@ -2427,6 +2480,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     if (variant == 54)  // closed-form stage inverses without the rerun launch
       return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, false);
+    if (variant == 97 || variant == 98)  // the round-3 query (+ rerun unless 98)
+      return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTrajG, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, variant == 97);
     if (variant == 40 || variant == 41)  // Gauss-Jordan stage inverses (+ rerun unless 41)
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondTraj, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, variant == 40);
@@ -2507,7 +2563,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
 #endif
   if (!pack1 && (pack2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count(stream))) {
     LftArgs<double> c = a;
-    c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
+    c.cond = (opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0) | why_bit;
     hipError_t e = launch(v2::lft_cond_kernel<v2::SchedCondLSymP, 13, 4>,
                           (size_t)v2::Geo<13, 4, 8, true>::WAVE_BYTES * kWavesPerBlock, c);
     if (e != hipSuccess || opt(HOP_OPT_NO_RERUN)) return e;

@@ -35,7 +35,8 @@ def probe(*a, **k):
     flagged = np.nonzero(st & _lib.ST_HANDOVER)[0]
     sel = len(log)
     full = orig(*a, **k)
-    log.append((len(st), flagged.tolist(), full.status.cpu().numpy()[flagged].tolist()))
+    log.append((len(st), flagged.tolist(), full.status.cpu().numpy()[flagged].tolist(),
+                [(int(st[i]) >> 5) & 255 for i in flagged], [int(st[i]) >> 13 for i in flagged]))
     names = ("A", "B", "a_res", "X", "U", "xg", "u_ref", "Q", "R_inv", "P", "w")
     for i in flagged.tolist():
         for nm, t in zip(names, a):
@@ -55,8 +56,9 @@ engine.propagate_traj = probe
 solver.engine.propagate_traj = probe
 res = solver.ilqr_timeopt_batch(2, X0, xg, u_ref, Q, R, Qf, w, N, max(1, N // 5), N, dt=F.dt,
                                 max_iter=iters, wrap_idx=wrap, use_central_diff=False)
-for i, (b, idx, sts) in enumerate(log):
-    print(f"select {i}: batch {b}, handed over {len(idx)}: {idx[:12]} final status {sts[:12]}")
+for i, (b, idx, sts, why, at) in enumerate(log):
+    print(f"select {i}: batch {b}, handed over {len(idx)}: {idx[:12]} final status {sts[:12]}"
+          f" reason bits {why[:12]} (developer builds) at horizon {at[:12]}")
 print("crashed", int(res["crashed"].sum().item()))
 os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
 np.savez_compressed(out, **caps)
