@@ -269,6 +269,7 @@ def _lft_workload(args, world, lo, hi, dev):
 
         host, alt = (At.data, Bt.data, Qt.data, Ri, z0, QTt.data), launch_bm
 
+    side = _traj64_side(hi - lo, s, m, N, t_min, dtype, dev) if tiled else None
     kname, bound = kernel_path(s, m, args.dtype)
     if small:
         kname = kname[:-1] + (",LY=2 tile64>" if tiled else ",LY=1 batch-major>")
@@ -277,8 +278,58 @@ def _lft_workload(args, world, lo, hi, dev):
                 executed=(cond_flops(N, s, m) if kname.startswith("lft_cond") else
                           small_flops(N, s, m) if kname.startswith("lft_small") else None),
                 t_min=t_min, t_max=t_max, s=s, m=m, N=N, host=host, alt=alt,
-                layout="tile64" if tiled else "batch-major")
+                layout="tile64" if tiled else "batch-major", side=side)
     return launch, info
+
+
+def _traj64_side(Bn, s, m, N, t_min, dtype, dev):
+    """Config 3 from the raw linearisation, timed beside the
+    line: the select block (augmented.py:10-87 built per lane in registers +
+    propagator + argmin, solver.py:514-522) streaming raw A_k, B_k, a_k, x_k, u_k in
+    the tile64 layout hop_linearize_tile64_* writes (synthetic raw arrays of
+    tools/bench_traj.py's distribution, rho_reg = 1e-12); and the same preceded by
+    that linearisation of cart-pole rollouts (fp64 in, fp32 tile64 out)."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    n = s - 1
+    g = torch.Generator(device=dev)
+    g.manual_seed(17)
+    kw = dict(device=dev, dtype=dtype, generator=g)
+    eye = torch.eye(n, device=dev, dtype=dtype)
+    raw = [eye + 0.05 * torch.randn((Bn, N, n, n), **kw), 0.1 * torch.randn((Bn, N, n, m), **kw),
+           0.02 * torch.randn((Bn, N, n, 1), **kw), 0.5 * torch.randn((Bn, N + 1, n, 1), **kw),
+           0.3 * torch.randn((Bn, N, m, 1), **kw)]
+    t64 = [engine.to_tile64(x) for x in raw]
+    del raw
+    xg, ur = 0.2 * torch.randn((n,), **kw), 0.1 * torch.randn((m,), **kw)
+    M = torch.randn((n, n), **kw)
+    Q = M @ M.T / n + 0.5 * eye
+    Rinv = torch.diag(1.0 / (0.5 + 1.5 * torch.rand((m,), **kw)))
+    P = torch.diag(1.0 + 9.0 * torch.rand((n,), **kw))
+    shared = (xg, ur, Q, Rinv, P, torch.full((1,), 0.5, dtype=dtype, device=dev))
+
+    def select():
+        return engine.propagate_traj(*t64, *shared, wrap_idx=[n - 1], t_min=t_min, t_max=N)
+
+    out = {"select_traj64": select,
+           "select_bytes_per_sweep": (N * (n * n + n * m + 2 * n + m) + n) * (4 if dtype ==
+                                                                              torch.float32 else 8)}
+    if (s, m) == (5, 1):  # cart-pole dynamics (systems.py:57-112)
+        from time_opt_ilqr_amd import systems
+        F, x0 = systems.make_cartpole_swingup(N=N)[:2]
+        g64 = dict(device=dev, dtype=torch.float64, generator=g)
+        U = 2.0 * torch.randn((Bn, N, 1), **g64)
+        X = engine.rollout(F.system_id, torch.as_tensor(x0, device=dev) +
+                           0.3 * torch.randn((Bn, n), **g64), U, F.dt)
+
+        def lin_select():
+            lin = engine.linearize(F.system_id, X, U, F.dt, central=True, tile64=True,
+                                   tile64_dtype=dtype)
+            return engine.propagate_traj(lin.A, lin.B, lin.a_res, lin.X, lin.U, *shared,
+                                         wrap_idx=[2], t_min=t_min, t_max=N)
+
+        out["linearize_select_traj64"] = lin_select
+    return out
 
 
 def _config5_workload(args, world, lo, hi, dev):
@@ -717,6 +768,36 @@ def main(argv=None):
                "each step (PCIe-inclusive); not the headline value"}
         del pinned
 
+    # side figures of the tile64 config-3 line: the select from the raw linearisation
+    traj64 = None
+    if rank == 0 and info.get("side") is not None and not args.no_alt:
+        traj64 = {}
+        for key in ("select_traj64", "linearize_select_traj64"):
+            fn = info["side"].get(key)
+            if fn is None:
+                continue
+            r_ = fn()
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 10
+            traj64[key] = {"ms": ms, "sweeps_per_s": (hi - lo) / (ms * 1e-3),
+                           "status_ok": bool(torch.isfinite(r_.J).all())}
+        bps = info["side"]["select_bytes_per_sweep"]
+        sel = traj64.get("select_traj64")
+        if sel is not None:
+            sel["alg_bytes_per_sweep"] = bps
+            sel["hbm_frac"] = bps * (hi - lo) / (sel["ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS
+        traj64["note"] = ("raw A_k, B_k, a_k, x_k, u_k in tile64 (hop_lft_sweep_traj_tile64); "
+                          "linearize_select adds hop_linearize_tile64_f32 of cart-pole "
+                          "rollouts in the same timing")
+        info["side"] = None
+
     # side figure: the same sweep on batch-major blocks (tile64 runs only)
     alt_ms = None
     if rank == 0 and info.get("alt") is not None and not args.no_alt:
@@ -819,6 +900,7 @@ def main(argv=None):
             "h2d_inclusive": h2d,
             "config4_shard_anchor": anchor,
             "config4_global_1gpu": anchor_g,
+            **({"config3_from_linearisation": traj64} if traj64 else {}),
             "status_ok": status_ok,
         }
         print(json.dumps(line), flush=True)

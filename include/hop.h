@@ -164,6 +164,42 @@ int hop_lft_sweep_tile64_f32(const float* A_aug, const float* B_aug, const float
                              int32_t* status, int32_t* t_star, float* j_star, void* stream);
 
 /*
+ * hop_lft_sweep_traj_tile64_f64 / _f32
+ * hop_lft_sweep_traj_* (the select block of solver.py:514-522: the augmented
+ * builders of augmented.py:10-87 + propagator_all_Jt_aug + argmin) with the raw
+ * linearisation in the tile64 layout -- A [.][n_alloc][n*n][64], Bm
+ * [.][n_alloc][n*m][64], a_res [.][n_alloc][n][64], U [.][n_alloc][m][64] and X
+ * [.][n_alloc+1][n][64] (x_0 .. x_{n_use}) -- as hop_linearize_tile64_* writes it.
+ * A wave of 64 problems then streams each step's raw blocks as contiguous spans
+ * (the batch-major raw arrays are 64 scattered rows per piece).  Shared inputs
+ * (xg, u_ref, Q, P, w, R_inv) and every output as hop_lft_sweep_traj_*; no
+ * extra_stage_cost.  Small-s shapes only (s = n + 1; fp32: s <= 5, m <= 2;
+ * fp64: s <= 4, m <= 2), else HOP_E_SIZE.
+ */
+int hop_lft_sweep_traj_tile64_f64(const double* A, const double* Bm, const double* a_res,
+                                  const double* X, const double* U, const double* xg,
+                                  int64_t xg_batch_stride, const double* u_ref,
+                                  int64_t u_ref_batch_stride, const double* Q,
+                                  int64_t q_batch_stride, const double* P, int64_t p_batch_stride,
+                                  const double* w, int64_t w_batch_stride, uint32_t wrap_mask,
+                                  double q_reg, double rho_reg, const double* R_inv,
+                                  int64_t r_batch_stride, int64_t batch, int32_t n_alloc,
+                                  int32_t n_use, int32_t n, int32_t m, int32_t max_tries,
+                                  int32_t t_min, int32_t t_max, double* J, int32_t* status,
+                                  int32_t* t_star, double* j_star, void* stream);
+int hop_lft_sweep_traj_tile64_f32(const float* A, const float* Bm, const float* a_res,
+                                  const float* X, const float* U, const float* xg,
+                                  int64_t xg_batch_stride, const float* u_ref,
+                                  int64_t u_ref_batch_stride, const float* Q,
+                                  int64_t q_batch_stride, const float* P, int64_t p_batch_stride,
+                                  const float* w, int64_t w_batch_stride, uint32_t wrap_mask,
+                                  float q_reg, float rho_reg, const float* R_inv,
+                                  int64_t r_batch_stride, int64_t batch, int32_t n_alloc,
+                                  int32_t n_use, int32_t n, int32_t m, int32_t max_tries,
+                                  int32_t t_min, int32_t t_max, float* J, int32_t* status,
+                                  int32_t* t_star, float* j_star, void* stream);
+
+/*
  * hop_select_horizon_f64 / _f32
  * Replaces T = int(np.argmin(J[T_min-1:T_max]) + T_min)
  *   /root/reference/solver.py:522, 590, 613 (legacy ilqr_propagator.py:496, 547).
@@ -409,6 +445,26 @@ int hop_linearize_f64(int32_t system, double dt, const double* X, const double* 
                       int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
                       double epsx, double epsu, double relx, double relu, double* A,
                       double* Bm, double* a_res, double* Fx, void* stream);
+
+/*
+ * hop_linearize_tile64_f64 / _f32
+ * hop_linearize_f64 (linearization.py:177-270, computed in fp64) writing the tile64
+ * layout hop_lft_sweep_traj_tile64_* reads, as fp64 or fp32: A [ceil(B/64)][n_alloc]
+ * [n*n][64], Bm [.][n_alloc][n*m][64], a_res [.][n_alloc][n][64] (nullable), and the
+ * tile64 copies of the trajectory, Xt [.][n_alloc+1][n][64] (rows 0 .. n_use) and
+ * Ut [.][n_alloc][m][64] (rows < n_use).  Padding slots of the last tile are 0;
+ * steps >= n_use are not written.  X [batch][n_alloc+1][n], U [batch][n_alloc][m]
+ * are fp64 batch-major as for hop_linearize_f64.  Size each output with
+ * hop_tile64_elems(batch, n_alloc (+1 for Xt), elems).
+ */
+int hop_linearize_tile64_f64(int32_t system, double dt, const double* X, const double* U,
+                             int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                             double epsx, double epsu, double relx, double relu, double* A,
+                             double* Bm, double* a_res, double* Xt, double* Ut, void* stream);
+int hop_linearize_tile64_f32(int32_t system, double dt, const double* X, const double* U,
+                             int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                             double epsx, double epsu, double relx, double relu, float* A,
+                             float* Bm, float* a_res, float* Xt, float* Ut, void* stream);
 
 /*
  * hop_dynamics_f64

@@ -1,0 +1,82 @@
+"""GPU parity of the select block on REAL linearisations.
+
+Ground truth (tests/golden/real_lin_hp.npz, tests/golden/make_hp.py): the
+reference's association of propagator_all_Jt_aug (horizon_selection.py:36-86)
+evaluated in 50-digit arithmetic on exactly the fp64 augmented blocks of the
+reference's builders (augmented.py:10-87, rho_reg = 1e-12) for perturbed
+rollouts of the quadrotor, segway, cart-pole and double integrator, central
+differences (linearization.py:177-211).  The fp64 NumPy reference is itself far
+from it on these inputs (the fixture records its J: 1e-4 .. 6 relative, and a
+different T* on one cart-pole problem), so J is held to the 50-digit value, not
+to the fp64 run.
+
+Batch scale (tests/real_lin.py): 4096 device-linearised problems per system;
+the product select against the reference association on the device
+(HOP_OPT_REFERENCE_ASSOC) and the oracle on a sample: T* agreement, J* spread,
+and the hand-over count of the conditioned kernels (HOP_OPT_NO_RERUN).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+
+from oracle import hop_oracle as orc  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+# relative J bar against the 50-digit curve over [T_min, T_max], per system
+J_BAR = {"quadrotor": 1e-6, "segway": 1e-6, "cartpole": 1e-6, "di": 1e-6}
+
+
+def _t(x, dev):
+    import torch
+    return torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64, device=dev)
+
+
+@pytest.mark.parametrize("name", ["quadrotor", "segway", "cartpole", "di"])
+def test_select_on_real_linearisations_vs_50_digit_reference(dev, golden_dir, name):
+    import make_hp as mh
+    from time_opt_ilqr_amd import engine
+    d = np.load(os.path.join(golden_dir, "real_lin_hp.npz"))
+    sid, N, T_min, T_max, _, xg, ur, Q, R, alpha, w, wrap = mh.CASES[name][:12]
+    cnt = int(d[f"{name}_count"])
+    tags = [f"{name}_p{i}" for i in range(cnt)]
+    st = {k: np.stack([d[f"{t}_{k}"][:N + (k == "X")] for t in tags])
+          for k in ("A", "B", "a_res", "X", "U")}
+    n = st["X"].shape[-1]
+    P = orc.terminal_weight(alpha, n)
+    Ri = orc.spd_inverse(orc.sym(R))[0]
+    res = engine.propagate_traj(*(_t(st[k], dev) for k in ("A", "B", "a_res", "X", "U")),
+                                _t(xg, dev), _t(ur, dev), _t(Q, dev), _t(Ri, dev), _t(P, dev),
+                                _t(np.array([w]), dev), wrap_idx=wrap, n_use=N, t_min=T_min,
+                                t_max=T_max)
+    J = res.J.cpu().numpy()
+    assert (res.status.cpu().numpy() == 0).all()
+    for b, t in enumerate(tags):
+        Jh = d[f"{t}_J_hp"]
+        win = slice(T_min - 1, T_max)
+        rel = np.max(np.abs(J[b, win] - Jh[win]) / np.abs(Jh[win]))
+        assert rel <= J_BAR[name], (t, rel)
+        assert int(res.t_star[b]) == int(np.argmin(Jh[win]) + T_min), t
+
+
+@pytest.mark.parametrize("name", ["quadrotor", "segway", "cartpole", "di"])
+def test_select_batch_scale_real_linearisations(dev, name):
+    """4096 device-linearised problems: the product select and the reference
+    association agree on T* except at near-ties (both curves carry the fp64
+    conditioning error of these inputs: a flip must be within 2e-2 relative on the
+    reference association's curve), the oracle's sample agrees with the product's
+    T* except at near-ties of its own curve (1e-3), and nothing the reference
+    solves cleanly is handed to the rerun launch: every hand-over is a problem
+    whose status the reference marks (a non-finite trajectory)."""
+    import real_lin
+    st = real_lin.stats(name, 4096, 1000 + list(real_lin.SYSTEMS).index(name), dev)
+    c = st["traj_vs_traj_ref"]
+    assert c["flips"] <= 0.005 * c["n"] and c["flip_gap_max"] <= 2e-2, c
+    o = st["traj_vs_oracle"]
+    assert o["flip_gap_max"] <= 1e-3, o
+    assert st["handover_traj_clean_final"] == 0, st["handover_traj_reasons"]
+    assert st["handover_traj"] <= 4096 - st["finite"]

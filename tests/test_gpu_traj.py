@@ -365,3 +365,107 @@ def test_reference_shaped_augmented_builders(dev):
     QT = augmented.build_terminal_aug_list(X, xg, alpha, wrap_idx=[2])
     oQT = orc.augment_terminal(X, xg, alpha, wrap_idx=[2])
     assert len(QT) == N and _rel(np.array(QT), oQT) <= 1e-14
+
+
+# ---- tile64 raw linearisation (hop_linearize_tile64_* -> hop_lft_sweep_traj_tile64_*)
+
+@pytest.mark.parametrize("sid,central", [(1, True), (1, False), (0, True), (4, False)])
+def test_linearize_tile64_equals_batch_major(dev, sid, central):
+    """hop_linearize_tile64_*: the same values as hop_linearize_f64 (fp64 output:
+    bitwise; fp32 output: the fp64 result rounded once), laid out as tile64, with
+    the trajectory copies X (rows 0 .. n_use) / U (rows < n_use) and zero padding
+    slots; a ragged batch (70 = one full tile + 6) and n_use < N."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    from oracle import dyn_oracle as dyn
+    n, m = dyn.DIMS[sid]
+    Bn, N, n_use = 70, 23, 19
+    rng = np.random.default_rng(40 + sid)
+    X = 0.7 * rng.standard_normal((Bn, N + 1, n))
+    U = 0.5 * rng.standard_normal((Bn, N, m))
+    Xt, Ut = _t(X, dev), _t(U, dev)
+    dt = dyn.DEFAULT_DT[sid]
+    ref = engine.linearize(sid, Xt, Ut, dt, central=central, n_use=n_use)
+    for odt in (torch.float64, torch.float32):
+        t = engine.linearize(sid, Xt, Ut, dt, central=central, n_use=n_use, tile64=True,
+                             tile64_dtype=odt)
+        for got, want, steps in ((t.A, ref.A, n_use), (t.B, ref.B, n_use),
+                                 (t.a_res, ref.a_res[..., None], n_use)):
+            bm = engine.from_tile64(got)[:, :steps].reshape(Bn, steps, -1)
+            w = want[:, :steps].reshape(Bn, steps, -1).to(odt)
+            assert torch.equal(bm, w)
+            assert (got.data[-1, :steps, :, Bn % 64:] == 0).all()  # padding slots
+        assert torch.equal(engine.from_tile64(t.X)[:, :n_use + 1, :, 0], Xt[:, :n_use + 1].to(odt))
+        assert torch.equal(engine.from_tile64(t.U)[:, :n_use, :, 0], Ut[:, :n_use].to(odt))
+
+
+@pytest.mark.parametrize("n,m,dt", [(4, 1, "f32"), (4, 2, "f32"), (2, 1, "f64"), (3, 1, "f64")])
+def test_traj_tile64_equals_batch_major_and_oracle(dev, n, m, dt):
+    """hop_lft_sweep_traj_tile64_* on tile64 raw arrays (a ragged 67-problem batch):
+    fp64 (the LFT association on both layouts) bitwise the batch-major trajectory
+    kernel's J / T* / status; fp32 (tile64: the conditioned association + the LFT
+    rerun, as the augmented tile64 sweep) within the fp32 bar of it, T* equal except
+    at near-ties; the oracle on a sample at the fp64 / fp32 bars."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    dtype = torch.float64 if dt == "f64" else torch.float32
+    N = 45
+    ps, st = _batch(range(1300, 1367), n, m, N)
+    raw = _dev_args(st, dev, dtype)
+    shared = (raw[5], raw[6], raw[7], _t(st["R_inv"], dev, dtype), _t(st["P"], dev, dtype),
+              _t(st["w"], dev, dtype))
+    kw = dict(wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=N)
+    bm = engine.propagate_traj(*raw[:5], *shared, **kw)
+    t64 = [engine.to_tile64(x if x.dim() == 4 else x[..., None]) for x in raw[:5]]
+    tl = engine.propagate_traj(*t64, *shared, **kw)
+    if dt == "f64":
+        assert torch.equal(tl.J, bm.J) and torch.equal(tl.t_star, bm.t_star)
+        assert torch.equal(tl.status, bm.status) and (tl.status == 0).all()
+    else:
+        from test_gpu_configs import _same_sweep
+        _same_sweep(tl, bm, False, tol=2e-3)
+    J = tl.J.double().cpu().numpy()
+    tol = 1e-9 if dt == "f64" else 2e-3
+    for i in (0, 33, 63, 64, 66):
+        _, o = _oracle(ps[i], 1.0)
+        assert _rel(J[i], o["J"]) <= tol
+
+
+def test_traj_tile64_config3_size_from_linearisation(dev):
+    """Config 3's shape end to end (s = 5, m = 1, N = 200, B = 65,536, fp32): cart-pole
+    rollouts linearised straight into fp32 tile64 (hop_linearize_tile64_f32), then
+    the tile64 select; problems spread over the batch against the oracle's builders
+    and propagator on the same (fp32-rounded) raw arrays, at the fp32 bar.  The cost
+    is a well-conditioned one (the maker's zero angle weight puts 1e9 entries in
+    E_k = (Q_aug + eps I)^-1, and rho_reg = 1e-12 Schur complements, neither of which
+    an fp32 sweep resolves)."""
+    import torch
+    from time_opt_ilqr_amd import engine, systems
+    F, x0, xg, u_ref, _, _, _, _, _, _, _, wrap, _ = systems.make_cartpole_swingup(N=200)
+    Q, R, alpha, w = np.diag([1.0, 0.5, 2.0, 0.5]), np.array([[0.1]]), np.array([5.0, 5.0, 20.0,
+                                                                                   5.0]), 0.03
+    Bn, N, T_min = 65536, 200, 40
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    U = 2.0 * torch.randn((Bn, N, 1), device=dev, dtype=torch.float64, generator=g)
+    X0 = torch.as_tensor(x0, device=dev) + 0.3 * torch.randn((Bn, 4), device=dev,
+                                                               dtype=torch.float64, generator=g)
+    X = engine.rollout(F.system_id, X0, U, F.dt)
+    lin = engine.linearize(F.system_id, X, U, F.dt, central=True, tile64=True,
+                           tile64_dtype=torch.float32)
+    P = orc.terminal_weight(alpha, 4)
+    Ri = orc.spd_inverse(orc.sym(R))[0]
+    f = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float32), device=dev)  # noqa: E731
+    res = engine.propagate_traj(lin.A, lin.B, lin.a_res, lin.X, lin.U, f(xg), f(u_ref), f(Q),
+                                f(Ri), f(P), f([w]), wrap_idx=wrap, rho_reg=1.0, t_min=T_min,
+                                t_max=N)
+    torch.cuda.synchronize()
+    assert torch.isfinite(res.J).all()
+    Ab, Bb, ab = (engine.from_tile64(t).double().cpu().numpy() for t in (lin.A, lin.B, lin.a_res))
+    Xb = engine.from_tile64(lin.X).double().cpu().numpy()[..., 0]
+    Ub = engine.from_tile64(lin.U).double().cpu().numpy()[..., 0]
+    for b in (0, 1, 63, 64, 40000, Bn - 1):
+        p = dict(A=Ab[b], B=Bb[b], a_res=ab[b, :, :, 0], X=Xb[b], U=Ub[b], xg=xg, u_ref=u_ref,
+                 Q=Q, R=R, alpha=alpha, w=w, wrap_idx=wrap)
+        _, o = _oracle(p, 1.0)
+        assert _rel(res.J[b].double().cpu().numpy(), o["J"]) <= 2e-3, b

@@ -5,6 +5,7 @@ oracle; the product path refuses to run without a HIP device."""
 import ctypes as C
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -30,7 +31,7 @@ def _header_functions():
 
 def test_header_symbols_exported(lib):
     names = _header_functions()
-    assert len(names) == 36
+    assert len(names) == 40
     from time_opt_ilqr_amd import _lib
     assert sorted(_lib.SIGNATURES) == names
     for n in names:
@@ -237,56 +238,6 @@ def test_hand_scheduled_blocks_emulated(n):
     E.run(E.extract(inc, "ElimQ", n), regs)
     q = z @ np.linalg.solve(M + eps * np.eye(n), z)
     assert abs(regs[n][n] - q) <= 1e-12 * abs(q)
-
-
-def test_elimq2_block_emulated():
-    """ElimQ2<13> (the closed-form query's elimination, dpp_blocks.inc): the bordered
-    LDL of A with the border columns m (lane 13) and u (lane 14) leaves m^T A^-1 m and
-    u^T A^-1 u on lanes 13 / 14 of acc and -m^T A^-1 u on lane 14 of accx, so
-    m^T (A + u u^T / sigma)^-1 m = a - b^2 / (sigma + c) (Sherman-Morrison) without
-    forming the 1/sigma ~ 1e9 entries (CPU emulation, tools/emu_dpp.py)."""
-    import sys
-    sys.path.insert(0, os.path.join(REPO, "tools"))
-    import emu_dpp as E
-    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
-    n = 13
-    rng = np.random.default_rng(5)
-    M = rng.standard_normal((n, n))
-    M = M @ M.T / n + 1e-3 * np.eye(n)
-    m, u = rng.standard_normal(n), rng.standard_normal(n)
-    regs = {}
-    for i in range(n):
-        col = np.zeros(16)
-        col[:n] = M[i]
-        col[n], col[n + 1] = m[i], u[i]
-        regs[i] = col
-    regs[n], regs[n + 1], regs[n + 2] = np.zeros(16), np.zeros(16), np.ones(16)
-    for j in range(6):
-        regs[n + 3 + j] = np.full(16, np.nan)
-    E.run(E.extract(inc, "ElimQ2", n), regs)
-    a, c, b = regs[n][n], regs[n][n + 1], -regs[n + 1][n + 1]
-    Mi = np.linalg.inv(M)
-    assert abs(a - m @ Mi @ m) <= 1e-11 * abs(m @ Mi @ m)
-    assert abs(c - u @ Mi @ u) <= 1e-11 * abs(u @ Mi @ u)
-    assert abs(b - m @ Mi @ u) <= 1e-11 * abs(m @ Mi @ m)
-    assert regs[n + 2][0] > 0
-    # the identity itself, against an exact rational solve of the 1e9-scaled matrix
-    # (LAPACK's fp64 solve of it is only ~2e-6 accurate here)
-    from fractions import Fraction as Fr
-    sig = 1e-9
-    K = [[Fr(M[i, j]) + Fr(u[i]) * Fr(u[j]) / Fr(sig) for j in range(n)] for i in range(n)]
-    y = [Fr(v) for v in m]
-    for p in range(n):
-        for i in range(p + 1, n):
-            f = K[i][p] / K[p][p]
-            for j in range(p, n):
-                K[i][j] -= f * K[p][j]
-            y[i] -= f * y[p]
-    x = [Fr(0)] * n
-    for i in reversed(range(n)):
-        x[i] = (y[i] - sum(K[i][j] * x[j] for j in range(i + 1, n))) / K[i][i]
-    want = float(sum(Fr(m[i]) * x[i] for i in range(n)))
-    assert abs((a - b * b / (sig + c)) - want) <= 1e-12 * abs(want)
 
 
 @pytest.mark.parametrize("n", [3, 13])
@@ -556,6 +507,42 @@ def test_small_cond_math_vs_golden(small_host, golden_dir, tag, dt):
     assert (st == 0).all()
     if dt == np.float64:
         assert ts.tolist() == d["T_star"].tolist()
+
+
+@pytest.mark.parametrize("name", ["segway", "cartpole", "di"])
+def test_small_cond_math_real_linearisations_vs_50_digit(small_host, golden_dir, name):
+    """The small-s conditioned arithmetic (small_math.hpp cond_step + cond_query, the
+    code the COND kernels run) on real linearisations at rho_reg = 1e-12
+    (tests/golden/real_lin_hp.npz): within 1e-9 of the 50-digit evaluation of the
+    reference's algorithm and the same T*, where the fp64 NumPy reference is 5e-6 ..
+    6 away and picks a different T* on one cart-pole problem; the round-3 query
+    (cond_query_direct: the elimination of Sigma_eps + X_t with X_t formed) is
+    worse than the new one on every problem."""
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    import make_hp as mh
+    d = np.load(os.path.join(golden_dir, "real_lin_hp.npz"))
+    sid, N, T_min, T_max = mh.CASES[name][:4]
+    p = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    win = slice(T_min - 1, T_max)
+    for i in range(int(d[f"{name}_count"])):
+        t = f"{name}_p{i}"
+        prob = {k: d[f"{t}_{k}"] for k in ("A", "B", "a_res", "X", "U")}
+        Aa, Ba, Qa, Ri, z0, QT = (np.ascontiguousarray(x, dtype=np.float64)
+                                  for x in mh.blocks(name, prob))
+        s, m = Aa.shape[-1], Ba.shape[-1]
+        Jh = d[f"{t}_J_hp"]
+        errs = []
+        for fn in (small_host.small_host_cond_sweep_f64, small_host.small_host_cond_sweep_direct_f64):
+            J = np.zeros((1, N))
+            st, ts = np.zeros(1, np.int32), np.zeros(1, np.int32)
+            assert fn(p(Aa), p(Ba), p(Qa), p(Ri), p(QT), p(np.ascontiguousarray(z0)), C.c_int64(1),
+                      N, s, m, T_min, T_max, p(J), p(st), p(ts)) == 0
+            errs.append(float(np.max(np.abs(J[0, win] - Jh[win]) / np.abs(Jh[win]))))
+            if len(errs) == 1:
+                assert st[0] == 0, t
+                assert int(ts[0]) == int(np.argmin(Jh[win]) + T_min), t
+        assert errs[0] <= 1e-9, (t, errs)
+        assert errs[0] <= errs[1], (t, errs)
 
 
 @pytest.mark.parametrize("tag,dt", [("s5_m1_N200", np.float64), ("s3_m1_N50", np.float64),

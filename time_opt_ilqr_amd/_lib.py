@@ -54,6 +54,11 @@ _TRJ32 = _TRJ64[:19] + [C.c_float, C.c_float]
 _AUG_TAIL = [_I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]
 _TRAJ_TAIL = [_P, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _I64,
               _P]
+# tile64 trajectory select tail: R_inv r_bs batch n_alloc n_use n m tries t_min t_max J st ts js stream
+_T64TAIL = [_P, _I64, _I64, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]
+# tile64 linearisation: system dt X U batch n_alloc n_use central epsx epsu relx relu A B a Xt Ut stream
+_LIN64 = [_I32, C.c_double, _P, _P, _I64, _I32, _I32, _I32, C.c_double, C.c_double, C.c_double,
+          C.c_double, _P, _P, _P, _P, _P, _P]
 # cost parameters of the forward-pass entries: xg bs u_ref bs Q bs R bs Qf bs w bs obs n_obs wrap
 _COST = [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _P, _I32, _U32]
 
@@ -84,6 +89,12 @@ SIGNATURES = {
     "hop_bruteforce_jcurve_f32": (C.c_int, _JC32),
     "hop_riccati_legacy_f64": (C.c_int, _RICLEG),
     "hop_bruteforce_jcurve_legacy_f64": (C.c_int, _JCLEG),
+    "hop_lft_sweep_traj_tile64_f64": (C.c_int, _TRJ64[:15] + [_U32, C.c_double, C.c_double] +
+                                      _T64TAIL),
+    "hop_lft_sweep_traj_tile64_f32": (C.c_int, _TRJ64[:15] + [_U32, C.c_float, C.c_float] +
+                                      _T64TAIL),
+    "hop_linearize_tile64_f64": (C.c_int, _LIN64),
+    "hop_linearize_tile64_f32": (C.c_int, _LIN64),
     "hop_system_dims": (C.c_int, [_I32, _P, _P]),
     "hop_linearize_f64": (C.c_int, [_I32, C.c_double, _P, _P, _I64, _I32, _I32, _I32,
                                     C.c_double, C.c_double, C.c_double, C.c_double, _P, _P, _P,

@@ -91,6 +91,10 @@ int lft_entry(const T* A, const T* B, const T* Q, const T* R, int64_t r_bs, int6
     if (dbg_efg || dbg_pre) return fail(HOP_E_ARG, "tile64 layout: no debug outputs");
     if (r_ks != 0) return fail(HOP_E_ARG, "tile64 layout: no per-step R");
     a.tile64 = 1;
+    if (traj) {  // raw linearisation in tile64 (hop_lft_sweep_traj_tile64_*)
+      a.traj = 1;
+      a.tr = *traj;
+    }
     const hipError_t e = hop::dispatch_lft_small<T>(a, (hipStream_t)stream);
     if (e != hipErrorNotSupported) return hip_status(e);
     return fail(HOP_E_SIZE, "tile64 layout: no small-s kernel for this (s, m, dtype)");
@@ -282,9 +286,8 @@ bool traj_fused(int32_t n, int32_t m, int32_t elem_bytes, bool has_extra) {
   if (hop::opt(HOP_OPT_FORCE_GENERIC | HOP_OPT_TRAJ_UNFUSED) || has_extra) return false;
   if (elem_bytes == 8 && n == 12 && m == 4) return true;
   const int s = n + 1;
-  const bool both = (s == 2 && m == 1) || (s == 3 && m == 1) || (s == 4 && (m == 1 || m == 2));
-  if (elem_bytes == 8) return both;
-  return both || (s == 5 && (m == 1 || m == 2));
+  return (s == 2 && m == 1) || (s == 3 && m == 1) || (s == 4 && (m == 1 || m == 2)) ||
+         (s == 5 && (m == 1 || m == 2));
 }
 
 constexpr int64_t kWsAlign = 256;
@@ -584,6 +587,59 @@ int hop_lft_sweep_traj_f32(const float* A, const float* Bm, const float* a_res, 
       workspace, workspace_bytes, stream);
 }
 
+extern "C++" {
+template <class T>
+int traj_tile64_entry(const hop::TrajArgs<T>& t, const T* R_inv, int64_t r_bs, int64_t batch,
+                      int32_t n_alloc, int32_t n_use, int32_t max_tries, int32_t t_min,
+                      int32_t t_max, T* J, int32_t* status, int32_t* t_star, T* j_star,
+                      void* stream) {
+  int rc = traj_check(t, batch, n_alloc, n_use);
+  if (rc != HOP_OK) return rc;
+  if (n_use <= 0 || batch == 0) return HOP_OK;
+  if (!R_inv) return fail(HOP_E_ARG, "null R_inv");
+  if (r_bs < 0) return fail(HOP_E_ARG, "negative stride");
+  const int32_t s = t.n + 1;
+  const bool shape = (s == 2 && t.m == 1) || (s == 3 && t.m == 1) ||
+                     (s == 4 && (t.m == 1 || t.m == 2)) || (s == 5 && (t.m == 1 || t.m == 2));
+  if (!shape) return fail(HOP_E_SIZE, "tile64 trajectory form: no small-s kernel for this shape");
+  return lft_entry<T>(nullptr, nullptr, nullptr, R_inv, r_bs, 0, 1, nullptr, nullptr, 0, batch,
+                      n_alloc, n_use, s, t.m, max_tries, t_min, t_max, J, status, t_star, j_star,
+                      nullptr, nullptr, stream, &t, true);
+}
+}  // extern "C++"
+
+int hop_lft_sweep_traj_tile64_f64(const double* A, const double* Bm, const double* a_res,
+                                  const double* X, const double* U, const double* xg,
+                                  int64_t xg_bs, const double* u_ref, int64_t ur_bs,
+                                  const double* Q, int64_t q_bs, const double* P, int64_t p_bs,
+                                  const double* w, int64_t w_bs, uint32_t wrap_mask, double q_reg,
+                                  double rho_reg, const double* R_inv, int64_t r_bs,
+                                  int64_t batch, int32_t n_alloc, int32_t n_use, int32_t n,
+                                  int32_t m, int32_t max_tries, int32_t t_min, int32_t t_max,
+                                  double* J, int32_t* status, int32_t* t_star, double* j_star,
+                                  void* stream) {
+  return traj_tile64_entry<double>(
+      traj_args<double>(A, Bm, a_res, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, P, p_bs, w, w_bs,
+                        nullptr, nullptr, nullptr, wrap_mask, q_reg, rho_reg, n, m),
+      R_inv, r_bs, batch, n_alloc, n_use, max_tries, t_min, t_max, J, status, t_star, j_star,
+      stream);
+}
+int hop_lft_sweep_traj_tile64_f32(const float* A, const float* Bm, const float* a_res,
+                                  const float* X, const float* U, const float* xg, int64_t xg_bs,
+                                  const float* u_ref, int64_t ur_bs, const float* Q, int64_t q_bs,
+                                  const float* P, int64_t p_bs, const float* w, int64_t w_bs,
+                                  uint32_t wrap_mask, float q_reg, float rho_reg,
+                                  const float* R_inv, int64_t r_bs, int64_t batch,
+                                  int32_t n_alloc, int32_t n_use, int32_t n, int32_t m,
+                                  int32_t max_tries, int32_t t_min, int32_t t_max, float* J,
+                                  int32_t* status, int32_t* t_star, float* j_star, void* stream) {
+  return traj_tile64_entry<float>(
+      traj_args<float>(A, Bm, a_res, X, U, xg, xg_bs, u_ref, ur_bs, Q, q_bs, P, p_bs, w, w_bs,
+                       nullptr, nullptr, nullptr, wrap_mask, q_reg, rho_reg, n, m),
+      R_inv, r_bs, batch, n_alloc, n_use, max_tries, t_min, t_max, J, status, t_star, j_star,
+      stream);
+}
+
 int hop_system_dims(int32_t system, int32_t* n, int32_t* m) {
   if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
   if (n) *n = hop::dyn::state_dim(system);
@@ -609,6 +665,42 @@ int hop_linearize_f64(int32_t system, double dt, const double* X, const double* 
   a.X = X; a.U = U; a.batch = batch; a.nalloc = n_alloc; a.nuse = n_use;
   a.A = A; a.B = Bm; a.a_res = a_res; a.Fx = Fx;
   return hip_status(hop::dispatch_linearize(a, (hipStream_t)stream));
+}
+
+static int linearize_tile64(int32_t system, double dt, const double* X, const double* U,
+                            int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                            double epsx, double epsu, double relx, double relu, void* A, void* Bm,
+                            void* a_res, void* Xt, void* Ut, int f32, void* stream) {
+  if (system < 0 || system >= hop::dyn::kNumSystems) return fail(HOP_E_ARG, "unknown system id");
+  if (batch < 0) return fail(HOP_E_ARG, "batch < 0");
+  if (n_use > n_alloc) return fail(HOP_E_ARG, "n_use > n_alloc");
+  if (central != 0 && central != 1) return fail(HOP_E_ARG, "central must be 0 or 1");
+  if (batch == 0 || n_use <= 0) return HOP_OK;
+  if (!X || !U || !A || !Bm || !Xt || !Ut) return fail(HOP_E_ARG, "null input/output pointer");
+  if ((batch + 63) / 64 * (int64_t)n_use > (int64_t)0xffffffffLL)
+    return fail(HOP_E_SIZE, "batch * n_use too large for one launch");
+  hop::LinArgs a{};
+  a.sys = system; a.central = central; a.dt = dt;
+  a.epsx = epsx; a.epsu = epsu; a.relx = relx; a.relu = relu;
+  a.X = X; a.U = U; a.batch = batch; a.nalloc = n_alloc; a.nuse = n_use;
+  a.A = A; a.B = Bm; a.a_res = a_res; a.Fx = nullptr;
+  a.tile64 = 1; a.out_f32 = f32; a.Xt = Xt; a.Ut = Ut;
+  return hip_status(hop::dispatch_linearize(a, (hipStream_t)stream));
+}
+
+int hop_linearize_tile64_f64(int32_t system, double dt, const double* X, const double* U,
+                             int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                             double epsx, double epsu, double relx, double relu, double* A,
+                             double* Bm, double* a_res, double* Xt, double* Ut, void* stream) {
+  return linearize_tile64(system, dt, X, U, batch, n_alloc, n_use, central, epsx, epsu, relx,
+                          relu, A, Bm, a_res, Xt, Ut, 0, stream);
+}
+int hop_linearize_tile64_f32(int32_t system, double dt, const double* X, const double* U,
+                             int64_t batch, int32_t n_alloc, int32_t n_use, int32_t central,
+                             double epsx, double epsu, double relx, double relu, float* A,
+                             float* Bm, float* a_res, float* Xt, float* Ut, void* stream) {
+  return linearize_tile64(system, dt, X, U, batch, n_alloc, n_use, central, epsx, epsu, relx,
+                          relu, A, Bm, a_res, Xt, Ut, 1, stream);
 }
 
 int hop_dynamics_f64(int32_t system, double dt, const double* X, int64_t x_stride,

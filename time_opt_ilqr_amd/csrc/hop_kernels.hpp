@@ -162,10 +162,14 @@ struct LinArgs {
   const double* U;      // [B][nalloc][m]
   long long batch;
   int nalloc, nuse;
-  double* A;            // [B][nalloc][n][n]
-  double* B;            // [B][nalloc][n][m]
-  double* a_res;        // [B][nalloc][n] or null
-  double* Fx;           // [B][nalloc][n] or null
+  void* A;              // [B][nalloc][n][n]  (tile64: [B/64][nalloc][n n][64] of OT)
+  void* B;              // [B][nalloc][n][m]  (tile64: [B/64][nalloc][n m][64])
+  void* a_res;          // [B][nalloc][n] or null (tile64: [B/64][nalloc][n][64])
+  double* Fx;           // [B][nalloc][n] or null (batch-major only)
+  int tile64 = 0;       // 1: tile64 outputs of A, B, a_res + the Xt / Ut copies
+  int out_f32 = 0;      // tile64 outputs as fp32 (computed in fp64)
+  void* Xt = nullptr;   // [B/64][nalloc+1][n][64]  x_k, k <= nuse
+  void* Ut = nullptr;   // [B/64][nalloc][m][64]    u_k, k < nuse
 };
 
 // batched dynamics step x' = F(x, u) (row strides in elements)

@@ -230,7 +230,7 @@ struct SchedCondTrajF : SchedCondTraj {
 };
 // lft_cond_cf_kernel with the round-3 query: the elimination of Sigma_eps + X_t with
 // X_t's 1/sigma ~ 1e9 rank-1 part formed (A/B, developer variant 97); the default
-// takes the rank-1 part by Sherman-Morrison (ElimQ2)
+// eliminates the congruent W^-T Sigma_eps W^-1 + diag(Pi, 1/sigma) instead
 struct SchedCondTrajG : SchedCondTraj {
   static constexpr int GJQ = 1;
 };
@@ -2271,7 +2271,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   static_for<S>([&](auto I) { X[I] = (c == S) ? (I == NN ? 1.0 : 0.0) : sel_lane<I>(0.0, eps); });
   X[S] = 0.0;
   const double e_s = (c == S) ? 1.0 : 0.0;
-  const double e_s1 = (c == S + 1) ? 1.0 : 0.0;  // the query's u border (ElimQ2)
+  const double e_nn = (c == NN) ? 1.0 : 0.0;  // the query's 1/sigma entry
   const double m1 = (c == NN) ? -1.0 : 0.0;  // lane NN of v' / u'
 
   double best = 0.0, jprev = 0.0;
@@ -2374,11 +2374,13 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       bad = bad || !(sig > 0.0);
       flag(!(sig > 0.0), 8, k + 1);
       double rq[S];
+      if constexpr (has_gjq<C>()) {
 #pragma unroll
-      for (int i = 0; i < NN; ++i) rq[i] = X[i] + Pi[i];
-      rq[NN] = X[NN];
+        for (int i = 0; i < NN; ++i) rq[i] = X[i] + Pi[i];
+        rq[NN] = X[NN];
+      }
       double q;
-      if constexpr (has_gjq<C>()) {  // round 3: eliminate A + u u^T / sigma itself
+      if constexpr (has_gjq<C>()) {  // round 3: eliminate Sigma_eps + X_t itself
         const double wq = u * recip_nr(sig);
         LaneB<S>::fma(rq, wq, u);
         double acc = 0.0, dmin = 1.0;
@@ -2387,19 +2389,27 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
         bad = bad || !(dmin > 0.0) || (q != q);
         flag(!(dmin > 0.0) || (q != q), 16, k + 1);
       } else {
-        // m^T (A + u u^T / sigma)^-1 m = a - b^2 / (sigma + c) with A = Sigma_eps +
-        // Pi_ext and a, b, c = m^T A^-1 m, m^T A^-1 u, u^T A^-1 u from ONE bordered
-        // elimination of [A | m u] (u rides on lane S + 1): A's pivots stay O(|A|)
-        // while the 1/sigma ~ 1e9 entries of the round-3 form cancelled in them
-        // (measured false hand-overs on real quadrotor linearisations)
-        LaneB<S>::fma(rq, u, e_s1);  // lane S + 1 of row i: u_i
-        double acc = 0.0, accx = 0.0, dmin = 1.0;
-        ElimQ2<S>::run(rq, acc, accx, dmin);
-        const double qa = bcast<S>(acc), qc = bcast<S + 1>(acc), qb = bcast<S + 1>(accx);
-        const double den = sig + qc;
-        q = qa - qb * qb * recip_nr(den);
-        bad = bad || !(dmin > 0.0) || !(den > 0.0) || (q != q);
-        flag(!(dmin > 0.0) || !(den > 0.0) || (q != q), 16, k + 1);
+        // X_t = W^T D W with D = diag(Pi, 1/sigma), W = [[I, 0], [-u^T, 1]] (u here the
+        // first NN lanes of u), so m^T (Sigma_eps + X_t)^-1 m = m~^T (Sigma~ + D)^-1 m~
+        // with Sigma~ = W^-T Sigma_eps W^-1, m~ = W^-T m, W^-1 = I + e_NN [u; 0]^T.  The
+        // 1/sigma ~ 1e9 of the terminal block then sits alone on the last diagonal
+        // entry: no pivot cancels it (the round-3 form, eliminating Sigma_eps + X_t,
+        // lost 1e-7 .. 1e-5 of q on real quadrotor linearisations and handed problems
+        // the reference solves cleanly to the rerun; this form holds ~1e-16, measured
+        // against exact rational arithmetic)
+        const double ub = in ? e1 - eps * z : 0.0;
+#pragma unroll
+        for (int i = 0; i < S; ++i) rq[i] = X[i];
+        RowB<S>::template sweep<NN>(rq, ub);  // Sigma W^-1: row i += Sigma_i,NN [u; 0]
+        LaneB<NN>::fma(reinterpret_cast<double (&)[NN]>(rq), ub, rq[NN]);  // W^-T (.): + u_i row NN
+#pragma unroll
+        for (int i = 0; i < NN; ++i) rq[i] += Pi[i];
+        rq[NN] = __builtin_fma(e_nn, recip_nr(sig), rq[NN]);  // D's 1/sigma
+        double acc = 0.0, dmin = 1.0;
+        ElimQ<S>::run(rq, acc, dmin, 0.0);
+        q = bcast<S>(acc);
+        bad = bad || !(dmin > 0.0) || (q != q);
+        flag(!(dmin > 0.0) || (q != q), 16, k + 1);
       }
       const double gam = bcast<S>(X[S]);
       jk = 0.5 * (q - gam);

@@ -35,7 +35,12 @@ constexpr int TILE = 64;
 // quadrotor at B = 4096, N = 100 (tools/ab_libs.py, same process, bitwise equal)
 #define HOP_LIN_STORE(v, p) __builtin_nontemporal_store((v), (p))
 
-template <int SYS, bool CEN>
+// LY 0: one workgroup per 64 consecutive (problem, step) pairs, fp64 batch-major
+// outputs.  LY 2: one workgroup per (64-problem tile, step k), outputs of type OT in
+// the tile64 layout [B/64][n_alloc][elems][64] (include/hop.h), plus the tile64
+// copies of x_k (and x_{n_use} for k = n_use - 1) and u_k the trajectory-form
+// select reads (hop_lft_sweep_traj_tile64_*): every store is 64 consecutive slots.
+template <int SYS, bool CEN, class OT = double, int LY = 0>
 __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
   constexpr int n = state_dim(SYS), m = control_dim(SYS), NC = n + m;
   constexpr int TS = trig_slots(SYS, CEN) > 0 ? trig_slots(SYS, CEN) : 1;
@@ -47,13 +52,27 @@ __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
   const int tid = threadIdx.x;
   const long long total = a.batch * (long long)a.nuse;
   const long long g0 = (long long)blockIdx.x * TILE;
+  // LY 2: tile blk, step kt; slot ls of element e at ((blk * nal + kt) * E + e) * 64 + ls
+  const long long blk = LY == 2 ? (long long)blockIdx.x / a.nuse : 0;
+  const int kt = LY == 2 ? (int)((long long)blockIdx.x - blk * a.nuse) : 0;
+  auto t64 = [&](long long nal, int E, int e, int ls) {
+    return ((blk * nal + kt) * E + e) * 64 + ls;
+  };
   if (tid < TILE) {
-    const long long g = g0 + tid;
     long long r = -1, xr = 0;
-    if (g < total) {
-      const long long b = g / a.nuse, k = g - b * a.nuse;
-      r = b * a.nalloc + k;
-      xr = r + b;
+    if constexpr (LY == 2) {
+      const long long b = blk * TILE + tid;
+      if (b < a.batch) {
+        r = b * a.nalloc + kt;
+        xr = r + b;
+      }
+    } else {
+      const long long g = g0 + tid;
+      if (g < total) {
+        const long long b = g / a.nuse, k = g - b * a.nuse;
+        r = b * a.nalloc + k;
+        xr = r + b;
+      }
     }
     srow[tid] = r;
     sxrow[tid] = xr;
@@ -68,6 +87,21 @@ __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
     su[e] = srow[ls] >= 0 ? a.U[srow[ls] * m + i] : 0.0;
   }
   __syncthreads();
+  if constexpr (LY == 2) {  // the tile64 copies of x_k (x_{n_use} too) and u_k; padding slots 0
+    OT* Xt = reinterpret_cast<OT*>(a.Xt);
+    OT* Ut = reinterpret_cast<OT*>(a.Ut);
+    for (int e = tid; e < TILE * n; e += TPB) {
+      const int i = e / TILE, ls = e - i * TILE;
+      HOP_LIN_STORE((OT)sx[ls * n + i], Xt + t64(a.nalloc + 1, n, i, ls));
+      if (kt == a.nuse - 1)
+        HOP_LIN_STORE(srow[ls] >= 0 ? (OT)a.X[(sxrow[ls] + 1) * n + i] : OT(0),
+                      Xt + t64(a.nalloc + 1, n, i, ls) + 64 * n);
+    }
+    for (int e = tid; e < TILE * m; e += TPB) {
+      const int i = e / TILE, ls = e - i * TILE;
+      HOP_LIN_STORE((OT)su[ls * m + i], Ut + t64(a.nalloc, m, i, ls));
+    }
+  }
   if constexpr (NJOB > 0) {
     for (int q = tid; q < TILE * NJOB; q += TPB) {
       const int ls = q % TILE, job = q / TILE;
@@ -94,19 +128,43 @@ __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
     sfin[tid] = fin;
   }
   __syncthreads();
-  if (a.a_res || a.Fx) {
+  if constexpr (LY == 2) {
+    OT* at = reinterpret_cast<OT*>(a.a_res);
+    if (at) {
+      for (int e = tid; e < TILE * n; e += TPB) {
+        const int i = e / TILE, ls = e - i * TILE;
+        const long long r = srow[ls];
+        const double v = r >= 0 ? sf[ls * n + i] - a.X[(sxrow[ls] + 1) * n + i] : 0.0;
+        HOP_LIN_STORE((OT)v, at + t64(a.nalloc, n, i, ls));
+      }
+    }
+  } else if (a.a_res || a.Fx) {
     for (int e = tid; e < TILE * n; e += TPB) {
       const int ls = e / n, i = e - ls * n;
       const long long r = srow[ls];
       if (r < 0) continue;
-      if (a.a_res) HOP_LIN_STORE(sf[e] - a.X[(sxrow[ls] + 1) * n + i], a.a_res + r * n + i);
+      if (a.a_res)
+        HOP_LIN_STORE(sf[e] - a.X[(sxrow[ls] + 1) * n + i],
+                      reinterpret_cast<double*>(a.a_res) + r * n + i);
       if (a.Fx) HOP_LIN_STORE(sf[e], a.Fx + r * n + i);
     }
   }
-  // phase 3: one (step, column) per thread
+  // phase 3: one (step, column) per thread (LY 2: a wave = one column of 64 slots)
   for (int it = tid; it < TILE * NC; it += TPB) {
-    const int ls = it / NC, j = it - ls * NC;
+    const int ls = LY == 2 ? it % TILE : it / NC, j = LY == 2 ? it / TILE : it - ls * NC;
     const long long r = srow[ls];
+    if constexpr (LY == 2) {
+      if (r < 0) {  // padding slot: zeros
+        OT* At = reinterpret_cast<OT*>(a.A);
+        OT* Bt = reinterpret_cast<OT*>(a.B);
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+          if (j < n) HOP_LIN_STORE(OT(0), At + t64(a.nalloc, n * n, i * n + j, ls));
+          else HOP_LIN_STORE(OT(0), Bt + t64(a.nalloc, n * m, i * m + (j - n), ls));
+        }
+        continue;
+      }
+    }
     if (r < 0) continue;
     double x[n], u[m], f0[n], col[n];
 #pragma unroll
@@ -115,12 +173,20 @@ __global__ __launch_bounds__(TPB) void linearize_kernel(LinArgs a) {
     for (int i = 0; i < m; ++i) u[i] = su[ls * m + i];
     fd_col<SYS, CEN>(x, u, f0, sfin[ls] != 0, st + ls * TS, a.dt, j, a.epsx, a.epsu, a.relx,
                      a.relu, col);
-    if (j < n) {
-      double* Ak = a.A + r * (n * n) + j;
+    if constexpr (LY == 2) {
+      OT* At = reinterpret_cast<OT*>(a.A);
+      OT* Bt = reinterpret_cast<OT*>(a.B);
+#pragma unroll
+      for (int i = 0; i < n; ++i) {
+        if (j < n) HOP_LIN_STORE((OT)col[i], At + t64(a.nalloc, n * n, i * n + j, ls));
+        else HOP_LIN_STORE((OT)col[i], Bt + t64(a.nalloc, n * m, i * m + (j - n), ls));
+      }
+    } else if (j < n) {
+      double* Ak = reinterpret_cast<double*>(a.A) + r * (n * n) + j;
 #pragma unroll
       for (int i = 0; i < n; ++i) HOP_LIN_STORE(col[i], Ak + i * n);
     } else {
-      double* Bk = a.B + r * (n * m) + (j - n);
+      double* Bk = reinterpret_cast<double*>(a.B) + r * (n * m) + (j - n);
 #pragma unroll
       for (int i = 0; i < n; ++i) HOP_LIN_STORE(col[i], Bk + i * m);
     }
@@ -145,6 +211,16 @@ __global__ __launch_bounds__(TPB) void dynamics_kernel(DynArgs a) {
 
 template <int SYS, bool CEN>
 hipError_t launch_lin(const LinArgs& a, hipStream_t stream) {
+  if (a.tile64) {  // one workgroup per (64-problem tile, step)
+    const long long blocks = (a.batch + TILE - 1) / TILE * (long long)a.nuse;
+    if (a.out_f32)
+      hipLaunchKernelGGL((linearize_kernel<SYS, CEN, float, 2>), dim3((unsigned)blocks),
+                         dim3(TPB), 0, stream, a);
+    else
+      hipLaunchKernelGGL((linearize_kernel<SYS, CEN, double, 2>), dim3((unsigned)blocks),
+                         dim3(TPB), 0, stream, a);
+    return hipGetLastError();
+  }
   const long long total = a.batch * (long long)a.nuse;
   const long long blocks = (total + TILE - 1) / TILE;
   hipLaunchKernelGGL((linearize_kernel<SYS, CEN>), dim3((unsigned)blocks), dim3(TPB), 0, stream,

@@ -52,7 +52,7 @@ static void run(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, 
 
 // conditioned-prefix path (lft_small.hip COND kernels): status = 16 when the
 // problem would be handed to the rerun launch
-template <class T, int S, int MM>
+template <class T, int S, int MM, bool DIRECT = false>
 static void run_cond(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, const T* z0,
                      int64_t batch, int n, int t_min, int t_max, T* J, int32_t* status,
                      int32_t* t_star) {
@@ -79,7 +79,7 @@ static void run_cond(const T* A, const T* B, const T* Q, const T* Rinv, const T*
       sym_of(E, Qk);
       cs.bad = cs.bad || !spd_inverse_once(E);
       cond_step<T, S, MM>(cs, E, Ak, Bk, rinv);
-      const T jk = cond_query<T, S, MM>(cs, QTk);
+      const T jk = DIRECT ? cond_query_direct<T, S, MM>(cs, QTk) : cond_query<T, S, MM>(cs, QTk);
       J[b * n + k] = jk;
       take(cs, k + 1, jk, t_min, t_max);
     }
@@ -94,6 +94,18 @@ extern "C" int small_host_cond_sweep_f64(const double* A, const double* B, const
                                          double* J, int32_t* status, int32_t* t_star) {
   if (s == 3 && m == 1) run_cond<double, 3, 1>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
   else if (s == 5 && m == 1) run_cond<double, 5, 1>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
+  else return -1;
+  return 0;
+}
+
+// the round-3 query (cond_query_direct), for the accuracy comparison
+extern "C" int small_host_cond_sweep_direct_f64(const double* A, const double* B, const double* Q,
+                                                const double* Rinv, const double* QT,
+                                                const double* z0, int64_t batch, int n, int s,
+                                                int m, int t_min, int t_max, double* J,
+                                                int32_t* status, int32_t* t_star) {
+  if (s == 3 && m == 1) run_cond<double, 3, 1, true>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
+  else if (s == 5 && m == 1) run_cond<double, 5, 1, true>(A, B, Q, Rinv, QT, z0, batch, n, t_min, t_max, J, status, t_star);
   else return -1;
   return 0;
 }

@@ -449,9 +449,89 @@ HOP_HD inline void cond_step(CondState<T, S, MM>& c, const Sym<T, S>& E, const G
   }
 }
 
-// J of horizon k+1: 1/2 (m^T (Sigma_eps + X_t)^-1 m - gamma), X_t = (QT_k + eps I)^-1
+// J of horizon k+1: 1/2 (m^T (Sigma_eps + X_t)^-1 m - gamma), X_t = (QT_k + eps I)^-1.
+// QT_k + eps I = [[P11, b], [b^T, cc]] is swept on its first S - 1 pivots only, which
+// leaves P11^-1, u = P11^-1 b and sigma = cc - b^T P11^-1 b (the potrf test of QT_k +
+// eps I is then: those pivots and sigma > 0).  With W = [[I, 0], [-u^T, 1]] and
+// D = diag(P11^-1, 1/sigma), X_t = W^T D W, so
+//   m^T (Sigma_eps + X_t)^-1 m = m~^T (W^-T Sigma_eps W^-1 + D)^-1 m~,  m~ = W^-T m,
+// W^-1 = I + e_{S-1} [u; 0]^T.  The augmented terminal block's rho_reg = 1e-12 makes
+// sigma ~ 1e-9: its 1/sigma then sits alone on the last diagonal entry, where no
+// pivot cancels it.  Eliminating Sigma_eps + X_t itself (cond_query_direct) loses
+// 1e-7 .. 1e-5 of q on real linearisations; this form holds ~1e-15 (tests/
+// test_host_cpu.py against the 50-digit curves of tests/golden/real_lin_hp.npz).
 template <class T, int S, int MM>
 HOP_HD inline T cond_query(CondState<T, S, MM>& c, const Gen<T, S>& QT) {
+  constexpr int NN = S - 1;
+  Sym<T, S> x;
+  sym_of(x, QT);
+#pragma unroll
+  for (int i = 0; i < S; ++i) x.at(i, i) += T(1e-9);
+  // symmetric sweep of pivots 0 .. NN-1: x = [[-P11^-1, u], [u^T, sigma]]
+#pragma unroll
+  for (int p = 0; p < NN; ++p) {
+    const T d = x.at(p, p);
+    c.bad = c.bad || !(d > T(0));
+    const T r = small_recip(d);
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      if (i == p) continue;
+      const T aip = x.at(i, p) * r;
+#pragma unroll
+      for (int j = i; j < S; ++j) {
+        if (j == p) continue;
+        x.at(i, j) -= aip * x.at(p, j);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (i != p) x.at(i, p) *= r;
+    x.at(p, p) = -r;
+  }
+  const T sig = x.at(NN, NN);
+  c.bad = c.bad || !(sig > T(0));
+  T u[NN];
+#pragma unroll
+  for (int i = 0; i < NN; ++i) u[i] = x.at(i, NN);
+  // y = W^-T Sigma_eps W^-1 + D, b = W^-T m
+  const Sym<T, S>& Sg = c.Sg;
+  Sym<T, S> y;
+  T b[S];
+  const T snn = Sg.at(NN, NN);
+#pragma unroll
+  for (int i = 0; i < NN; ++i) {
+    const T sin_ = Sg.at(i, NN) + u[i] * snn;  // row i of Sigma W^-1 at column NN, then W^-T
+#pragma unroll
+    for (int j = i; j < NN; ++j)
+      y.at(i, j) = (Sg.at(i, j) + u[j] * Sg.at(i, NN)) + u[i] * (Sg.at(NN, j) + u[j] * snn) -
+                   x.at(i, j);  // + P11^-1
+    y.at(i, NN) = sin_;
+    b[i] = c.m[i] + u[i] * c.m[NN];
+  }
+  y.at(NN, NN) = snn + small_recip(sig);
+  b[NN] = c.m[NN];
+  T acc = T(0);
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    const T d = y.at(p, p);
+    c.bad = c.bad || !(d > T(0));
+    const T r = small_recip(d);
+    acc += b[p] * b[p] * r;
+#pragma unroll
+    for (int i = p + 1; i < S; ++i) {
+      const T l = y.at(p, i) * r;
+      b[i] -= l * b[p];
+#pragma unroll
+      for (int j = i; j < S; ++j) y.at(i, j) -= l * y.at(p, j);
+    }
+  }
+  return T(0.5) * (acc - c.gam);
+}
+
+// round 3's query: eliminate Sigma_eps + X_t with X_t formed by a full sweep
+// (kept for the host comparison in tests/test_host_cpu.py)
+template <class T, int S, int MM>
+HOP_HD inline T cond_query_direct(CondState<T, S, MM>& c, const Gen<T, S>& QT) {
   Sym<T, S> x;
   sym_of(x, QT);
   c.bad = c.bad || !spd_inverse_once(x);

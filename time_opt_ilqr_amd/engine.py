@@ -602,6 +602,11 @@ def propagate_traj(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, *, wrap_idx=No
     and never written to HBM; otherwise they go through a workspace.
     """
     torch = _torch()
+    if isinstance(A, Tile64):
+        if any(t is not None for t in (qxx_extra, qx_extra, c_extra)):
+            raise ValueError("tile64 trajectory form: no extra_stage_cost")
+        return _propagate_traj_tile64(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, wrap_idx,
+                                      n_use, t_min, t_max, max_tries, q_reg, rho_reg)
     args, (Bn, N, n, m, dt, dev, has_extra), keep = _traj_args(
         A, Bm, a_res, X, U, xg, u_ref, Q, P, w, wrap_idx, q_reg, rho_reg, qxx_extra, qx_extra,
         c_extra)
@@ -638,6 +643,53 @@ def propagate_traj(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, *, wrap_idx=No
     return SweepResult(J, status, ts, js)
 
 
+def _propagate_traj_tile64(A, Bm, a_res, X, U, xg, u_ref, Q, R_inv, P, w, wrap_idx, n_use,
+                           t_min, t_max, max_tries, q_reg, rho_reg) -> SweepResult:
+    """propagate_traj on the raw linearisation in the tile64 layout (every one of A,
+    Bm, a_res, X, U a Tile64, as linearize(..., tile64=True) returns them):
+    hop_lft_sweep_traj_tile64_*, small-s shapes."""
+    torch = _torch()
+    for name, t in (("A", A), ("Bm", Bm), ("a_res", a_res), ("X", X), ("U", U)):
+        if not isinstance(t, Tile64):
+            raise TypeError(f"{name}: the tile64 trajectory form needs every raw array as Tile64")
+    Bn, N, n, _ = A.shape
+    m = Bm.cols
+    dt, dev = A.dtype, A.device
+    for name, t, steps, r, c in (("A", A, N, n, n), ("Bm", Bm, N, n, m), ("a_res", a_res, N, n, 1),
+                                 ("X", X, N + 1, n, 1), ("U", U, N, m, 1)):
+        t.check(name)
+        if t.batch != Bn or t.shape[1] != steps or t.rows * t.cols != r * c or t.dtype != dt \
+                or t.device != dev:
+            raise ValueError(f"{name}: tile64 {t.shape} does not match A {A.shape}")
+    xg, u_ref, Q, P = (_dev(v, nm, dt, dev) for v, nm in ((xg, "xg"), (u_ref, "u_ref"), (Q, "Q"),
+                                                           (P, "P")))
+    w = _scalar_or_vec(w, dt, dev, "w")
+    if w.numel() not in (1, Bn):
+        raise ValueError("w must be a scalar or [B]")
+    R_inv = _dev(R_inv, "R_inv", dt, dev)
+    if tuple(R_inv.shape[-2:]) != (m, m):
+        raise ValueError(f"R_inv blocks must be {m}x{m}")
+    n_use = N if n_use is None else int(n_use)
+    if n_use > N:
+        raise IndexError(f"T_use={n_use} exceeds the {N} stages supplied")
+    n_eff = max(n_use, 0)
+    J = torch.empty((Bn, n_eff), dtype=dt, device=dev)
+    status = (torch.empty if n_eff > 0 else torch.zeros)((Bn,), dtype=torch.int32, device=dev)
+    fuse = t_max is not None
+    ts = torch.empty((Bn,), dtype=torch.int32, device=dev) if fuse else None
+    js = torch.empty((Bn,), dtype=dt, device=dev) if fuse else None
+    rc = _fn("hop_lft_sweep_traj_tile64", dt)(
+        _lib.ptr(A.data), _lib.ptr(Bm.data), _lib.ptr(a_res.data), _lib.ptr(X.data),
+        _lib.ptr(U.data), _lib.ptr(xg), _bstride(xg, 1, "xg", Bn), _lib.ptr(u_ref),
+        _bstride(u_ref, 1, "u_ref", Bn), _lib.ptr(Q), _bstride(Q, 2, "Q", Bn), _lib.ptr(P),
+        _bstride(P, 2, "P", Bn), _lib.ptr(w), 0 if w.numel() == 1 else 1, wrap_mask(wrap_idx, n),
+        float(q_reg), float(rho_reg), _lib.ptr(R_inv), _bstride(R_inv, 2, "R_inv", Bn), Bn, N,
+        n_use, n, m, int(max_tries), int(t_min) if fuse else 0, int(t_max) if fuse else 0,
+        _lib.ptr(J), _lib.ptr(status), _lib.ptr(ts), _lib.ptr(js), _lib.stream_handle(dev))
+    _lib.check(rc)
+    return SweepResult(J, status, ts, js)
+
+
 # ---- batched dynamics + finite-difference linearisation (SURVEY.md §8(f) rank 2)
 
 SYSTEM_IDS = {"double_integrator": 0, "di": 0, "cartpole": 1, "quadrotor": 2, "pointmass": 3,
@@ -669,16 +721,25 @@ class Linearization:
     B: "object"       # [B, N, n, m]
     a_res: "object"   # [B, N, n]  F(x_k, u_k) - x_{k+1}
     Fx: "object" = None  # [B, N, n] F(x_k, u_k) (want_fx=True)
+    X: "object" = None   # tile64=True: the trajectory's x_k (k <= n_use) as Tile64
+    U: "object" = None   # tile64=True: u_k (k < n_use) as Tile64
 
 
 def linearize(system, X, U, dt: float, *, central: bool = False, n_use: Optional[int] = None,
               epsx: float = 1e-5, epsu: float = 1e-5, relx: float = 1e-6, relu: float = 1e-6,
-              want_fx: bool = False) -> Linearization:
+              want_fx: bool = False, tile64: bool = False,
+              tile64_dtype=None) -> Linearization:
     """Batched linearize_{forward,central}_diff_traj + compute_affine_residuals
     (linearization.py:177-270) for X [B, N+1, n], U [B, N, m] (fp64, on the
     device).  Steps k < n_use (default N) are written; A / B / a_res come out in
-    the layout augment / propagate_traj / riccati read."""
+    the layout augment / propagate_traj / riccati read.
+    tile64=True: A, B, a_res and the trajectory X, U come out as Tile64 (of
+    tile64_dtype, default fp64; computed in fp64) -- the layout the small-s
+    trajectory-form select streams (propagate_traj on Tile64 inputs)."""
     torch = _torch()
+    if tile64:
+        return _linearize_tile64(system, X, U, dt, central, n_use, epsx, epsu, relx, relu,
+                                 tile64_dtype or torch.float64)
     sid = system_id(system)
     n, m = system_dims(sid)
     X = _dev(X, "X", torch.float64)
@@ -704,6 +765,36 @@ def linearize(system, X, U, dt: float, *, central: bool = False, n_use: Optional
                                        _lib.ptr(Fx), _lib.stream_handle(dev))
     _lib.check(rc)
     return Linearization(A, Bm, a_res, Fx)
+
+
+def _linearize_tile64(system, X, U, dt, central, n_use, epsx, epsu, relx, relu, odt):
+    torch = _torch()
+    sid = system_id(system)
+    n, m = system_dims(sid)
+    X = _dev(X, "X", torch.float64)
+    U = _dev(U, "U", torch.float64, X.device)
+    if X.dim() != 3 or U.dim() != 3 or X.shape[-1] != n or U.shape[-1] != m:
+        raise ValueError(f"X must be [B, N+1, {n}] and U [B, N, {m}] for system {sid}")
+    Bn, N = U.shape[0], U.shape[1]
+    if X.shape[0] != Bn or X.shape[1] != N + 1:
+        raise ValueError("X must hold N+1 states per problem (len(U) + 1)")
+    n_use = N if n_use is None else int(n_use)
+    if n_use > N:
+        raise IndexError(f"n_use={n_use} exceeds the {N} steps supplied")
+    if odt not in (torch.float64, torch.float32):
+        raise TypeError("tile64_dtype must be float64 or float32")
+    dev = X.device
+    nt = (Bn + 63) // 64
+    mk = lambda steps, e: torch.empty((nt, steps, e, 64), dtype=odt, device=dev)  # noqa: E731
+    A, Bm, ar, Xt, Ut = mk(N, n * n), mk(N, n * m), mk(N, n), mk(N + 1, n), mk(N, m)
+    fn = _lib.load().hop_linearize_tile64_f64 if odt == torch.float64 else \
+        _lib.load().hop_linearize_tile64_f32
+    rc = fn(sid, float(dt), _lib.ptr(X), _lib.ptr(U), Bn, N, n_use, int(bool(central)),
+            float(epsx), float(epsu), float(relx), float(relu), _lib.ptr(A), _lib.ptr(Bm),
+            _lib.ptr(ar), _lib.ptr(Xt), _lib.ptr(Ut), _lib.stream_handle(dev))
+    _lib.check(rc)
+    return Linearization(Tile64(A, Bn, n, n), Tile64(Bm, Bn, n, m), Tile64(ar, Bn, n, 1), None,
+                         Tile64(Xt, Bn, n, 1), Tile64(Ut, Bn, m, 1))
 
 
 def dynamics(system, X, U, dt: float):
