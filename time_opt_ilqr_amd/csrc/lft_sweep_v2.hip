@@ -122,6 +122,7 @@ struct SchedCond : SchedLdlDma {
 // + the QT image reads under the E sweep, the A/B reads under the X sweep
 struct SchedCondL : SchedCond {
   static constexpr int LDSPIPE = 1;
+  static constexpr int WQ = 1;
 };
 template <class C>
 constexpr bool has_ldspipe() {
@@ -145,6 +146,17 @@ struct SchedCondL2Stamped : SchedCondL2 {
 // the three parts of SchedCondL2 alone (developer A/B)
 struct SchedCondLSym : SchedCondL {  // the default since round 3
   static constexpr int SYM2 = 1, NEWT = 0, PEPS = 0;
+};
+// round 4: the query by congruence (the X sweep stops one pivot short; see the
+// query below): the default of SchedCondL and its descendants; WQ = 0 keeps the
+// round-3 query (developer variant 99, A/B)
+template <class C>
+constexpr bool has_wq() {
+  if constexpr (requires { C::WQ; }) return C::WQ != 0;
+  return false;
+}
+struct SchedCondLSymG : SchedCondLSym {
+  static constexpr int WQ = 0;
 };
 // the default at two waves per SIMD: packed images (Geo PACK), 2 workgroups per CU
 // (batches above one wave per SIMD)
@@ -951,10 +963,37 @@ struct Geo {
                 "raw blocks must fit the augmented image areas");
   static constexpr int OFF_VX = OFF_T + TILE_W, OFF_VA = OFF_VX + 1024 * NJX,
                        OFF_VU = OFF_VA + 1024 * NJV;
-  // raw Q of the wave's problems, transposed (lane c reads its row as a column)
+  // raw Q of the wave's problems, transposed (lane c reads its row as a column); the
+  // closed-form kernel uses the area as its S x S symmetrisation scratch
   static constexpr int OFF_CQ = OFF_VU + 1024 * NJU;
-  static constexpr int WAVE_BYTES_T = OFF_CQ + kProbPerWave * NN * NN * 8;
+  static constexpr int CQ_BYTES = kProbPerWave * 8 * (NN * NN > SS ? NN * NN : SS);
+  static constexpr int WAVE_BYTES_T = OFF_CQ + CQ_BYTES;
 };
+
+// Sigma from its upper triangle (lanes c < i of row i take Sigma[c][i]; lanes >= S,
+// m and gamma, untouched) through a wave-private S x S scratch t of this lane's
+// problem.  The conditioned update Sigma' = Sigma_eps - Sigma_eps S^-1 Sigma_eps
+// passes Sigma_eps's antisymmetric rounding through unchanged while it contracts
+// the symmetric part, so without this the antisymmetric part accumulates over the
+// horizon: on a real quadrotor linearisation (tests/golden/real_lin_hp.npz) J ends
+// 0.5 off the 50-digit value; symmetrised every 8 steps it stays within 1e-11
+// (NumPy model of the arithmetic).
+constexpr int kSymEvery = 8;
+template <int S>
+__device__ __forceinline__ void sym_from_upper(double (&X)[S], double* t, int c) {
+  if (c < S) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) t[i * S + c] = X[i];
+  }
+  wave_sync();
+  const int cr = c < S ? c : 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const double y = t[cr * S + i];
+    X[i] = c < i ? y : X[i];
+  }
+  wave_sync();
+}
 
 // per-lane DMA source offset of piece j: lane q = 64 j + lane carries chunk
 // q % CH of problem q / CH of the wave (OOB sentinel for unused lanes)
@@ -1651,6 +1690,10 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   const unsigned eps_addr = zaddr + 8u * (EPSV + 15 - c);
   constexpr double DOFF = has_sym2<C>() ? 1e-9 - 0.5 : 1e-9 - 1.0;  // image diagonal offset
   constexpr double KOFF = has_sym2<C>() ? 2.0 : 1.0;  // update / query diagonal offset
+  // the congruence query (has_wq): the ldspipe schedules on augmented images only
+  constexpr bool WQ = has_wq<C>() && has_ldspipe<C>() && !TRAJ && !MF;
+  const double kmask = c < S - 1 ? -KOFF : 0.0;     // P11^-1 - KOFF I on lanes < S-1
+  const double e_last = c == S - 1 ? 1.0 : 0.0;
   const T* imQ = reinterpret_cast<const T*>(wbase + G::OFF_Q + g * G::IMGM);
   const T* imA = reinterpret_cast<const T*>(wbase + G::OFF_A + g * G::IMGM);
   const T* imT = reinterpret_cast<const T*>(wbase + G::OFF_QT + g * G::IMGM);
@@ -1848,7 +1891,8 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       float o2[2 * S + MM];
       const unsigned ab[3] = {in ? lds_addr(imA) + 4u * S * c : zaddr, lds_addr(imA) + 4u * c,
                               in ? lds_addr(imB) + 4u * MM * c : zaddr};
-      SweepQABF<S>::run(NX, d2, o2, ab);
+      if constexpr (WQ) SweepQABFP<S>::run(NX, d2, o2, ab);  // pivots 0 .. S-2 (the query)
+      else SweepQABF<S>::run(NX, d2, o2, ab);
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
 #pragma unroll
       for (int j = 0; j < S; ++j) {
@@ -1878,7 +1922,8 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       double o2[2 * S + MM];
       const unsigned ab[3] = {in ? lds_addr(imA) + 8u * S * c : zaddr, lds_addr(imA) + 8u * c,
                               in ? lds_addr(imB) + 8u * MM * c : zaddr};
-      SweepQAB<S>::run(NX, d2, o2, ab);
+      if constexpr (WQ) SweepQABP<S>::run(NX, d2, o2, ab);  // pivots 0 .. S-2 (the query)
+      else SweepQAB<S>::run(NX, d2, o2, ab);
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
       flag(!pivots_ok(NE, d1) || !pivots_ok(NX, d2), 1, k + 1);
 #pragma unroll
@@ -1960,6 +2005,12 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
         dma_stepAB<G::OFF_A, G::OFF_B>(voM, voB, rA, rB, wlds, (unsigned)((k + 1) * SS * ES),
                                        (unsigned)((k + 1) * SM * ES));
     } else if (!dma_late) {
+      // the step's images are consumed: their area is the symmetrisation scratch
+      if constexpr (!TRAJ) {
+        if (k % kSymEvery == kSymEvery - 1)
+          sym_from_upper<S>(reinterpret_cast<double (&)[S]>(X),
+                            reinterpret_cast<double*>(wbase + G::OFF_Q) + g * S * S, c);
+      }
       wave_sync();
       if (k + 1 < N) dma_step(k + 1);
     }
@@ -2052,7 +2103,35 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     stamp(6);
     // ---- query horizon t = k + 1: [Sigma_eps + X_t - I | m] by bordered elimination
     double jk;
-    {
+    if constexpr (WQ) {
+      // QT + eps I = [[P11, b], [b^T, cc]] swept on pivots 0 .. S-2 only (offset form,
+      // x KOFF for SYM2): NX = I - P11^-1 / KOFF on rows / lanes < S-1, u = P11^-1 b
+      // on lane S-1 of those rows and on row S-1, KOFF sigma - 1 at (S-1, S-1),
+      // sigma = cc - b^T P11^-1 b.  X_t = W^T diag(P11^-1, 1/sigma) W with W = [[I, 0],
+      // [-u^T, 1]], so the query eliminates W^-T Sigma_eps W^-1 + D with m~ = W^-T m:
+      // the augmented terminal block's 1/sigma ~ 1e9 (rho_reg = 1e-12) then sits alone
+      // on the last pivot instead of cancelling in every pivot (lft_cond_cf_kernel
+      // and small_math.hpp cond_query do the same)
+      const double ub = c < S - 1 ? NX[S - 1] : 0.0;
+      const double sg = (bcast<S - 1>(NX[S - 1]) + 1.0) * (1.0 / KOFF);
+      bad = bad || !(sg > 0.0);
+      flag(!(sg > 0.0), 1, k + 1);
+      double rq[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) rq[i] = X[i];
+      RowB<S>::template sweep<S - 1>(rq, ub);  // Sigma W^-1
+      LaneB<S - 1>::fma(reinterpret_cast<double (&)[S - 1]>(rq), ub, rq[S - 1]);  // W^-T (.)
+#pragma unroll
+      for (int i = 0; i < S - 1; ++i) rq[i] = __builtin_fma(kmask, NX[i], rq[i]);  // + P11^-1 - KOFF I
+      rq[S - 1] = __builtin_fma(e_last, recip_nr(sg) - KOFF, rq[S - 1]);  // + 1/sigma - KOFF
+      double acc = 0.0, dmin = 1.0;
+      ElimQ<S>::run(rq, acc, dmin, KOFF);
+      const double q = bcast<S>(acc);
+      const double gam = bcast<S>(X[S]);
+      bad = bad || !(dmin > 0.0) || (q != q);
+      flag(!(dmin > 0.0) || (q != q), 16, k + 1);
+      jk = 0.5 * (q - gam);
+    } else {
       double rq[S];
 #pragma unroll
       for (int i = 0; i < S; ++i)
@@ -2203,6 +2282,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   // LDS as register images (row i of lane l at [i][l]; the Q / QT image areas
   // and the tile slot are free in this kernel) and re-read each step
   double* lq = reinterpret_cast<double*>(wbase + G::OFF_T);
+  double* csym = reinterpret_cast<double*>(wbase + G::OFF_CQ) + g * S * S;  // sym scratch
   double* lqi = reinterpret_cast<double*>(wbase + G::OFF_Q);
   double* lpi = reinterpret_cast<double*>(wbase + G::OFF_QT);
   static_assert(G::TILE_W >= NN * 512 && G::IMGM_W >= NN * 512, "constant images");
@@ -2338,6 +2418,8 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     }
     const double eqe1 = lane_sum<NN>(e1 * qe1);
     // ---- update: condition the prefix on stage k's cost
+    if (k % kSymEvery == kSymEvery - 1)
+      sym_from_upper<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
     {
       double Ht[S];
       copy(Ht, reinterpret_cast<double (&)[S]>(X));
@@ -2514,6 +2596,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, a);
 #ifdef HOP_DEV
   switch (variant) {
+    case 99:  // the round-3 query (the full X sweep, Sigma_eps + X_t eliminated) + rerun
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymG, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
     case 42:  // stamps of the default (tools/stamps.py --cond), no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
     case 59:  // stamps of the round-2 default (halved sums), no rerun
