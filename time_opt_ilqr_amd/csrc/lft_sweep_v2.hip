@@ -2116,13 +2116,14 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       const double sg = (bcast<S - 1>(NX[S - 1]) + 1.0) * (1.0 / KOFF);
       bad = bad || !(sg > 0.0);
       flag(!(sg > 0.0), 1, k + 1);
+      // P = diag(P11^-1 - KOFF I, 0) has a zero last row and column, so W^-T P W^-1 = P:
+      // it is added before the congruence (no copy of Sigma's rows needed)
       double rq[S];
 #pragma unroll
-      for (int i = 0; i < S; ++i) rq[i] = X[i];
-      RowB<S>::template sweep<S - 1>(rq, ub);  // Sigma W^-1
+      for (int i = 0; i < S - 1; ++i) rq[i] = __builtin_fma(kmask, NX[i], X[i]);
+      rq[S - 1] = X[S - 1];
+      RowB<S>::template sweep<S - 1>(rq, ub);  // (.) W^-1
       LaneB<S - 1>::fma(reinterpret_cast<double (&)[S - 1]>(rq), ub, rq[S - 1]);  // W^-T (.)
-#pragma unroll
-      for (int i = 0; i < S - 1; ++i) rq[i] = __builtin_fma(kmask, NX[i], rq[i]);  // + P11^-1 - KOFF I
       rq[S - 1] = __builtin_fma(e_last, recip_nr(sg) - KOFF, rq[S - 1]);  // + 1/sigma - KOFF
       double acc = 0.0, dmin = 1.0;
       ElimQ<S>::run(rq, acc, dmin, KOFF);
@@ -2479,13 +2480,14 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
         // lost 1e-7 .. 1e-5 of q on real quadrotor linearisations and handed problems
         // the reference solves cleanly to the rerun; this form holds ~1e-16, measured
         // against exact rational arithmetic)
+        // Pi_ext has a zero last row and column: W^-T Pi_ext W^-1 = Pi_ext, so it is
+        // added before the congruence
         const double ub = in ? e1 - eps * z : 0.0;
 #pragma unroll
-        for (int i = 0; i < S; ++i) rq[i] = X[i];
-        RowB<S>::template sweep<NN>(rq, ub);  // Sigma W^-1: row i += Sigma_i,NN [u; 0]
+        for (int i = 0; i < NN; ++i) rq[i] = X[i] + Pi[i];
+        rq[NN] = X[NN];
+        RowB<S>::template sweep<NN>(rq, ub);  // (.) W^-1: row i += (.)_i,NN [u; 0]
         LaneB<NN>::fma(reinterpret_cast<double (&)[NN]>(rq), ub, rq[NN]);  // W^-T (.): + u_i row NN
-#pragma unroll
-        for (int i = 0; i < NN; ++i) rq[i] += Pi[i];
         rq[NN] = __builtin_fma(e_nn, recip_nr(sig), rq[NN]);  // D's 1/sigma
         double acc = 0.0, dmin = 1.0;
         ElimQ<S>::run(rq, acc, dmin, 0.0);
