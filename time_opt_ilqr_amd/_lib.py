@@ -138,6 +138,8 @@ def load(path: str | None = None):
         import torch  # noqa: F401
         lib = C.CDLL(p)
         for name, (res, args) in SIGNATURES.items():
+            if path is not None and not hasattr(lib, name):
+                continue  # an older build loaded for an A/B (tools/ab_libs.py)
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

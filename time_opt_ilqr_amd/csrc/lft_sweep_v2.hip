@@ -158,6 +158,15 @@ constexpr bool has_wq() {
 struct SchedCondLSymG : SchedCondLSym {
   static constexpr int WQ = 0;
 };
+// the default without the periodic Sigma symmetrisation (developer variant 96, A/B)
+struct SchedCondLSymNS : SchedCondLSym {
+  static constexpr int NOSYM = 1;
+};
+template <class C>
+constexpr bool has_sym_every() {
+  if constexpr (requires { C::NOSYM; }) return C::NOSYM == 0;
+  return true;
+}
 // the default at two waves per SIMD: packed images (Geo PACK), 2 workgroups per CU
 // (batches above one wave per SIMD)
 struct SchedCondLSymP : SchedCondLSym {
@@ -2006,7 +2015,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
                                        (unsigned)((k + 1) * SM * ES));
     } else if (!dma_late) {
       // the step's images are consumed: their area is the symmetrisation scratch
-      if constexpr (!TRAJ) {
+      if constexpr (!TRAJ && has_sym_every<C>()) {
         if (k % kSymEvery == kSymEvery - 1)
           sym_from_upper<S>(reinterpret_cast<double (&)[S]>(X),
                             reinterpret_cast<double*>(wbase + G::OFF_Q) + g * S * S, c);
@@ -2598,6 +2607,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, a);
 #ifdef HOP_DEV
   switch (variant) {
+    case 96:  // the default without the periodic symmetrisation + rerun
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymNS, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
     case 99:  // the round-3 query (the full X sweep, Sigma_eps + X_t eliminated) + rerun
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymG, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
