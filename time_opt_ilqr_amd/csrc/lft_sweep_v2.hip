@@ -255,6 +255,14 @@ struct SchedCondTrajF : SchedCondTraj {
 struct SchedCondTrajG : SchedCondTraj {
   static constexpr int GJQ = 1;
 };
+// without the periodic Sigma symmetrisation (developer A/B: 95; 94 = with the
+// round-3 query too, i.e. round 3's kernel)
+struct SchedCondTrajNS : SchedCondTraj {
+  static constexpr int NOSYM = 1;
+};
+struct SchedCondTrajGNS : SchedCondTrajG {
+  static constexpr int NOSYM = 1;
+};
 template <class C>
 constexpr bool has_gjq() {
   if constexpr (requires { C::GJQ; }) return C::GJQ != 0;
@@ -1015,6 +1023,147 @@ __device__ __forceinline__ unsigned chunk_voff(int j, int lane, long long wave_p
   return (q < kProbPerWave * CH) ? (unsigned)((pe - pb0) * pstr + r * 16) : 0x7FFFFFFFu;
 }
 
+// First index < cnt of a non-finite element of p (INT_MAX if none), scanned by the
+// whole wave in chunks of 64 x 16 elements (16 loads in flight per lane); stops
+// after the first chunk that holds one.  Wave-uniform result.
+__device__ __forceinline__ int wave_first_nonfinite(const double* p, long long cnt, int lane) {
+  constexpr int U = 16;
+  int found = INT_MAX;
+#pragma unroll 1
+  for (long long base = 0; base < cnt; base += 64 * U) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = base + u * 64 + lane;
+      v[u] = i < cnt ? p[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = (int)(base + u * 64 + lane);
+      if (!finite_val(v[u]) && i < found) found = i;
+    }
+    if (__any(found != INT_MAX)) break;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const int x = __shfl_xor(found, o);
+    found = x < found ? x : found;
+  }
+  return found;
+}
+__device__ __forceinline__ int step_of(int idx, int per) { return idx == INT_MAX ? INT_MAX : idx / per; }
+
+// Non-finite triage of the conditioned kernels' hand-overs (rerun launch).  The
+// reference turns a non-finite input into a NaN inverse with ST_NONFINITE and no
+// ladder (utils.py:77; the oracle's and every kernel's semantics), so
+// with h_poison = 1 + the first stage whose inputs are non-finite (1 for shared
+// inputs: R^-1, z0 / xg, u_ref, Q, P, w) and h_qt = the first horizon whose
+// terminal block is non-finite, J(t) is NaN for every t >= h_nf = min(h_poison,
+// h_qt) as soon as h_poison <= h_qt + 1 (the usual shape: a rollout that leaves
+// the finite range at x_k poisons stage k and horizon k's terminal block at once).
+// When the conditioned kernel's first flag came at or after h_nf, its J(t < h_nf)
+// were computed from finite inputs before any flag: the problem's outcome is that
+// curve, NaN from h_nf on, status ST_NONFINITE and the fused argmin replayed over
+// it -- what the reference association computes, without the sequential rerun
+// (0.8 ms of latency for one wave).  Returns this lane's "resolved".
+template <int S, int MM, bool TRAJ>
+__device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane, int g,
+                                               long long wave_prob0, bool need_me, int st_me) {
+  const unsigned long long nb = __ballot(need_me);
+  const int N = a.n;
+  const int INF = N + 1;
+  bool resolved = false;
+#pragma unroll 1
+  for (int gg = 0; gg < kProbPerWave; ++gg) {
+    if (((nb >> (16 * gg)) & 0xffffull) == 0ull) continue;  // wave-uniform
+    const long long pb = wave_prob0 + gg;
+    const int kf = __shfl(st_me, 16 * gg) >> 13;  // first flagged horizon (0: prologue / forced)
+    int shared = INT_MAX, kS = INT_MAX, h_qt = INF;
+    shared = min(shared, wave_first_nonfinite(a.R + pb * a.r_bstride, (long long)MM * MM, lane));
+    if constexpr (TRAJ) {
+      constexpr int NN = S - 1;
+      const TrajArgs<double>& t = a.tr;
+      shared = min(shared, wave_first_nonfinite(t.xg + pb * t.xg_bs, NN, lane));
+      shared = min(shared, wave_first_nonfinite(t.u_ref + pb * t.ur_bs, MM, lane));
+      shared = min(shared, wave_first_nonfinite(t.Q + pb * t.q_bs, (long long)NN * NN, lane));
+      shared = min(shared, wave_first_nonfinite(t.P + pb * t.p_bs, (long long)NN * NN, lane));
+      shared = min(shared, wave_first_nonfinite(t.w + pb * t.w_bs, 1, lane));
+      // x_k feeds stage k and horizon k's terminal block
+      const int kX = step_of(wave_first_nonfinite(t.X + pb * (long long)(a.nalloc + 1) * NN,
+                                                  (long long)(N + 1) * NN, lane), NN);
+      if (kX != INT_MAX && kX >= 1) h_qt = kX;
+      if (kX != INT_MAX && kX < N) kS = kX;
+      // the other stage inputs matter only before kX (h_poison <= kX + 1 already)
+      const long long steps = kX < N ? kX : N;
+      const long long na = a.nalloc;
+      kS = min(kS, step_of(wave_first_nonfinite(t.A + pb * na * NN * NN, steps * NN * NN, lane), NN * NN));
+      kS = min(kS, step_of(wave_first_nonfinite(t.Bm + pb * na * NN * MM, steps * NN * MM, lane), NN * MM));
+      kS = min(kS, step_of(wave_first_nonfinite(t.ares + pb * na * NN, steps * NN, lane), NN));
+      kS = min(kS, step_of(wave_first_nonfinite(t.U + pb * na * MM, steps * MM, lane), MM));
+      if (t.qxx_extra)
+        kS = min(kS, step_of(wave_first_nonfinite(t.qxx_extra + pb * na * NN * NN, steps * NN * NN, lane), NN * NN));
+      if (t.qx_extra)
+        kS = min(kS, step_of(wave_first_nonfinite(t.qx_extra + pb * na * NN, steps * NN, lane), NN));
+      if (t.c_extra) kS = min(kS, step_of(wave_first_nonfinite(t.c_extra + pb * na, steps, lane), 1));
+    } else {
+      constexpr int SS = S * S, SM = S * MM;
+      const long long na = a.nalloc;
+      shared = min(shared, wave_first_nonfinite(a.z0 + pb * a.z_bstride, S, lane));
+      const int kq = step_of(wave_first_nonfinite(a.QT + pb * na * SS, (long long)N * SS, lane), SS);
+      if (kq != INT_MAX) h_qt = kq + 1;
+      // stages up to h_qt decide h_poison <= h_qt + 1
+      const long long steps = h_qt < N ? h_qt : N;
+      kS = min(kS, step_of(wave_first_nonfinite(a.Q + pb * na * SS, steps * SS, lane), SS));
+      kS = min(kS, step_of(wave_first_nonfinite(a.A + pb * na * SS, steps * SS, lane), SS));
+      kS = min(kS, step_of(wave_first_nonfinite(a.B + pb * na * SM, steps * SM, lane), SM));
+    }
+    const int h_poison = shared != INT_MAX ? 1 : (kS != INT_MAX ? kS + 1 : INF);
+    const int h_nf = h_poison < h_qt ? h_poison : h_qt;
+    const bool ok = h_nf <= N && kf >= h_nf && h_poison <= h_qt + 1;
+    if (ok) {  // wave-uniform
+      double* J = a.J + pb * N;
+      const double qnan = __builtin_nan("");
+#pragma unroll 1
+      for (int t = h_nf + lane; t <= N; t += 64) J[t - 1] = qnan;
+      if (lane == 0) {
+        if (a.t_max > 0 && a.t_star != nullptr) {  // the fused argmin, replayed
+          double best = 0.0;
+          int tbest = 0;
+#pragma unroll 1
+          for (int t0 = 1; t0 <= N; t0 += 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int t = t0 + u;
+              v[u] = (t <= N && t < h_nf) ? J[t - 1] : qnan;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+              const int t = t0 + u;
+              if (t > N) break;
+              const double jk = v[u];
+              if (t == a.t_min) {
+                best = jk;
+                tbest = t;
+              } else if (t > a.t_min && t <= a.t_max) {
+                if (!(best != best) && ((jk != jk) || jk < best)) {
+                  best = jk;
+                  tbest = t;
+                }
+              }
+            }
+          }
+          a.t_star[pb] = tbest;
+          a.j_star[pb] = best;
+        }
+        a.status[pb] = (int)ST_NONFINITE;
+      }
+    }
+    if (gg == g) resolved = ok;
+  }
+  return resolved;
+}
+
 // The exact-size LFT sweep of one wave's 4 problems (the kernel below).  need: -1 =
 // a.cond's semantics (rerun launch: the problems whose status carries ST_RERUN);
 // 0 / 1 = this lane's problem is (not) recomputed -- the conditioned kernel's fused
@@ -1048,7 +1197,16 @@ __device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
     valid = valid && need_in != 0;
     if (!__any(valid)) return;
   } else if (a.cond & 1) {  // rerun launch after SchedCond: only the problems it handed over
-    const bool need = valid && (a.status[prob] & (int)ST_RERUN);
+    const int st_in = valid ? a.status[prob] : 0;
+    bool need = valid && (st_in & (int)ST_RERUN);
+    // hand-overs explained by non-finite inputs take the reference's outcome here
+    // instead of a recompute (bit 4: a forced hand-over, never triaged)
+    if (!(a.cond & 16) && __any(need))
+      need = need && !nonfinite_resolve<S, MM, TRAJ>(a, lane, g, wave_prob0, need, st_in);
+    if (a.cond & 8) {  // triage only (HOP_OPT_NO_RERUN): the rest keep the hand-over bit
+      if (need && c == 0 && !(a.cond & 4)) a.status[prob] = (int)ST_RERUN;
+      return;
+    }
     if (!__any(need)) return;  // wave-uniform; no workgroup barrier in this kernel
     valid = need;
   }
@@ -1808,6 +1966,9 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   X[S] = 0.0;
   const double e_s = (c == S) ? 1.0 : 0.0;  // row S of A~^T: carries m through the first product
   bool bad = (a.cond & 2) != 0;
+  // the first flagged horizon + 1 (0: none; 1: the prologue or a forced hand-over),
+  // left in status bits 13.. for the rerun launch's non-finite triage
+  int kf1 = bad ? 1 : 0;
   int why = 0;  // developer builds: first failing test and horizon (see lft_cond_cf_kernel)
   auto flag = [&](bool f, int bit, int t) {
     if constexpr (kDevBuild) why = (f && why == 0) ? (bit | (t << 8)) : why;
@@ -2158,6 +2319,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     if constexpr (TRAJ && !F32) tb.load_rows(cq, imT, c);
     bad = bad || !finite_val(jk);
     flag(!finite_val(jk), 32, k + 1);
+    kf1 = (bad && kf1 == 0) ? k + 2 : kf1;  // first flagged horizon + 1
     if (fuse_argmin) {
       const int t = k + 1;
       if (t == a.t_min) {
@@ -2182,7 +2344,8 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   }
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = (T)jprev;
-    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : 0) : 0;
+    // fp32 blocks: their rerun (the generic kernel) has no triage, so no horizon bits
+    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : F32 ? 0 : (kf1 - 1) << 13) : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = (T)best;
@@ -2282,6 +2445,9 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   const int cc = in ? c : 0;
   const double eps = 1e-9;
   bool bad = (a.cond & 2) != 0;
+  // the first flagged horizon + 1 (0: none; 1: the prologue or a forced hand-over),
+  // left in status bits 13.. for the rerun launch's non-finite triage
+  int kf1 = bad ? 1 : 0;
   // developer builds: the first failing test and its horizon (hand-over diagnosis,
   // reported in status bits 5.. under a.cond & 4); product builds compile none of it
   int why = 0;
@@ -2315,6 +2481,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     SweepQ<NN>::run(Pi, d2);
     bad = bad || !pivots_ok(Qi, d1) || !pivots_ok(Pi, d2);
     flag(bad, 1, 0);
+    kf1 = bad ? 1 : 0;
     static_for<NN>([&](auto I) {
       Qi[I] = sel_lane<I>(0.0, 1.0) - Qi[I];
       Pi[I] = sel_lane<I>(0.0, 1.0) - Pi[I];
@@ -2428,7 +2595,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     }
     const double eqe1 = lane_sum<NN>(e1 * qe1);
     // ---- update: condition the prefix on stage k's cost
-    if (k % kSymEvery == kSymEvery - 1)
+    if (has_sym_every<C>() && k % kSymEvery == kSymEvery - 1)
       sym_from_upper<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
     {
       double Ht[S];
@@ -2511,6 +2678,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     eqe_k = eqe1;
     bad = bad || !finite_val(jk);
     flag(!finite_val(jk), 32, k + 1);
+    kf1 = (bad && kf1 == 0) ? k + 2 : kf1;
     if (fuse_argmin) {
       const int tt = k + 1;
       if (tt == a.t_min) {
@@ -2529,7 +2697,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   dma_wait();
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = jprev;
-    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : 0) : 0;
+    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : (kf1 - 1) << 13) : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = best;
@@ -2567,11 +2735,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   const int why_bit = (kDevBuild && opt(HOP_OPT_NO_RERUN)) ? 4 : 0;
   auto cond_rerun = [&](auto kc, auto kr, size_t bytes, bool rerun) {
     LftArgs<double> c = a;
-    c.cond = (opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0) | why_bit;
+    const bool force = opt(HOP_OPT_FORCE_HANDOVER);
+    c.cond = (force ? 2 : 0) | why_bit;
     hipError_t e = launch(kc, bytes, c);
-    if (e != hipSuccess || !rerun || opt(HOP_OPT_NO_RERUN)) return e;
+    if (e != hipSuccess || !rerun) return e;
+    // the rerun launch: non-finite triage, then the recompute of the rest
+    // (HOP_OPT_NO_RERUN: the triage alone, the rest keep HOP_ST_HANDOVER)
     LftArgs<double> r = a;
-    r.cond = 1;
+    r.cond = 1 | (force ? 16 : 0) | (opt(HOP_OPT_NO_RERUN) ? 8 | why_bit : 0);
     return launch(kr, bytes, r);
   };
   if (a.traj) {  // in-kernel augmentation (capi routes only s = 13, m = 4 here)
@@ -2583,6 +2754,12 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     if (variant == 54)  // closed-form stage inverses without the rerun launch
       return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, false);
+    if (variant == 95)
+      return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTrajNS, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
+    if (variant == 94)
+      return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTrajGNS, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
     if (variant == 97 || variant == 98)  // the round-3 query (+ rerun unless 98)
       return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTrajG, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, variant == 97);
@@ -2672,12 +2849,13 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
 #endif
   if (!pack1 && (pack2 || (a.batch + kProbPerWave - 1) / kProbPerWave > 4ll * cu_count(stream))) {
     LftArgs<double> c = a;
-    c.cond = (opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0) | why_bit;
+    const bool force = opt(HOP_OPT_FORCE_HANDOVER);
+    c.cond = (force ? 2 : 0) | why_bit;
     hipError_t e = launch(v2::lft_cond_kernel<v2::SchedCondLSymP, 13, 4>,
                           (size_t)v2::Geo<13, 4, 8, true>::WAVE_BYTES * kWavesPerBlock, c);
-    if (e != hipSuccess || opt(HOP_OPT_NO_RERUN)) return e;
-    LftArgs<double> r = a;
-    r.cond = 1;
+    if (e != hipSuccess) return e;
+    LftArgs<double> r = a;  // as cond_rerun: triage, then the recompute
+    r.cond = 1 | (force ? 16 : 0) | (opt(HOP_OPT_NO_RERUN) ? 8 | why_bit : 0);
     return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, r);
   }
   // default (variant 40): conditioned prefix + rerun of the problems it flagged; the

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("kernel")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--whole", action="store_true", help="count the whole function body")
     args = ap.parse_args()
     lines = open(args.asm).read().split("\n")
     start = next(i for i, l in enumerate(lines)
@@ -36,6 +37,8 @@ def main():
                        default=None)
             if last is not None and (best is None or last - i > best[1] - best[0]):
                 best = (i, last)
+    if args.whole or (best is not None and best[1] < best[0]):
+        best = (0, len(body) - 1)
     if best is None:
         raise SystemExit("no loop found")
     loop = body[best[0]:best[1] + 1]
