@@ -1201,8 +1201,10 @@ __device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
     bool need = valid && (st_in & (int)ST_RERUN);
     // hand-overs explained by non-finite inputs take the reference's outcome here
     // instead of a recompute (bit 4: a forced hand-over, never triaged)
-    if (!(a.cond & 16) && __any(need))
-      need = need && !nonfinite_resolve<S, MM, TRAJ>(a, lane, g, wave_prob0, need, st_in);
+    if (!(a.cond & 16) && __any(need)) {  // called by the whole wave (lane-0 writes, shuffles)
+      const bool resolved = nonfinite_resolve<S, MM, TRAJ>(a, lane, g, wave_prob0, need, st_in);
+      need = need && !resolved;
+    }
     if (a.cond & 8) {  // triage only (HOP_OPT_NO_RERUN): the rest keep the hand-over bit
       if (need && c == 0 && !(a.cond & 4)) a.status[prob] = (int)ST_RERUN;
       return;
