@@ -1003,12 +1003,13 @@ __device__ __forceinline__ void sym_from_upper(double (&X)[S], double* t, int c)
     for (int i = 0; i < S; ++i) t[i * S + c] = X[i];
   }
   wave_sync();
+  // row c of the scratch (column c of Sigma) in one asm block: plain C++ reads here
+  // were sunk one by one under the lane condition (13 branches, each waiting alone)
   const int cr = c < S ? c : 0;
+  double y[S];
+  LdsRow<S>::run(lds_addr(t) + 8u * S * cr, y);
 #pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const double y = t[cr * S + i];
-    X[i] = c < i ? y : X[i];
-  }
+  for (int i = 0; i < S; ++i) X[i] = c < i ? y[i] : X[i];
   wave_sync();
 }
 
