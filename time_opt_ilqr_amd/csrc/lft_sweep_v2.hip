@@ -1112,8 +1112,8 @@ __device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane
       shared = min(shared, wave_first_nonfinite(a.z0 + pb * a.z_bstride, S, lane));
       const int kq = step_of(wave_first_nonfinite(a.QT + pb * na * SS, (long long)N * SS, lane), SS);
       if (kq != INT_MAX) h_qt = kq + 1;
-      // stages up to h_qt decide h_poison <= h_qt + 1
-      const long long steps = h_qt < N ? h_qt : N;
+      // stages 0 .. h_qt decide h_poison <= h_qt + 1
+      const long long steps = h_qt < N ? h_qt + 1 : N;
       kS = min(kS, step_of(wave_first_nonfinite(a.Q + pb * na * SS, steps * SS, lane), SS));
       kS = min(kS, step_of(wave_first_nonfinite(a.A + pb * na * SS, steps * SS, lane), SS));
       kS = min(kS, step_of(wave_first_nonfinite(a.B + pb * na * SM, steps * SM, lane), SM));
