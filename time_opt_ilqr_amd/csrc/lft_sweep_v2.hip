@@ -987,29 +987,32 @@ struct Geo {
   static constexpr int WAVE_BYTES_T = OFF_CQ + CQ_BYTES;
 };
 
-// Sigma from its upper triangle (lanes c < i of row i take Sigma[c][i]; lanes >= S,
-// m and gamma, untouched) through a wave-private S x S scratch t of this lane's
-// problem.  The conditioned update Sigma' = Sigma_eps - Sigma_eps S^-1 Sigma_eps
-// passes Sigma_eps's antisymmetric rounding through unchanged while it contracts
+// Sigma symmetrised, (Sigma + Sigma^T) / 2 (lanes >= S, m and gamma, untouched),
+// through a wave-private S x S scratch t of this lane's problem.  The conditioned
+// update Sigma' = Sigma_eps - Sigma_eps S^-1 Sigma_eps passes Sigma_eps's antisymmetric rounding through unchanged while it contracts
 // the symmetric part, so without this the antisymmetric part accumulates over the
 // horizon: on a real quadrotor linearisation (tests/golden/real_lin_hp.npz) J ends
 // 0.5 off the 50-digit value; symmetrised every 8 steps it stays within 1e-11
 // (NumPy model of the arithmetic).
 constexpr int kSymEvery = 8;
 template <int S>
-__device__ __forceinline__ void sym_from_upper(double (&X)[S], double* t, int c) {
+__device__ __forceinline__ void sym_average(double (&X)[S], double* t, int c) {
   if (c < S) {
 #pragma unroll
     for (int i = 0; i < S; ++i) t[i * S + c] = X[i];
   }
   wave_sync();
   // row c of the scratch (column c of Sigma) in one asm block: plain C++ reads here
-  // were sunk one by one under the lane condition (13 branches, each waiting alone)
+  // were sunk one by one under the lane condition (13 branches, each waiting alone);
+  // then Sigma <- (Sigma + Sigma^T) / 2 on lanes < S by one FMA per row (a per-row
+  // lane mask "c < i" would hold 13 loop-invariant SGPR pairs: the closed-form
+  // kernel spilled 63 SGPRs with it)
   const int cr = c < S ? c : 0;
+  const double hs = c < S ? 0.5 : 0.0;
   double y[S];
   LdsRow<S>::run(lds_addr(t) + 8u * S * cr, y);
 #pragma unroll
-  for (int i = 0; i < S; ++i) X[i] = c < i ? y[i] : X[i];
+  for (int i = 0; i < S; ++i) X[i] = __builtin_fma(hs, y[i] - X[i], X[i]);
   wave_sync();
 }
 
@@ -2181,7 +2184,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       // the step's images are consumed: their area is the symmetrisation scratch
       if constexpr (!TRAJ && has_sym_every<C>()) {
         if (k % kSymEvery == kSymEvery - 1)
-          sym_from_upper<S>(reinterpret_cast<double (&)[S]>(X),
+          sym_average<S>(reinterpret_cast<double (&)[S]>(X),
                             reinterpret_cast<double*>(wbase + G::OFF_Q) + g * S * S, c);
       }
       wave_sync();
@@ -2599,7 +2602,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     const double eqe1 = lane_sum<NN>(e1 * qe1);
     // ---- update: condition the prefix on stage k's cost
     if (has_sym_every<C>() && k % kSymEvery == kSymEvery - 1)
-      sym_from_upper<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
+      sym_average<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
     {
       double Ht[S];
       copy(Ht, reinterpret_cast<double (&)[S]>(X));
