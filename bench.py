@@ -270,6 +270,8 @@ def _lft_workload(args, world, lo, hi, dev):
         host, alt = (At.data, Bt.data, Qt.data, Ri, z0, QTt.data), launch_bm
 
     side = _traj64_side(hi - lo, s, m, N, t_min, dtype, dev) if tiled else None
+    if (s, m, args.dtype) == (13, 4, "f64") and not tiled and world == 1 and not args.no_alt:
+        side = _quad_side(hi - lo, N, t_min, dev)
     kname, bound = kernel_path(s, m, args.dtype)
     if small:
         kname = kname[:-1] + (",LY=2 tile64>" if tiled else ",LY=1 batch-major>")
@@ -323,10 +325,59 @@ def _traj64_side(Bn, s, m, N, t_min, dtype, dev):
                                      rho_reg=1.0, t_min=t_min, t_max=N)
 
     n = s - 1
-    return {"select_traj64": lambda: select_on(lin0),
-            "linearize_select_traj64": lambda: select_on(lin()),
+    return {"name": "config3_from_linearisation", "select_key": "select_traj64",
+            "fns": {"select_traj64": lambda: select_on(lin0),
+                    "linearize_select_traj64": lambda: select_on(lin())},
             "select_bytes_per_sweep": (N * (n * n + n * m + 2 * n + m) + n) *
-                                      (4 if dtype == torch.float32 else 8)}
+                                      (4 if dtype == torch.float32 else 8),
+            "note": ("cart-pole rollouts linearised into tile64 (hop_linearize_tile64), raw A_k, "
+                     "B_k, a_k, x_k, u_k streamed by hop_lft_sweep_traj_tile64; select_traj64 = "
+                     "the select alone, linearize_select_traj64 = both stages in the timing; "
+                     "well-conditioned cost, rho_reg = 1 (fp32)")}
+
+
+def _quad_side(Bn, N, t_min, dev):
+    """Config 2's shape from the raw linearisation, timed beside the line: Bn perturbed
+    quadrotor rollouts (systems.py:119-230 maker, x0 + 0.1 N(0, 1), U = u_ref + 0.05
+    N(0, 1)), the forward-difference linearisation of ilqr_timeopt's default
+    (linearization.py:177-211), then the select block on it (augmented.py:10-87 in
+    registers + the closed-form conditioned kernel + argmin, solver.py:514-522) with
+    the maker's cost at the reference's rho_reg = 1e-12.  `select_traj` times the select
+    alone on one linearisation, `linearize_select_traj` both stages."""
+    import numpy as np
+    import torch
+    from time_opt_ilqr_amd import engine, systems
+    from time_opt_ilqr_amd.utils import as_terminal_weight
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap, _ = systems.make_quadrotor(N=N)
+    g = torch.Generator(device=dev)
+    g.manual_seed(23)
+    kw = dict(device=dev, dtype=torch.float64, generator=g)
+    U = torch.as_tensor(u_ref, device=dev) + 0.05 * torch.randn((Bn, N, F.m), **kw)
+    X = engine.rollout(F.system_id, torch.as_tensor(x0, device=dev) +
+                       0.1 * torch.randn((Bn, F.n), **kw), U, F.dt)
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
+    shared = (t(xg), t(u_ref), t(Q), torch.linalg.inv(t(R)), t(as_terminal_weight(alpha, F.n)),
+              t([w]))
+
+    def lin():
+        return engine.linearize(F.system_id, X, U, F.dt, central=False)
+
+    lin0 = lin()
+
+    def select_on(L):
+        return engine.propagate_traj(L.A, L.B, L.a_res, X, U, *shared, wrap_idx=wrap,
+                                     t_min=t_min, t_max=N)
+
+    n, m = F.n, F.m
+    return {"name": "config2_from_linearisation", "select_key": "select_traj",
+            "fns": {"select_traj": lambda: select_on(lin0),
+                    "linearize_select_traj": lambda: select_on(lin())},
+            "select_bytes_per_sweep": (N * (n * n + n * m + 2 * n + m) + n) * 8,
+            "note": ("quadrotor rollouts linearised by forward differences (hop_linearize_f64), "
+                     "then hop_lft_sweep_traj_f64 (closed-form conditioned kernel) at "
+                     "rho_reg = 1e-12; select_traj = the select alone, linearize_select_traj = "
+                     "both stages; problems_status_ok counts the problems with a clean status "
+                     "and finite curve")}
 
 
 def _config5_workload(args, world, lo, hi, dev):
@@ -765,14 +816,13 @@ def main(argv=None):
                "each step (PCIe-inclusive); not the headline value"}
         del pinned
 
-    # side figures of the tile64 config-3 line: the select from the raw linearisation
-    traj64 = None
+    # side figures: the select from the raw linearisation (config 3: tile64 cart-pole;
+    # config 2: batch-major quadrotor)
+    side_fig = None
     if rank == 0 and info.get("side") is not None and not args.no_alt:
-        traj64 = {}
-        for key in ("select_traj64", "linearize_select_traj64"):
-            fn = info["side"].get(key)
-            if fn is None:
-                continue
+        sd = info["side"]
+        side_fig = {}
+        for key, fn in sd["fns"].items():
             r_ = fn()
             for _ in range(3):
                 fn()
@@ -783,17 +833,17 @@ def main(argv=None):
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 10
-            traj64[key] = {"ms": ms, "sweeps_per_s": (hi - lo) / (ms * 1e-3),
-                           "status_ok": bool(torch.isfinite(r_.J).all() and (r_.status == 0).all())}
-        bps = info["side"]["select_bytes_per_sweep"]
-        sel = traj64.get("select_traj64")
+            fin = torch.isfinite(r_.J).all(dim=1)
+            side_fig[key] = {"ms": ms, "sweeps_per_s": (hi - lo) / (ms * 1e-3),
+                             "status_ok": bool(fin.all() and (r_.status == 0).all()),
+                             "problems_status_ok": int(((r_.status == 0) & fin).sum().item())}
+        sel = side_fig.get(sd["select_key"])
         if sel is not None:
+            bps = sd["select_bytes_per_sweep"]
             sel["alg_bytes_per_sweep"] = bps
             sel["hbm_frac"] = bps * (hi - lo) / (sel["ms"] * 1e-3) / 1e9 / PEAK_HBM_GBS
-        traj64["note"] = ("cart-pole rollouts linearised into tile64 (hop_linearize_tile64), "
-                          "raw A_k, B_k, a_k, x_k, u_k streamed by hop_lft_sweep_traj_tile64; "
-                          "select_traj64 = the select alone, linearize_select_traj64 = both "
-                          "stages in the timing; well-conditioned cost, rho_reg = 1 (fp32)")
+        side_fig["note"] = sd["note"]
+        side_fig = (sd["name"], side_fig)
         info["side"] = None
 
     # side figure: the same sweep on batch-major blocks (tile64 runs only)
@@ -898,7 +948,7 @@ def main(argv=None):
             "h2d_inclusive": h2d,
             "config4_shard_anchor": anchor,
             "config4_global_1gpu": anchor_g,
-            **({"config3_from_linearisation": traj64} if traj64 else {}),
+            **({side_fig[0]: side_fig[1]} if side_fig else {}),
             "status_ok": status_ok,
         }
         print(json.dumps(line), flush=True)
