@@ -1028,10 +1028,11 @@ __device__ __forceinline__ unsigned chunk_voff(int j, int lane, long long wave_p
 }
 
 // First index < cnt of a non-finite element of p (INT_MAX if none), scanned by the
-// whole wave in chunks of 64 x 16 elements (16 loads in flight per lane); stops
-// after the first chunk that holds one.  Wave-uniform result.
+// whole wave in chunks of 64 x 64 elements (64 loads in flight per lane: the scan is
+// latency-bound, one round trip per chunk); stops after the first chunk that holds
+// one.  Wave-uniform result.
 __device__ __forceinline__ int wave_first_nonfinite(const double* p, long long cnt, int lane) {
-  constexpr int U = 16;
+  constexpr int U = 64;
   int found = INT_MAX;
 #pragma unroll 1
   for (long long base = 0; base < cnt; base += 64 * U) {
@@ -1054,6 +1055,26 @@ __device__ __forceinline__ int wave_first_nonfinite(const double* p, long long c
     found = x < found ? x : found;
   }
   return found;
+}
+// Any non-finite element in K small arrays (each at most 256 elements), all loads in
+// flight at once (one round trip).  Wave-uniform.
+template <int K>
+__device__ __forceinline__ bool wave_any_nonfinite(const double* const (&p)[K],
+                                                   const int (&cnt)[K], int lane) {
+  double v[K][4];
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 64 * r + lane;
+      v[s][r] = i < cnt[s] ? p[s][i] : 0.0;
+    }
+  bool bad = false;
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bad = bad || !finite_val(v[s][r]);
+  return __any(bad);
 }
 __device__ __forceinline__ int step_of(int idx, int per) { return idx == INT_MAX ? INT_MAX : idx / per; }
 
@@ -1082,16 +1103,17 @@ __device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane
     if (((nb >> (16 * gg)) & 0xffffull) == 0ull) continue;  // wave-uniform
     const long long pb = wave_prob0 + gg;
     const int kf = __shfl(st_me, 16 * gg) >> 13;  // first flagged horizon (0: prologue / forced)
-    int shared = INT_MAX, kS = INT_MAX, h_qt = INF;
-    shared = min(shared, wave_first_nonfinite(a.R + pb * a.r_bstride, (long long)MM * MM, lane));
+    int kS = INT_MAX, h_qt = INF;
+    bool shared;
     if constexpr (TRAJ) {
       constexpr int NN = S - 1;
+      static_assert(NN * NN <= 256 && MM * MM <= 256, "shared arrays of one scan round trip");
       const TrajArgs<double>& t = a.tr;
-      shared = min(shared, wave_first_nonfinite(t.xg + pb * t.xg_bs, NN, lane));
-      shared = min(shared, wave_first_nonfinite(t.u_ref + pb * t.ur_bs, MM, lane));
-      shared = min(shared, wave_first_nonfinite(t.Q + pb * t.q_bs, (long long)NN * NN, lane));
-      shared = min(shared, wave_first_nonfinite(t.P + pb * t.p_bs, (long long)NN * NN, lane));
-      shared = min(shared, wave_first_nonfinite(t.w + pb * t.w_bs, 1, lane));
+      const double* const sp[6] = {a.R + pb * a.r_bstride, t.xg + pb * t.xg_bs,
+                                   t.u_ref + pb * t.ur_bs, t.Q + pb * t.q_bs, t.P + pb * t.p_bs,
+                                   t.w + pb * t.w_bs};
+      const int sc[6] = {MM * MM, NN, MM, NN * NN, NN * NN, 1};
+      shared = wave_any_nonfinite<6>(sp, sc, lane);
       // x_k feeds stage k and horizon k's terminal block
       const int kX = step_of(wave_first_nonfinite(t.X + pb * (long long)(a.nalloc + 1) * NN,
                                                   (long long)(N + 1) * NN, lane), NN);
@@ -1112,7 +1134,9 @@ __device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane
     } else {
       constexpr int SS = S * S, SM = S * MM;
       const long long na = a.nalloc;
-      shared = min(shared, wave_first_nonfinite(a.z0 + pb * a.z_bstride, S, lane));
+      const double* const sp[2] = {a.R + pb * a.r_bstride, a.z0 + pb * a.z_bstride};
+      const int sc[2] = {MM * MM, S};
+      shared = wave_any_nonfinite<2>(sp, sc, lane);
       const int kq = step_of(wave_first_nonfinite(a.QT + pb * na * SS, (long long)N * SS, lane), SS);
       if (kq != INT_MAX) h_qt = kq + 1;
       // stages 0 .. h_qt decide h_poison <= h_qt + 1
@@ -1121,7 +1145,7 @@ __device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane
       kS = min(kS, step_of(wave_first_nonfinite(a.A + pb * na * SS, steps * SS, lane), SS));
       kS = min(kS, step_of(wave_first_nonfinite(a.B + pb * na * SM, steps * SM, lane), SM));
     }
-    const int h_poison = shared != INT_MAX ? 1 : (kS != INT_MAX ? kS + 1 : INF);
+    const int h_poison = shared ? 1 : (kS != INT_MAX ? kS + 1 : INF);
     const int h_nf = h_poison < h_qt ? h_poison : h_qt;
     const bool ok = h_nf <= N && kf >= h_nf && h_poison <= h_qt + 1;
     if (ok) {  // wave-uniform
@@ -1129,39 +1153,61 @@ __device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane
       const double qnan = __builtin_nan("");
 #pragma unroll 1
       for (int t = h_nf + lane; t <= N; t += 64) J[t - 1] = qnan;
-      if (lane == 0) {
-        if (a.t_max > 0 && a.t_star != nullptr) {  // the fused argmin, replayed
-          double best = 0.0;
-          int tbest = 0;
+      if (a.t_max > 0 && a.t_star != nullptr) {
+        // the fused argmin, replayed over the stored curve in one pass: its sequential
+        // rule (the first horizon t_min initialises, a NaN wins and sticks, a strictly
+        // smaller value replaces) is "the first NaN of the window, else the first
+        // minimiser", with a virtual (0, 0.0) first when t_min < 1
+        const int t_hi = a.t_max < N ? a.t_max : N;
+        int nan_t = INT_MAX, min_t = INT_MAX;
+        double min_v = 0.0;
 #pragma unroll 1
-          for (int t0 = 1; t0 <= N; t0 += 16) {
-            double v[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              const int t = t0 + u;
-              v[u] = (t <= N && t < h_nf) ? J[t - 1] : qnan;
+        for (int t = 1 + lane; t <= N; t += 64) {
+          const bool in = t >= a.t_min && (t == a.t_min || t <= t_hi);
+          const double jk = t < h_nf ? J[t - 1] : qnan;
+          if (in) {
+            if (jk != jk) {
+              nan_t = t < nan_t ? t : nan_t;
+            } else if (min_t == INT_MAX || jk < min_v) {
+              min_v = jk;
+              min_t = t;
             }
+          }
+        }
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-              const int t = t0 + u;
-              if (t > N) break;
-              const double jk = v[u];
-              if (t == a.t_min) {
-                best = jk;
-                tbest = t;
-              } else if (t > a.t_min && t <= a.t_max) {
-                if (!(best != best) && ((jk != jk) || jk < best)) {
-                  best = jk;
-                  tbest = t;
-                }
-              }
+        for (int o = 32; o >= 1; o >>= 1) {
+          const int xn = __shfl_xor(nan_t, o);
+          nan_t = xn < nan_t ? xn : nan_t;
+          const int xt = __shfl_xor(min_t, o);
+          const double xv = __shfl_xor(min_v, o);
+          if (xt != INT_MAX && (min_t == INT_MAX || xv < min_v || (xv == min_v && xt < min_t))) {
+            min_v = xv;
+            min_t = xt;
+          }
+        }
+        if (lane == 0) {
+          int tbest = 0;
+          double best = 0.0;
+          if (a.t_min < 1) {  // the virtual (0, 0.0): only a NaN or a negative value replaces it
+            if (nan_t != INT_MAX) {
+              tbest = nan_t;
+              best = qnan;
+            } else if (min_t != INT_MAX && min_v < 0.0) {
+              tbest = min_t;
+              best = min_v;
             }
+          } else if (nan_t != INT_MAX) {
+            tbest = nan_t;
+            best = qnan;
+          } else if (min_t != INT_MAX) {
+            tbest = min_t;
+            best = min_v;
           }
           a.t_star[pb] = tbest;
           a.j_star[pb] = best;
         }
-        a.status[pb] = (int)ST_NONFINITE;
       }
+      if (lane == 0) a.status[pb] = (int)ST_NONFINITE;
     }
     if (gg == g) resolved = ok;
   }
