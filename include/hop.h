@@ -66,10 +66,14 @@ const char* hop_last_error(void);
  *                           kernel (no conditioned prefix)
  *   HOP_OPT_TRAJ_UNFUSED    trajectory form through hop_augment + the sweep
  *   HOP_OPT_STAMPS          section-stamped instantiations (developer builds)
- *   HOP_OPT_NO_RERUN        the conditioned-prefix kernels run without their
- *                           rerun launch: a problem they hand over keeps
- *                           HOP_ST_HANDOVER in status and its J is not valid
- *                           (counts hand-overs; tests and tools only)
+ *   HOP_OPT_NO_RERUN        the conditioned-prefix kernels run without the
+ *                           recompute of their rerun launch: a problem they hand
+ *                           over keeps HOP_ST_HANDOVER in status and its J is not
+ *                           valid (counts hand-overs; tests and tools only).  The
+ *                           s = 13 fp64 paths still run the launch's non-finite
+ *                           triage: a hand-over explained by non-finite inputs
+ *                           gets the reference's outcome (ST_NONFINITE, NaN from
+ *                           the first affected horizon) and is not counted
  * `variant` selects an A/B schedule; only developer builds (HOP_DEV_BUILD=1 at
  * build time, hop_build_flags() & 1) compile them -- product builds return
  * HOP_E_ARG for variant != 0 or HOP_OPT_STAMPS.
