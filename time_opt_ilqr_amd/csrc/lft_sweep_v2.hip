@@ -1092,7 +1092,7 @@ __device__ __forceinline__ int step_of(int idx, int per) { return idx == INT_MAX
 // it -- what the reference association computes, without the sequential rerun
 // (0.8 ms of latency for one wave).  Returns this lane's "resolved".
 template <int S, int MM, bool TRAJ>
-__device__ __noinline__ bool nonfinite_resolve(const LftArgs<double> a, int lane, int g,
+__device__ __forceinline__ bool nonfinite_resolve(const LftArgs<double>& a, int lane, int g,
                                                long long wave_prob0, bool need_me, int st_me) {
   const unsigned long long nb = __ballot(need_me);
   const int N = a.n;
