@@ -1036,16 +1036,18 @@ __device__ __forceinline__ int wave_first_nonfinite(const double* p, long long c
   int found = INT_MAX;
 #pragma unroll 1
   for (long long base = 0; base < cnt; base += 64 * U) {
+    // unconditional loads (a clamped index past the end): a load under "i < cnt"
+    // became a branch with its own vmcnt(0) wait, 64 serial round trips per chunk
     double v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long long i = base + u * 64 + lane;
-      v[u] = i < cnt ? p[i] : 0.0;
+      v[u] = p[i < cnt ? i : cnt - 1];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int i = (int)(base + u * 64 + lane);
-      if (!finite_val(v[u]) && i < found) found = i;
+      const long long i = base + u * 64 + lane;
+      if (i < cnt && !finite_val(v[u]) && (int)i < found) found = (int)i;
     }
     if (__any(found != INT_MAX)) break;
   }
@@ -1067,13 +1069,13 @@ __device__ __forceinline__ bool wave_any_nonfinite(const double* const (&p)[K],
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = 64 * r + lane;
-      v[s][r] = i < cnt[s] ? p[s][i] : 0.0;
+      v[s][r] = p[s][i < cnt[s] ? i : cnt[s] - 1];  // unconditional (see above)
     }
   bool bad = false;
 #pragma unroll
   for (int s = 0; s < K; ++s)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bad = bad || !finite_val(v[s][r]);
+    for (int r = 0; r < 4; ++r) bad = bad || (64 * r + lane < cnt[s] && !finite_val(v[s][r]));
   return __any(bad);
 }
 __device__ __forceinline__ int step_of(int idx, int per) { return idx == INT_MAX ? INT_MAX : idx / per; }
@@ -1164,7 +1166,7 @@ __device__ __forceinline__ bool nonfinite_resolve(const LftArgs<double>& a, int 
 #pragma unroll 1
         for (int t = 1 + lane; t <= N; t += 64) {
           const bool in = t >= a.t_min && (t == a.t_min || t <= t_hi);
-          const double jk = t < h_nf ? J[t - 1] : qnan;
+          const double jk = t < h_nf ? J[t - 1] : qnan;  // (at most 2 per lane at N = 100)
           if (in) {
             if (jk != jk) {
               nan_t = t < nan_t ? t : nan_t;
