@@ -54,12 +54,15 @@ def baseline_metric():
         return "batched iLQR backward sweeps/sec, Quadrotor n=13 N=100, at 1/2/4/8 GPU"
 
 
-def kernel_path(s, m, dtype):
+def kernel_path(s, m, dtype, batch=4096):
     """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound.
     The s=13 kernels are compute-bound on the fp64 pipe (MI355X: vector fp64 peak ==
-    matrix fp64 peak); they issue DPP-broadcast FMAs, not MFMA."""
+    matrix fp64 peak); they issue DPP-broadcast FMAs, not MFMA.  Above
+    one wave per SIMD (4 problems per wave, 4 x 256 SIMDs) the s=13 fp64 path takes the
+    packed two-waves-per-SIMD layout."""
     if dtype == "f64" and (s, m) == (13, 4):
-        return "lft_cond_kernel<SchedCondLSym,13,4>", "fp64"
+        packed = (batch + 3) // 4 > 4 * 256
+        return f"lft_cond_kernel<{'SchedCondLSymP' if packed else 'SchedCondLSymL'},13,4>", "fp64"
     if dtype == "f32" and (s, m) == (13, 4):
         return "lft_cond_kernel<SchedCond,13,4,float>", "fp64"  # fp32 blocks, fp64 arithmetic
     if (s, m) in SMALL_SHAPES[dtype]:
@@ -272,7 +275,7 @@ def _lft_workload(args, world, lo, hi, dev):
     side = _traj64_side(hi - lo, s, m, N, t_min, dtype, dev) if tiled else None
     if (s, m, args.dtype) == (13, 4, "f64") and not tiled and world == 1 and not args.no_alt:
         side = _quad_side(hi - lo, N, t_min, dev)
-    kname, bound = kernel_path(s, m, args.dtype)
+    kname, bound = kernel_path(s, m, args.dtype, hi - lo)
     if small:
         kname = kname[:-1] + (",LY=2 tile64>" if tiled else ",LY=1 batch-major>")
     w = 8 if args.dtype == "f64" else 4

@@ -162,6 +162,16 @@ struct SchedCondLSymG : SchedCondLSym {
 struct SchedCondLSymNS : SchedCondLSym {
   static constexpr int NOSYM = 1;
 };
+// the symmetrisation after the step's DMA issue, through its own LDS scratch past the
+// four waves' areas (developer variant 93, A/B)
+struct SchedCondLSymL : SchedCondLSym {
+  static constexpr int SYMLATE = 1;
+};
+template <class C>
+constexpr bool has_symlate() {
+  if constexpr (requires { C::SYMLATE; }) return C::SYMLATE != 0;
+  return false;
+}
 template <class C>
 constexpr bool has_sym_every() {
   if constexpr (requires { C::NOSYM; }) return C::NOSYM == 0;
@@ -2230,13 +2240,21 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
                                        (unsigned)((k + 1) * SM * ES));
     } else if (!dma_late) {
       // the step's images are consumed: their area is the symmetrisation scratch
-      if constexpr (!TRAJ && has_sym_every<C>()) {
+      if constexpr (!TRAJ && has_sym_every<C>() && !has_symlate<C>()) {
         if (k % kSymEvery == kSymEvery - 1)
           sym_average<S>(reinterpret_cast<double (&)[S]>(X),
                             reinterpret_cast<double*>(wbase + G::OFF_Q) + g * S * S, c);
       }
       wave_sync();
       if (k + 1 < N) dma_step(k + 1);
+      if constexpr (has_symlate<C>()) {
+        static_assert(!TRAJ && !has_pack<C>(), "own scratch: the one-wave layout");
+        if (k % kSymEvery == kSymEvery - 1)
+          sym_average<S>(reinterpret_cast<double (&)[S]>(X),
+                         reinterpret_cast<double*>(smem_raw + kWavesPerBlock * WB) +
+                             (w * kProbPerWave + g) * S * S,
+                         c);
+      }
     }
     stamp(4);
     // ---- update: condition the prefix on stage k's cost
@@ -2834,10 +2852,16 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   }
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
   constexpr size_t bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
+  // + the symmetrisation scratch of SchedCondLSymL past the four waves' areas
+  constexpr size_t bytes_symlate = bytes + (size_t)kWavesPerBlock * kProbPerWave * 13 * 13 * 8;
+  static_assert(bytes_symlate <= 160 * 1024, "one workgroup per CU");
   if (opt(HOP_OPT_REFERENCE_ASSOC) || variant == 30)
     return launch(v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, a);
 #ifdef HOP_DEV
   switch (variant) {
+    case 93:  // the symmetrisation after the DMA issue, own scratch + rerun (= the default)
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymL, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes_symlate, true);
     case 96:  // the default without the periodic symmetrisation + rerun
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymNS, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
@@ -2871,8 +2895,11 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     case 52:  // the unhalved sums + the reciprocal Newton (47 + 48), no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLSN, 13, 4>, bytes, a);
     case 41:  // the default's conditioned kernel without the rerun launch (A/B timing)
+      return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymL, 13, 4>,
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes_symlate, false);
+    case 90:  // round 4's first placement: the symmetrisation before the DMA issue, + rerun
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
-                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, false);
+                        v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
     case 58:  // round-2 default (halved symmetric sums) without the rerun launch
       return launch(v2::lft_cond_kernel<v2::SchedCondL, 13, 4>, bytes, a);
     case 60: {  // fused hand-over: flagged problems recomputed at the end of the same
@@ -2914,9 +2941,11 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   }
   // default (variant 40): conditioned prefix + rerun of the problems it flagged; the
   // stage / terminal inverses of the unhalved symmetric sums (SYM2: 1-2 % faster than
-  // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_ab_pe.txt)
-  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSym, 13, 4>,
-                    v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
+  // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_ab_pe.txt); the periodic
+  // symmetrisation after the step's DMA issue, in its own LDS scratch (SchedCondLSymL:
+  // 0.4 % faster than before it, bitwise equal, profiles/r04_p18_ab_symlate.txt)
+  return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymL, 13, 4>,
+                    v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes_symlate, true);
 }
 
 }  // namespace hop
