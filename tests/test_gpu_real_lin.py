@@ -80,3 +80,7 @@ def test_select_batch_scale_real_linearisations(dev, name):
     assert o["flip_gap_max"] <= 1e-3, o
     assert st["handover_traj_clean_final"] == 0, st["handover_traj_reasons"]
     assert st["handover_traj"] <= 4096 - st["finite"]
+    # round 4: the rerun launch's non-finite triage resolves the diverged rollouts too
+    # (DESIGN.md 3.7), so nothing on these batches is left to the sequential recompute
+    assert st["handover_traj"] == 0 and st["handover_aug"] == 0, (st["handover_traj"],
+                                                                 st["handover_aug"])
