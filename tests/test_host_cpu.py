@@ -868,3 +868,38 @@ def test_lane_rows_q_block_emulated():
             want = want + np.full(16, X[i][j]) * Y[j]
         assert np.array_equal(regs[i], want)
         assert np.array_equal(regs[n + i], lds[(base + 128 * i) // 8])
+
+
+def test_argmin_replay_rule_equals_the_fused_sequential_rule():
+    """The rerun launch's non-finite triage replays the fused argmin as one wave
+    reduction (lft_sweep_v2.hip nonfinite_resolve): "the first NaN of the window, else
+    the first minimiser".  That equals the kernels' sequential rule (t_min initialises;
+    later t <= t_max replace when best is not NaN and J is NaN or strictly smaller) on
+    every window the C ABI accepts (1 <= t_min <= t_max <= N), NaN tails included."""
+    rng = np.random.default_rng(11)
+    for _ in range(3000):
+        N = int(rng.integers(1, 40))
+        J = rng.choice([-1.0, 0.0, 1.0, 2.0], size=N) + rng.integers(0, 3, size=N) * 0.5
+        if rng.random() < 0.5:
+            J[rng.integers(0, N, size=int(rng.integers(1, 4)))] = np.nan
+        if rng.random() < 0.3:
+            J[int(rng.integers(0, N)):] = np.nan  # the triage's NaN tail from h_nf
+        t_min = int(rng.integers(1, N + 1))
+        t_max = int(rng.integers(t_min, N + 1))
+        best, tbest = 0.0, 0
+        for t in range(1, N + 1):
+            jk = J[t - 1]
+            if t == t_min:
+                best, tbest = jk, t
+            elif t_min < t <= t_max and not np.isnan(best) and (np.isnan(jk) or jk < best):
+                best, tbest = jk, t
+        win = np.arange(t_min, t_max + 1)
+        nans = [t for t in win if np.isnan(J[t - 1])]
+        if nans:
+            t2, b2 = nans[0], np.nan
+        else:
+            vals = J[win - 1]
+            t2 = int(win[int(np.argmin(vals))])
+            b2 = J[t2 - 1]
+        assert t2 == tbest, (J, t_min, t_max)
+        assert (np.isnan(b2) and np.isnan(best)) or b2 == best
