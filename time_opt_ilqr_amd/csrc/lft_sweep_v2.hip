@@ -190,6 +190,10 @@ constexpr bool has_pack() {
 struct SchedCondLSymStamped : SchedCondLSym {
   static constexpr int STAMP = 1;
 };
+// stamps of the round-4 default (the symmetrisation after the DMA issue)
+struct SchedCondLSymLStamped : SchedCondLSymL {
+  static constexpr int STAMP = 1;
+};
 struct SchedCondLNewt : SchedCondL {
   static constexpr int SYM2 = 0, NEWT = 1, PEPS = 0;
 };
@@ -2869,7 +2873,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return cond_rerun(v2::lft_cond_kernel<v2::SchedCondLSymG, 13, 4>,
                         v2::lft_sweep_v2_kernel<v2::SchedLdlDma, 13, 4>, bytes, true);
     case 42:  // stamps of the default (tools/stamps.py --cond), no rerun
-      return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
+      return launch(v2::lft_cond_kernel<v2::SchedCondLSymLStamped, 13, 4>, bytes_symlate, a);
     case 59:  // stamps of the round-2 default (halved sums), no rerun
       return launch(v2::lft_cond_kernel<v2::SchedCondLStamped, 13, 4>, bytes, a);
     case 43:  // image reads not overlapped with the sweeps, no rerun
@@ -2919,7 +2923,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
     default: break;
   }
   if (opt(HOP_OPT_STAMPS))
-    return launch(v2::lft_cond_kernel<v2::SchedCondLSymStamped, 13, 4>, bytes, a);
+    return launch(v2::lft_cond_kernel<v2::SchedCondLSymLStamped, 13, 4>, bytes_symlate, a);
 #endif
   // more waves than SIMDs: the packed-image layout at two waves per SIMD (the rerun
   // launch keeps the LFT kernel's own layout)
