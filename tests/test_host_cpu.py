@@ -903,3 +903,54 @@ def test_argmin_replay_rule_equals_the_fused_sequential_rule():
             b2 = J[t2 - 1]
         assert t2 == tbest, (J, t_min, t_max)
         assert (np.isnan(b2) and np.isnan(best)) or b2 == best
+
+
+def test_nonfinite_triage_rule_matches_oracle_semantics():
+    """The rerun launch's non-finite triage (lft_sweep_v2.hip nonfinite_resolve) claims
+    that with h_poison = 1 + the first stage whose Q_k / A_k / B_k is non-finite (1 for a
+    non-finite z0 or R^-1), h_qt = the first horizon whose QT block is non-finite and
+    h_nf = min of the two, h_poison <= h_qt + 1 implies: the reference association's J is
+    finite before h_nf and NaN from h_nf on, and its status is ST_NONFINITE alone.  The
+    oracle (pinned to the reference's outputs, utils.py:77's finiteness semantics) holds
+    it on random NaN / inf placements; when the rule does not apply the triage leaves
+    the problem to the recompute (nothing to check)."""
+    rng = np.random.default_rng(77)
+    s, m, N = 4, 2, 12
+    checked = 0
+    for case in range(400):
+        A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_problem(900 + case, s, m, N)
+        A, Bm, Q, QT, z0, Ri = A.copy(), Bm.copy(), Q.copy(), QT.copy(), z0.copy(), Ri.copy()
+        for _ in range(int(rng.integers(1, 3))):
+            what = int(rng.integers(0, 6))
+            k = int(rng.integers(0, N))
+            val = [np.nan, np.inf, -np.inf][int(rng.integers(0, 3))]
+            i, j = int(rng.integers(0, s)), int(rng.integers(0, s))
+            if what == 0:
+                Q[k, i, j] = val
+            elif what == 1:
+                A[k, i, j] = val
+            elif what == 2:
+                Bm[k, i, j % m] = val
+            elif what == 3:
+                QT[k, i, j] = val
+            elif what == 4 and rng.random() < 0.2:
+                z0[i] = val
+            elif what == 5 and rng.random() < 0.2:
+                Ri[i % m, j % m] = val
+        bad = lambda x: not np.isfinite(x).all()  # noqa: E731
+        INF = N + 1
+        stage = [k for k in range(N) if bad(Q[k]) or bad(A[k]) or bad(Bm[k])]
+        h_poison = 1 if (bad(z0) or bad(Ri)) else (stage[0] + 1 if stage else INF)
+        qts = [k + 1 for k in range(N) if bad(QT[k])]
+        h_qt = qts[0] if qts else INF
+        h_nf = min(h_poison, h_qt)
+        if not (h_nf <= N and h_poison <= h_qt + 1):
+            continue
+        with np.errstate(invalid="ignore", over="ignore", divide="ignore"):
+            o = orc.lft_sweep(A, Bm, Q, Ri, z0, QT, N)
+        J = o["J"]
+        assert np.isfinite(J[:h_nf - 1]).all(), (case, h_nf, J)
+        assert np.isnan(J[h_nf - 1:]).all(), (case, h_nf, J)
+        assert int(o["status"]) == 4, (case, o["status"])
+        checked += 1
+    assert checked > 100
