@@ -28,6 +28,7 @@
 #ifndef HOP_H
 #define HOP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -85,6 +86,37 @@ const char* hop_last_error(void);
 #define HOP_OPT_STAMPS 16u
 #define HOP_OPT_NO_RERUN 32u
 #define HOP_ST_HANDOVER 16 /* status bit, set only under HOP_OPT_NO_RERUN */
+/*
+ * The hand-over word: the status a conditioned-prefix kernel leaves for a problem
+ * it hands to its rerun launch, read by that launch (the s = 13 fp64 non-finite
+ * triage) and returned to the caller only under HOP_OPT_NO_RERUN.  One definition
+ * for every kernel that writes or reads it (lft_sweep_v2.hip, lft_small.hip,
+ * small_math.hpp; tests/test_host_cpu.py decodes it from the host build):
+ *   HOP_ST_HANDOVER | (h << HOP_HANDOVER_SHIFT)
+ *   h = the first horizon (1-based) whose evaluation raised a flag of the
+ *       conditioned form (a first-attempt pivot, a non-positive Schur complement,
+ *       a non-finite J); 0 = flagged before horizon 1 (HOP_OPT_FORCE_HANDOVER);
+ *       clamped to HOP_HANDOVER_H_MAX (a clamped h only makes the triage decline)
+ *   developer builds under HOP_OPT_NO_RERUN also put the reason of the first flag
+ *   in bits HOP_HANDOVER_REASON_SHIFT .. HOP_HANDOVER_SHIFT - 1
+ */
+#define HOP_HANDOVER_SHIFT 13
+#define HOP_HANDOVER_H_MAX 262143 /* 2^18 - 1: h << 13 stays below the int32 sign bit */
+#define HOP_HANDOVER_REASON_SHIFT 5
+#define HOP_HANDOVER_WORD(h)                                                        \
+  (HOP_ST_HANDOVER | ((int32_t)((h) < HOP_HANDOVER_H_MAX ? (h) : HOP_HANDOVER_H_MAX) \
+                      << HOP_HANDOVER_SHIFT))
+#define HOP_HANDOVER_HORIZON(st) ((int32_t)((uint32_t)(st) >> HOP_HANDOVER_SHIFT))
+/*
+ * The triage rule (rerun launch of the s = 13 fp64 kernels): with h_poison = 1 +
+ * the first stage whose inputs are non-finite (1 for shared inputs), h_qt = the
+ * first horizon whose terminal block is non-finite (N + 1 if none) and h the
+ * hand-over word's horizon, the reference's outcome is the conditioned curve
+ * before min(h_poison, h_qt), NaN from there on, ST_NONFINITE, when
+ */
+#define HOP_TRIAGE_ACCEPTS(h, h_poison, h_qt, n_use)                                  \
+  (((h_poison) < (h_qt) ? (h_poison) : (h_qt)) <= (n_use) &&                          \
+   (h) >= ((h_poison) < (h_qt) ? (h_poison) : (h_qt)) && (h_poison) <= (h_qt) + 1)
 int hop_set_options(uint32_t flags, int32_t variant);
 int hop_get_options(uint32_t* flags, int32_t* variant); /* the calling thread's; nullable */
 int hop_build_flags(void); /* bit 0: developer build (A/B schedules and stamps compiled) */

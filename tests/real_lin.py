@@ -10,15 +10,24 @@ builders with the reference's q_reg = 1e-9, rho_reg = 1e-12
 argmin over [T_min, T_max].  Every stage runs on the device; the candidates
 compared on the same inputs are
 
-  traj      hop_lft_sweep_traj (the product select block; for s = 13 the
-            closed-form conditioned kernel + its rerun launch)
-  traj_ref  the same under HOP_OPT_REFERENCE_ASSOC (the reference association)
-  aug       hop_augment -> hop_lft_sweep (for s = 13 the conditioned kernel
-            on HBM blocks + its rerun launch)
+  traj      hop_lft_sweep_traj (the product select block: the conditioned
+            association + its rerun launch; s = 13 the closed-form kernel,
+            s <= 5 lft_small_traj_kernel<COND>)
+  traj_ref  the same under HOP_OPT_REFERENCE_ASSOC: the reference association
+            alone (s = 13 the trajectory LFT kernel, s <= 5 the LFT
+            instantiation of lft_small_traj_kernel)
+  aug       hop_augment -> hop_lft_sweep (the conditioned kernel on HBM blocks
+            + its rerun launch; since round 5 also for fp64 s <= 5)
   aug_ref   the same under HOP_OPT_REFERENCE_ASSOC
+  aug_gen   the same under HOP_OPT_FORCE_GENERIC (lft_sweep.hip, the reference
+            association: the fp64 s = 5 drop-in path of round 4)
   oracle    oracle/hop_oracle.py (the reference's association in NumPy, pinned
             by tests/golden) on a sample of problems, from the same device
             linearisation copied to the host
+
+None of these is ground truth on these inputs (fp64 evaluations of an
+ill-conditioned association); tools/real_lin_capture.py + tests/golden/
+make_hp_batch.py adjudicate their disagreements in 50-digit arithmetic.
 
 and the hand-over count of the conditioned kernels (HOP_OPT_NO_RERUN leaves
 HOP_ST_HANDOVER in status).
@@ -62,7 +71,7 @@ def build(name, Bn, seed, dev):
     lin = engine.linearize(F.system_id, X, Ut, F.dt, central=True)
     P = orc.terminal_weight(alpha, n)
     Ri = orc.spd_inverse(orc.sym(R))[0]
-    return dict(F=F, X=X, U=Ut, lin=lin, xg=xg, u_ref=u_ref, Q=Q, R=R, Ri=Ri, P=P, alpha=alpha,
+    return dict(F=F, X=X, U=Ut, X0=X0, U_np=U, lin=lin, xg=xg, u_ref=u_ref, Q=Q, R=R, Ri=Ri, P=P, alpha=alpha,
                 w=w, N=N, T_min=T_min, T_max=T_max, wrap=wrap, t=t)
 
 
@@ -92,6 +101,8 @@ def run(d, dev):
     with _lib.options(reference_assoc=True):
         out["traj_ref"] = traj()
         out["aug_ref"] = aug()
+    with _lib.options(force_generic=True):
+        out["aug_gen"] = aug()
     with _lib.options(no_rerun=True):
         ho_traj = traj().status
         ho_aug = aug().status
@@ -164,7 +175,7 @@ def compare(Ja, ta, Jb, tb, ok, T_min, T_max):
                 flip_examples=[(i, int(ta[i]), int(tb[i]), g) for i, g in zip(flips[:5], gaps)])
 
 
-def stats(name, Bn, seed, dev, n_oracle=32):
+def stats(name, Bn, seed, dev, n_oracle=32, want_raw=False):
     d = build(name, Bn, seed, dev)
     r = run(d, dev)
     T_min, T_max = d["T_min"], d["T_max"]
@@ -176,12 +187,18 @@ def stats(name, Bn, seed, dev, n_oracle=32):
     out = dict(system=name, batch=Bn, seed=seed, N=d["N"], s=d["F"].n + 1, m=d["F"].m,
                T_min=T_min, T_max=T_max, finite=int(ok.sum()),
                handover_traj=r["handover_traj"], handover_aug=r["handover_aug"])
-    for k in ("traj", "aug", "aug_ref"):
+    for k in ("traj", "aug", "aug_ref", "aug_gen"):
         J, ts, st = r[k]
         out[f"{k}_vs_traj_ref"] = compare(J, ts, Jr, tr, ok, T_min, T_max)
         out[f"{k}_status_equal"] = bool(np.array_equal(st[ok], sr[ok]))
+    # the two product entry points (trajectory form, augmented blocks) against each other
+    Jt, tt, _ = r["traj"]
+    for k in ("aug", "aug_gen"):
+        J, ts, _ = r[k]
+        out[f"{k}_vs_traj"] = compare(J, ts, Jt, tt, ok, T_min, T_max)
     hist = lambda st: {int(v): int(c) for v, c in zip(*np.unique(st[ok], return_counts=True))}  # noqa
-    out["status_hist"] = {k: hist(r[k][2]) for k in ("traj", "traj_ref", "aug", "aug_ref")}
+    out["status_hist"] = {k: hist(r[k][2]) for k in ("traj", "traj_ref", "aug", "aug_ref",
+                                                     "aug_gen")}
     # hand-overs the reference association finishes with status 0 (no jitter
     # escalation: a false positive of the conditioned form's own tests)
     for k in ("traj", "aug"):
@@ -198,7 +215,9 @@ def stats(name, Bn, seed, dev, n_oracle=32):
     sel = np.zeros(Bn, dtype=bool)
     for b, (J, ts, st) in zip(idx, orr):
         Jo[b], to[b], so[b], sel[b] = J, ts, st, True
-    for k in ("traj", "traj_ref", "aug"):
+    for k in ("traj", "traj_ref", "aug", "aug_gen"):
         J, ts, st = r[k]
         out[f"{k}_vs_oracle"] = compare(J, ts, Jo, to, sel, T_min, T_max)
+    if want_raw:
+        return out, dict(d=d, r=r, ok=ok, oracle_idx=idx, oracle_J=Jo[idx], oracle_t=to[idx])
     return out

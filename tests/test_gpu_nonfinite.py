@@ -48,6 +48,7 @@ def test_nonfinite_triage_augmented_blocks_vs_reference_association(dev):
     A, Bm, Q, QT = A.copy(), Bm.copy(), Q.copy(), QT.copy()
     rng = np.random.default_rng(5)
     kinds = np.arange(Bn) % 6
+    h_qt = np.zeros(Bn, np.int64)
     for b in range(Bn):
         k = int(rng.integers(1, N))
         i, j = int(rng.integers(0, s)), int(rng.integers(0, s))
@@ -55,6 +56,7 @@ def test_nonfinite_triage_augmented_blocks_vs_reference_association(dev):
             Q[b, k, i, j] = np.nan
         elif kinds[b] == 2:  # before the last horizon (J(N) alone would be explained)
             QT[b, min(k, N - 2), i, j] = np.nan
+            h_qt[b] = min(k, N - 2) + 1
         elif kinds[b] == 3:
             A[b, k, i, j] = np.inf
         elif kinds[b] == 4:
@@ -76,7 +78,11 @@ def test_nonfinite_triage_augmented_blocks_vs_reference_association(dev):
     handed = (ho & _lib.ST_HANDOVER) != 0
     # only the terminal-block-only kind is left to the recompute
     assert np.array_equal(handed, kinds == 2), np.nonzero(handed != (kinds == 2))[0][:8]
-    assert (ho[handed] == _lib.ST_HANDOVER).all() or _lib.dev_build()
+    # the hand-over word (include/hop.h): the bit, and the first flagged horizon = the
+    # poisoned terminal block's (developer builds add the reason field)
+    low = (1 << _lib.HANDOVER_SHIFT) - 1
+    assert ((ho[handed] & low) == _lib.ST_HANDOVER).all() or _lib.dev_build()
+    assert np.array_equal(_lib.handover_horizon(ho[handed]), h_qt[handed])
     assert (ho[kinds == 0] == 0).all()
 
 

@@ -565,9 +565,12 @@ def test_nonfinite_inputs_status_and_curve_match_oracle(dev, s, m):
     jitter ladder).  Every kernel family (s=13 default + rerun, generic s=8, small
     s=5/3) gives the oracle's exact status word and NaN pattern, the finite
     horizons to 1e-9: NaN in Q_k (every later horizon NaN), in QT_k (one horizon),
-    inf in A_k, NaN in z0, and an indefinite block beside them (jitter bits kept)."""
+    inf in A_k, NaN in z0, and an indefinite block beside them (jitter bits kept);
+    since round 5 also +inf on the diagonal of Q_k and of QT_k (an "infinite cost"
+    pivot, which an exact reciprocal would turn into a finite zero row: the
+    kernels' v_rcp + Newton gives NaN there, and the reference raises)."""
     from time_opt_ilqr_amd import engine
-    Bn, N = 6, 14
+    Bn, N = 8, 14
     A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(7070 + s, Bn, s, m, N)
     A, Q, QT, z0 = A.copy(), Q.copy(), QT.copy(), z0.copy()
     Q[0, 4, 1, 2] = np.nan
@@ -576,6 +579,8 @@ def test_nonfinite_inputs_status_and_curve_match_oracle(dev, s, m):
     z0[3, 1] = np.nan
     Q[4, 2] = Q[4, 2] - np.eye(s) * (np.linalg.eigvalsh(Q[4, 2]).min() + 5e-8)  # jitter
     Q[5, 9, s - 1, 0] = -np.inf
+    Q[6, 3, 1, 1] = np.inf
+    QT[7, 5, s - 1, s - 1] = np.inf
     res = engine.propagate(_t(A, dev), _t(Bm, dev), _t(Q, dev), _t(Ri, dev), _t(z0, dev),
                            _t(QT, dev))
     st = res.status.cpu().numpy()

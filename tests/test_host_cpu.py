@@ -55,7 +55,7 @@ def test_tile64_host_side_checks(lib):
                                 None, None, None)
     assert lib.hop_lft_sweep_tile64_f64(*args(13, 4)) == -2  # HOP_E_SIZE: s = 13
     assert b"tile64" in lib.hop_last_error()
-    assert lib.hop_lft_sweep_tile64_f64(*args(5, 1)) == -2  # no fp64 kernel at s = 5
+    assert lib.hop_lft_sweep_tile64_f64(*args(6, 1)) == -2  # no small-s kernel at s = 6
     assert lib.hop_lft_sweep_tile64_f32(*args(6, 1)) == -2
     assert lib.hop_tile64_f32(d, d, 5, 2, 0, 0, None) == -1  # elems < 1
 
@@ -954,3 +954,81 @@ def test_nonfinite_triage_rule_matches_oracle_semantics():
         assert int(o["status"]) == 4, (case, o["status"])
         checked += 1
     assert checked > 100
+
+
+def test_handover_word_is_defined_once_in_hop_h(small_host):
+    """The hand-over word (status bit 16 + the first flagged horizon at bits
+    HOP_HANDOVER_SHIFT.., include/hop.h) has one definition: the host build encodes /
+    decodes it with hop.h's macros (round trip, clamp below the sign bit), and no
+    kernel source packs or unpacks the field by hand (a literal shift by 13 or a
+    reason shift by 5 outside hop.h would be a second definition)."""
+    import re
+    for h in (0, 1, 2, 99, 100, 4096, 262142, 262143):
+        w = small_host.small_host_handover_word(h)
+        assert w & 16 and w >= 0
+        assert small_host.small_host_handover_horizon(w) == h
+    for h in (262144, 1 << 20, (1 << 31) - 1):
+        w = small_host.small_host_handover_word(h)
+        assert w >= 0 and small_host.small_host_handover_horizon(w) == 262143
+    csrc = os.path.join(REPO, "time_opt_ilqr_amd", "csrc")
+    for fn in os.listdir(csrc):
+        if not fn.endswith((".hip", ".hpp", ".cpp")):
+            continue
+        with open(os.path.join(csrc, fn)) as f:
+            src = f.read()
+        assert not re.search(r"(<<|>>)\s*13\b", src), fn
+        assert not re.search(r"why\s*<<\s*5\b", src), fn
+
+
+def test_handover_horizon_of_small_cond_math_vs_oracle_first_nonfinite(small_host):
+    """The conditioned small-s math (small_math.hpp, the COND kernels' arithmetic) hands
+    a problem with non-finite inputs over with the first flagged horizon in the word;
+    decoded with hop.h's definition it is the reference association's first non-finite
+    horizon (the oracle's J curve, pinned to the reference), and the conditioned J
+    before it is finite.  This is the field the s = 13 rerun launch's triage reads
+    (HOP_TRIAGE_ACCEPTS: it requires h >= the first poisoned horizon)."""
+    rng = np.random.default_rng(91)
+    s, m, N = 3, 1, 16
+    p = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
+    checked = 0
+    for case in range(300):
+        A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_problem(1300 + case, s, m, N)
+        A, Bm, Q, QT, z0, Ri = A.copy(), Bm.copy(), Q.copy(), QT.copy(), z0.copy(), Ri.copy()
+        what = int(rng.integers(0, 4))
+        k = int(rng.integers(0, N))
+        i, j = int(rng.integers(0, s)), int(rng.integers(0, s))
+        val = np.nan if rng.random() < 0.5 else np.inf * (1 if rng.random() < 0.5 else -1)
+        if what == 0:
+            Q[k, i, j] = val
+        elif what == 1:
+            A[k, i, j] = val
+        elif what == 2:
+            Bm[k, i, 0] = val
+        else:
+            QT[k, i, j] = val
+        with np.errstate(invalid="ignore", over="ignore", divide="ignore"):
+            o = orc.lft_sweep(A, Bm, Q, Ri, z0, QT, N)
+        nf = np.nonzero(~np.isfinite(o["J"]))[0]
+        if not len(nf):
+            continue
+        h_ref = int(nf[0]) + 1
+        J = np.zeros((1, N))
+        st, ts = np.zeros(1, np.int32), np.zeros(1, np.int32)
+        args = [np.ascontiguousarray(x, dtype=np.float64) for x in (A, Bm, Q, Ri[None], QT, z0[None])]
+        with np.errstate(invalid="ignore", over="ignore"):
+            assert small_host.small_host_cond_sweep_f64(*[p(x) for x in args], C.c_int64(1), N, s,
+                                                        m, 1, N, p(J), p(st), p(ts)) == 0
+        assert st[0] & 16, (case, what, val, h_ref)
+        h = small_host.small_host_handover_horizon(int(st[0]))
+        assert h == h_ref, (case, what, val, h, h_ref)
+        assert np.isfinite(J[0, :h - 1]).all(), (case, J[0])
+        # the triage's verdict on this shape: a poisoned stage k (h_poison = k + 1) makes
+        # every later horizon NaN and is accepted; a lone non-finite terminal block
+        # (h_qt = k + 1, later horizons finite again) is left to the recompute
+        h_poison = k + 1 if what < 3 else N + 1
+        h_qt = k + 1 if what == 3 else N + 1
+        want = 1 if (what < 3 or k == N - 1) else 0
+        assert small_host.small_host_triage_accepts(h, h_poison, h_qt, N) == want
+        assert small_host.small_host_triage_accepts(h - 1, h_poison, h_qt, N) == 0
+        checked += 1
+    assert checked > 150

@@ -158,6 +158,14 @@ OPT_TRAJ_UNFUSED = 8
 OPT_STAMPS = 16
 OPT_NO_RERUN = 32
 ST_HANDOVER = 16  # status bit left by the conditioned kernels under OPT_NO_RERUN
+# the hand-over word (include/hop.h): ST_HANDOVER | first flagged horizon << HANDOVER_SHIFT
+HANDOVER_SHIFT = 13
+
+
+def handover_horizon(status):
+    """The first flagged horizon of hand-over words (HOP_HANDOVER_HORIZON); works on
+    ints and integer arrays."""
+    return status >> HANDOVER_SHIFT
 
 
 def dev_build() -> bool:

@@ -65,8 +65,12 @@ struct Geo {
   static constexpr int PIECES = 3 * CM + CB;
   static constexpr int PIECE = 16 * PW;  // bytes per piece (one 16-B chunk per problem)
   static constexpr int WAVE_BYTES = PIECES * PIECE;
-  static constexpr int TPB = 256;  // 4 waves per block
-  static constexpr int PPB = 4 * PW;  // problems per block
+  // waves per block: 4, or as many as fit the CU's 160 KiB of LDS (fp64 s = 5: 42 KiB
+  // per wave of 64 problems, 3 waves per block)
+  static constexpr int WPB = (160 * 1024) / WAVE_BYTES < 4 ? (160 * 1024) / WAVE_BYTES : 4;
+  static_assert(WPB >= 1, "one wave's images must fit in LDS");
+  static constexpr int TPB = 64 * WPB;
+  static constexpr int PPB = WPB * PW;  // problems per block
   // tile64 layout: a block's 64 problems are 64 S S (64 S MM) contiguous elements;
   // lanes loading the last piece of a section (the rest would be the next step's)
   static constexpr int LAST_M = (64 * S * S * (int)sizeof(T) - (CM - 1) * 1024) / 16;
@@ -204,6 +208,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
   if constexpr (COND) {
     cond_init(cs, z);
     cs.bad = (a.cond & 2) != 0;
+    cs.kf1 = cs.bad ? 1 : 0;
   }
   T rinv[MM][MM];
   {
@@ -287,8 +292,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
 #pragma unroll
     for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
     jring[JR - 1] = jk;
-    if constexpr (COND) take(cs, k + 1, jk, a.t_min, a.t_max);
-    else take(ps, k + 1, jk, a.t_min, a.t_max);
+    if constexpr (COND) {
+      take(cs, k + 1, jk, a.t_min, a.t_max);
+      cond_mark(cs, k);
+    } else {
+      take(ps, k + 1, jk, a.t_min, a.t_max);
+    }
   }
   vm_wait();
   if (N > 0) {
@@ -297,7 +306,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
   }
   if (valid) {
     if constexpr (COND) {
-      a.status[prob] = (cs.bad || (cs.st & kStNonfinite)) ? 16 : 0;
+      a.status[prob] = cond_status_word(cs);
       if (a.t_max > 0 && a.t_star != nullptr) {
         a.t_star[prob] = cs.tbest;
         a.j_star[prob] = cs.best;
@@ -331,7 +340,7 @@ struct GeoT {
   static constexpr int P_A = 0, P_B = CA, P_X = CA + CB, P_V = P_X + CX, P_U = P_V + CX;
   static constexpr int PIECES = P_U + CU;
   static constexpr int WAVE_BYTES = PIECES * 1024;
-  static constexpr int TPB = 256;
+  static constexpr int WPB = 4, TPB = 256, PPB = 256;
   static constexpr int LAST_A = (64 * NN * NN * TS - (CA - 1) * 1024) / 16;
   static constexpr int LAST_B = (64 * NN * MM * TS - (CB - 1) * 1024) / 16;
   static constexpr int LAST_X = (64 * NN * TS - (CX - 1) * 1024) / 16;
@@ -477,6 +486,7 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
   if constexpr (COND) {
     cond_init(cs, z);
     cs.bad = (a.cond & 2) != 0;
+    cs.kf1 = cs.bad ? 1 : 0;
   }
   T rinv[MM][MM];  // R_inv_cached
   {
@@ -559,8 +569,12 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
 #pragma unroll
     for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];
     jring[JR - 1] = jk;
-    if constexpr (COND) take(cs, k + 1, jk, a.t_min, a.t_max);
-    else take(ps, k + 1, jk, a.t_min, a.t_max);
+    if constexpr (COND) {
+      take(cs, k + 1, jk, a.t_min, a.t_max);
+      cond_mark(cs, k);
+    } else {
+      take(ps, k + 1, jk, a.t_min, a.t_max);
+    }
 #pragma unroll
     for (int i = 0; i < NN; ++i) qe[i] = qe1[i];
     eqe = eqe1;
@@ -572,7 +586,7 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
   }
   if (valid) {
     if constexpr (COND) {
-      a.status[prob] = (cs.bad || (cs.st & kStNonfinite)) ? 16 : 0;
+      a.status[prob] = cond_status_word(cs);
       if (a.t_max > 0 && a.t_star != nullptr) {
         a.t_star[prob] = cs.tbest;
         a.j_star[prob] = cs.best;
@@ -585,6 +599,15 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
       }
     }
   }
+}
+
+// launch shape of a geometry: dynamic LDS per block, problems and threads per block
+struct LaunchGeo {
+  int bytes, ppb, tpb;
+};
+template <class G>
+constexpr LaunchGeo geo_of() {
+  return {G::WAVE_BYTES * G::WPB, G::PPB, G::TPB};
 }
 
 }  // namespace small
@@ -602,50 +625,48 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
   // the COND kernel alone, A/B) and the layout / occupancy experiments (72-78).
   // The conditioned step issues half the FLOPs but its loop-carried chain is no
   // shorter, and the stream, not the arithmetic, bounds this kernel
-  auto go1 = [&](auto kl, int bytes, int ppb = 256) {
-    const long long blocks = (a.batch + ppb - 1) / ppb;
-    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, a);
+  using small::LaunchGeo;
+  auto launch = [&](auto kern, LaunchGeo g, const LftArgs<T>& args) {
+    const long long blocks = (a.batch + g.ppb - 1) / g.ppb;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)g.tpb), (size_t)g.bytes, stream,
+                       args);
     return hipGetLastError();
   };
+  auto go1 = [&](auto kl, LaunchGeo g) { return launch(kl, g, a); };
 #ifdef HOP_DEV
-  const int cmode = (g_opt_variant == 61 || g_opt_variant == 73 ||
-                     (a.tile64 && sizeof(T) == 4 && g_opt_variant == 0))
-                        ? 1
-                        : g_opt_variant == 62 ? 2 : 0;
-  auto go2 = [&](auto kc, auto kl, int bytes, int ppb = 256) {
-    if (cmode == 0) return go1(kl, bytes, ppb);
-    const long long blocks = (a.batch + ppb - 1) / ppb;
+  // cmode 1: the product default (conditioned + rerun), 2: COND alone (62),
+  // 0: the LFT association alone (HOP_OPT_REFERENCE_ASSOC)
+  const int cmode = opt(HOP_OPT_REFERENCE_ASSOC) ? 0 : g_opt_variant == 62 ? 2 : 1;
+  auto go2 = [&](auto kc, auto kl, LaunchGeo g) {
+    if (cmode == 0) return go1(kl, g);
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
-    hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
-    if (cmode == 2 || opt(HOP_OPT_NO_RERUN)) return hipGetLastError();
+    const hipError_t e = launch(kc, g, c);
+    if (e != hipSuccess || cmode == 2 || opt(HOP_OPT_NO_RERUN)) return e;
     LftArgs<T> r = a;
     r.cond = 1;
-    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
-    return hipGetLastError();
+    return launch(kl, g, r);
   };
   // the trajectory form (both layouts): the conditioned association + the LFT rerun
   // (the product default); variant 79: the LFT association alone, 62: COND alone
-  auto go2t = [&](auto kc, auto kl, int bytes) {
-    const long long blocks = (a.batch + 255) / 256;
-    if (g_opt_variant == 79) return go1(kl, bytes);
+  auto go2t = [&](auto kc, auto kl, LaunchGeo g) {
+    if (g_opt_variant == 79 || opt(HOP_OPT_REFERENCE_ASSOC)) return go1(kl, g);
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;
-    hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
-    if (g_opt_variant == 62 || opt(HOP_OPT_NO_RERUN)) return hipGetLastError();
+    const hipError_t e = launch(kc, g, c);
+    if (e != hipSuccess || g_opt_variant == 62 || opt(HOP_OPT_NO_RERUN)) return e;
     LftArgs<T> r = a;
     r.cond = 1;
-    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
-    return hipGetLastError();
+    return launch(kl, g, r);
   };
 #define HOP_SMALL_TRAJ(S_, M_)                                                            \
   if (a.traj && a.s == S_ && a.m == M_)                                                   \
     return a.tile64 ? go2t(small::lft_small_traj_kernel<T, S_, M_, true, 2>,              \
                            small::lft_small_traj_kernel<T, S_, M_, false, 2>,             \
-                           small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                       \
+                           small::geo_of<small::GeoT<T, S_, M_>>())                       \
                     : go2t(small::lft_small_traj_kernel<T, S_, M_, true, 0>,              \
                            small::lft_small_traj_kernel<T, S_, M_, false, 0>,             \
-                           small::GeoT<T, S_, M_>::WAVE_BYTES * 4);
+                           small::geo_of<small::GeoT<T, S_, M_>>());
 #define HOP_SMALL_TRAJ_DEV(S_, M_) HOP_SMALL_TRAJ(S_, M_)
   // variant 72: 32 problems per wave (two waves per SIMD), A/B against 64;
   // 73: the conditioned association at 32 problems per wave + the rerun launch
@@ -653,84 +674,82 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
   if (a.s == S_ && a.m == M_) {                                                           \
     HOP_SMALL_TRAJ_DEV(S_, M_)                                                            \
     if (a.tile64) {                                                                       \
-      if (cmode != 0 || (sizeof(T) == 4 && g_opt_variant == 0))                           \
+      if (cmode != 0)                                                                     \
         return go2(small::lft_small_kernel<T, S_, M_, true, 64, 0, 2>,                    \
                    small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,                   \
-                   small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                \
+                   small::geo_of<small::Geo<T, S_, M_>>());                                \
       if (g_opt_variant == 78)                                                            \
         return go1(small::lft_small_kernel<T, S_, M_, false, 64, 1, 2>,                   \
-                   small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                \
+                   small::geo_of<small::Geo<T, S_, M_>>());                                \
       return go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,                     \
-                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+                 small::geo_of<small::Geo<T, S_, M_>>());                                  \
     }                                                                                     \
     if (!a.traj && g_opt_variant == 72)                                                   \
       return go1(small::lft_small_kernel<T, S_, M_, false, 32>,                           \
-                 small::Geo<T, S_, M_, 32>::WAVE_BYTES * 4, small::Geo<T, S_, M_, 32>::PPB); \
+                 small::geo_of<small::Geo<T, S_, M_, 32>>()); \
     if (!a.traj && (g_opt_variant == 74 || g_opt_variant == 75))                          \
       return go1(g_opt_variant == 74 ? small::lft_small_kernel<T, S_, M_, false, 64, 1>     \
                                      : small::lft_small_kernel<T, S_, M_, false, 64, 2>,    \
-                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+                 small::geo_of<small::Geo<T, S_, M_>>());                                  \
     if (!a.traj && g_opt_variant == 76)                                                   \
       return go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 0>,                     \
-                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+                 small::geo_of<small::Geo<T, S_, M_>>());                                  \
     if (!a.traj && g_opt_variant == 77)                                                   \
       return go1(small::lft_small_kernel<T, S_, M_, false, 64, 1, 1>,                     \
-                 small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                  \
+                 small::geo_of<small::Geo<T, S_, M_>>());                                  \
     if (!a.traj && g_opt_variant == 73)                                                   \
       return go2(small::lft_small_kernel<T, S_, M_, true, 32>,                            \
                  small::lft_small_kernel<T, S_, M_, false, 32>,                           \
-                 small::Geo<T, S_, M_, 32>::WAVE_BYTES * 4, small::Geo<T, S_, M_, 32>::PPB); \
+                 small::geo_of<small::Geo<T, S_, M_, 32>>()); \
     return go2(small::lft_small_kernel<T, S_, M_, true, 64, 0, 1>,                        \
                small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,                       \
-               small::Geo<T, S_, M_>::WAVE_BYTES * 4);                                   \
+               small::geo_of<small::Geo<T, S_, M_>>());                                   \
   }
 #else
-  // tile64 fp32: the conditioned association (half the FLOPs; its stream, not its
-  // arithmetic, is then the bound: config 3 0.83 ms against 0.91 for the LFT and
-  // 0.81 for the stream alone), then the LFT kernel in rerun mode for the problems
-  // it handed over (chol_inv ladders, status bits: the reference's semantics)
-  auto gocond = [&](auto kc, auto kl, int bytes) {
-    const long long blocks = (a.batch + 255) / 256;
+  // Every small-s shape, both layouts and both dtypes: the conditioned association
+  // (half the FLOPs; at config 3 its stream, not its arithmetic, is the bound:
+  // 0.83 ms against 0.91 for the LFT and 0.81 for the stream alone), then the LFT
+  // kernel in rerun mode for the problems it handed over (chol_inv ladders, status
+  // bits: the reference's semantics).  On real s = 5 linearisations at rho_reg =
+  // 1e-12 the conditioned form holds the 50-digit reference curve where the fp64
+  // reference association is 1e-2 .. 1 off, so augmented blocks and
+  // the trajectory form run the same arithmetic.  HOP_OPT_REFERENCE_ASSOC: the LFT
+  // kernel alone (the reference association; comparator for the tests and tools)
+  auto gocond = [&](auto kc, auto kl, LaunchGeo g) {
+    if (opt(HOP_OPT_REFERENCE_ASSOC)) return go1(kl, g);
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
-    hipLaunchKernelGGL(kc, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, c);
-    if (opt(HOP_OPT_NO_RERUN)) return hipGetLastError();  // flags left in status (tests)
+    const hipError_t e = launch(kc, g, c);
+    if (e != hipSuccess || opt(HOP_OPT_NO_RERUN)) return e;  // hand-over words left in status
     LftArgs<T> r = a;
     r.cond = 1;
-    hipLaunchKernelGGL(kl, dim3((unsigned)blocks), dim3(256), (size_t)bytes, stream, r);
-    return hipGetLastError();
+    return launch(kl, g, r);
   };
 #define HOP_SMALL_TRAJ(S_, M_)                                                            \
   if (a.traj && a.s == S_ && a.m == M_)                                                   \
     return a.tile64 ? gocond(small::lft_small_traj_kernel<T, S_, M_, true, 2>,            \
                              small::lft_small_traj_kernel<T, S_, M_, false, 2>,           \
-                             small::GeoT<T, S_, M_>::WAVE_BYTES * 4)                     \
+                             small::geo_of<small::GeoT<T, S_, M_>>())                     \
                     : gocond(small::lft_small_traj_kernel<T, S_, M_, true, 0>,            \
                              small::lft_small_traj_kernel<T, S_, M_, false, 0>,           \
-                             small::GeoT<T, S_, M_>::WAVE_BYTES * 4);
+                             small::geo_of<small::GeoT<T, S_, M_>>());
 #define HOP_SMALL(S_, M_)                                                                 \
   HOP_SMALL_TRAJ(S_, M_)                                                                  \
   if (a.s == S_ && a.m == M_) {                                                           \
-    if (a.tile64 && sizeof(T) == 4)                                                       \
-      return gocond(small::lft_small_kernel<T, S_, M_, true, 64, 0, 2>,                   \
-                    small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,                  \
-                    small::Geo<T, S_, M_>::WAVE_BYTES * 4);                               \
-    return a.tile64 ? go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,            \
-                          small::Geo<T, S_, M_>::WAVE_BYTES * 4)                         \
-                    : go1(small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,            \
-                          small::Geo<T, S_, M_>::WAVE_BYTES * 4);                        \
+    return a.tile64 ? gocond(small::lft_small_kernel<T, S_, M_, true, 64, 0, 2>,          \
+                             small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,         \
+                             small::geo_of<small::Geo<T, S_, M_>>())                      \
+                    : gocond(small::lft_small_kernel<T, S_, M_, true, 64, 0, 1>,          \
+                             small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,         \
+                             small::geo_of<small::Geo<T, S_, M_>>());                     \
   }
 #endif
   if constexpr (sizeof(T) == 4) {
     HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)
     HOP_SMALL(5, 2)  // s = 6 spills: generic kernel
   } else {
-    HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2)
-    // s = 5 fp64: the trajectory form only (the segway / cart-pole select on real
-    // linearisations, where the conditioned association holds 1e-9 of the 50-digit
-    // reference and the reference association 1e-2 .. 1); augmented blocks at s = 5
-    // fp64 stay on the generic kernel
-    HOP_SMALL_TRAJ(5, 1) HOP_SMALL_TRAJ(5, 2)
+    HOP_SMALL(2, 1) HOP_SMALL(3, 1) HOP_SMALL(4, 1) HOP_SMALL(4, 2) HOP_SMALL(5, 1)
+    HOP_SMALL(5, 2)
   }
 #undef HOP_SMALL
 #undef HOP_SMALL_TRAJ

@@ -1118,7 +1118,7 @@ __device__ __forceinline__ bool nonfinite_resolve(const LftArgs<double>& a, int 
   for (int gg = 0; gg < kProbPerWave; ++gg) {
     if (((nb >> (16 * gg)) & 0xffffull) == 0ull) continue;  // wave-uniform
     const long long pb = wave_prob0 + gg;
-    const int kf = __shfl(st_me, 16 * gg) >> 13;  // first flagged horizon (0: prologue / forced)
+    const int kf = HOP_HANDOVER_HORIZON(__shfl(st_me, 16 * gg));  // 0: prologue / forced
     int kS = INT_MAX, h_qt = INF;
     bool shared;
     if constexpr (TRAJ) {
@@ -1163,7 +1163,7 @@ __device__ __forceinline__ bool nonfinite_resolve(const LftArgs<double>& a, int 
     }
     const int h_poison = shared ? 1 : (kS != INT_MAX ? kS + 1 : INF);
     const int h_nf = h_poison < h_qt ? h_poison : h_qt;
-    const bool ok = h_nf <= N && kf >= h_nf && h_poison <= h_qt + 1;
+    const bool ok = HOP_TRIAGE_ACCEPTS(kf, h_poison, h_qt, N);
     if (ok) {  // wave-uniform
       double* J = a.J + pb * N;
       const double qnan = __builtin_nan("");
@@ -1271,10 +1271,7 @@ __device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
       const bool resolved = nonfinite_resolve<S, MM, TRAJ>(a, lane, g, wave_prob0, need, st_in);
       need = need && !resolved;
     }
-    if (a.cond & 8) {  // triage only (HOP_OPT_NO_RERUN): the rest keep the hand-over bit
-      if (need && c == 0 && !(a.cond & 4)) a.status[prob] = (int)ST_RERUN;
-      return;
-    }
+    if (a.cond & 8) return;  // triage only (HOP_OPT_NO_RERUN): the rest keep their hand-over word
     if (!__any(need)) return;  // wave-uniform; no workgroup barrier in this kernel
     valid = need;
   }
@@ -2037,7 +2034,11 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   // the first flagged horizon + 1 (0: none; 1: the prologue or a forced hand-over),
   // left in status bits 13.. for the rerun launch's non-finite triage
   int kf1 = bad ? 1 : 0;
-  int why = 0;  // developer builds: first failing test and horizon (see lft_cond_cf_kernel)
+  // developer builds: first failing test and horizon (see lft_cond_cf_kernel); stored
+  // at HOP_HANDOVER_REASON_SHIFT, which puts the horizon where the hand-over word has it
+  static_assert(HOP_HANDOVER_REASON_SHIFT + 8 == HOP_HANDOVER_SHIFT, "why = reason | t << 8");
+  static_assert(ST_RERUN == HOP_ST_HANDOVER, "the hand-over bit");
+  int why = 0;
   auto flag = [&](bool f, int bit, int t) {
     if constexpr (kDevBuild) why = (f && why == 0) ? (bit | (t << 8)) : why;
   };
@@ -2420,8 +2421,10 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   }
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = (T)jprev;
-    // fp32 blocks: their rerun (the generic kernel) has no triage, so no horizon bits
-    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : F32 ? 0 : (kf1 - 1) << 13) : 0;
+    // the hand-over word (include/hop.h); the developer reason field under cond & 4
+    a.status[prob] = bad ? ((a.cond & 4) ? (int)ST_RERUN | why << HOP_HANDOVER_REASON_SHIFT
+                                         : HOP_HANDOVER_WORD(kf1 - 1))
+                         : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = (T)best;
@@ -2773,7 +2776,9 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   dma_wait();
   if (valid && c == 0) {
     if (N > 0) a.J[prob * N + N - 1] = jprev;
-    a.status[prob] = bad ? (int)ST_RERUN | ((a.cond & 4) ? why << 5 : (kf1 - 1) << 13) : 0;
+    a.status[prob] = bad ? ((a.cond & 4) ? (int)ST_RERUN | why << HOP_HANDOVER_REASON_SHIFT
+                                         : HOP_HANDOVER_WORD(kf1 - 1))
+                         : 0;
     if (fuse_argmin && a.t_star != nullptr) {
       a.t_star[prob] = tbest;
       a.j_star[prob] = best;

@@ -5,8 +5,14 @@
 
 namespace hop {
 namespace small {
+// exact division, except where the device's v_rcp + Newton step (lft_small.hip) gives
+// NaN: d = 0 or +-inf (the residual fma(-d, rcp(d), 1) is 0 * inf there), so that a
+// non-finite or zero pivot poisons the host result exactly as it does on the device
 template <class T>
-inline T small_recip(T d) { return T(1) / d; }
+inline T small_recip(T d) {
+  const T r = T(1) / d;
+  return (d == T(0) || r == T(0) || r != r) ? T(__builtin_nan("")) : r;
+}
 }  // namespace small
 }  // namespace hop
 
@@ -50,8 +56,9 @@ static void run(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, 
   }
 }
 
-// conditioned-prefix path (lft_small.hip COND kernels): status = 16 when the
-// problem would be handed to the rerun launch
+// conditioned-prefix path (lft_small.hip COND kernels): status = the hand-over word
+// (HOP_HANDOVER_WORD of the first flagged horizon) when the problem would be handed
+// to the rerun launch
 template <class T, int S, int MM, bool DIRECT = false>
 static void run_cond(const T* A, const T* B, const T* Q, const T* Rinv, const T* QT, const T* z0,
                      int64_t batch, int n, int t_min, int t_max, T* J, int32_t* status,
@@ -82,8 +89,9 @@ static void run_cond(const T* A, const T* B, const T* Q, const T* Rinv, const T*
       const T jk = DIRECT ? cond_query_direct<T, S, MM>(cs, QTk) : cond_query<T, S, MM>(cs, QTk);
       J[b * n + k] = jk;
       take(cs, k + 1, jk, t_min, t_max);
+      cond_mark(cs, k);
     }
-    status[b] = (cs.bad || (cs.st & kStNonfinite)) ? 16 : 0;
+    status[b] = cond_status_word(cs);  // the kernels' hand-over word (include/hop.h)
     t_star[b] = cs.tbest;
   }
 }
@@ -156,4 +164,12 @@ extern "C" int small_host_lu_sym_solve_f64(const double* A, int n, double eps, c
       hop::lu_sym_solve<double, 16>([&](int i, int j) { return A[i * n + j]; }, n, eps, y);
   for (int i = 0; i < n; ++i) x[i] = y[i];
   return ok ? 0 : -1;
+}
+
+// the hand-over word's field and the triage rule as include/hop.h defines them (the
+// kernels use the same macros; tests/test_host_cpu.py decodes statuses with these)
+extern "C" int small_host_handover_horizon(int32_t status) { return HOP_HANDOVER_HORIZON(status); }
+extern "C" int small_host_handover_word(int32_t h) { return HOP_HANDOVER_WORD(h); }
+extern "C" int small_host_triage_accepts(int32_t h, int32_t h_poison, int32_t h_qt, int32_t n) {
+  return HOP_TRIAGE_ACCEPTS(h, h_poison, h_qt, n) ? 1 : 0;
 }

@@ -16,6 +16,7 @@
 #endif
 
 #include "lu_pivot.hpp"
+#include "../../include/hop.h"
 
 namespace hop {
 namespace small {
@@ -344,6 +345,7 @@ struct CondState {
   int tbest;
   unsigned st;
   bool bad;
+  int kf1;  // 1 + the first flagged horizon (0: none yet)
 };
 
 template <class T, int S, int MM>
@@ -360,6 +362,24 @@ HOP_HD inline void cond_init(CondState<T, S, MM>& c, const T (&z)[S]) {
   c.tbest = 0;
   c.st = 0;
   c.bad = false;
+  c.kf1 = 0;
+}
+
+// after horizon k + 1 is evaluated (and taken): the first horizon that raised a flag
+// (a pivot, a Schur complement, a non-finite J); a flag set before the sweep
+// (a forced hand-over) is horizon 0
+template <class T, int S, int MM>
+HOP_HD inline bool cond_flagged(const CondState<T, S, MM>& c) {
+  return c.bad || (c.st & kStNonfinite) != 0u;
+}
+template <class T, int S, int MM>
+HOP_HD inline void cond_mark(CondState<T, S, MM>& c, int k) {
+  if (cond_flagged(c) && c.kf1 == 0) c.kf1 = k + 2;
+}
+// the status the conditioned kernel leaves: 0, or the hand-over word (include/hop.h)
+template <class T, int S, int MM>
+HOP_HD inline int cond_status_word(const CondState<T, S, MM>& c) {
+  return cond_flagged(c) ? HOP_HANDOVER_WORD(c.kf1 > 0 ? c.kf1 - 1 : 0) : 0;
 }
 
 // (sym(M) + 1e-9 I)^-1 on the first attempt only (utils.py:69-93 without the ladder)
