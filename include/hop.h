@@ -63,8 +63,9 @@ const char* hop_last_error(void);
  *                           cross-check
  *   HOP_OPT_FORCE_HANDOVER  the conditioned-prefix kernels hand EVERY problem to
  *                           their rerun launch (tests the hand-over path)
- *   HOP_OPT_REFERENCE_ASSOC s = 13 fp64 / fp32: only the reference-association
- *                           kernel (no conditioned prefix)
+ *   HOP_OPT_REFERENCE_ASSOC only the reference-association kernel (no
+ *                           conditioned prefix): s = 13 fp64 / fp32 and every
+ *                           small-s shape (s <= 5, both layouts, both forms)
  *   HOP_OPT_TRAJ_UNFUSED    trajectory form through hop_augment + the sweep
  *   HOP_OPT_STAMPS          section-stamped instantiations (developer builds)
  *   HOP_OPT_NO_RERUN        the conditioned-prefix kernels run without the
@@ -178,8 +179,11 @@ int hop_lft_sweep_f32(const float* A_aug, const float* B_aug, const float* Q_aug
  * hop_lft_sweep_tile64_f64/_f32: hop_lft_sweep_* (same reference function,
  *   arguments and outputs) with A_aug, B_aug, Q_aug, QT_aug in tile64 layout;
  *   R (no per-step stride), z0 and every output as hop_lft_sweep_*.  Shapes with
- *   a small-s kernel only (fp32: s <= 5, m <= 2; fp64: s <= 4, m <= 2), else
- *   HOP_E_SIZE; padding slots are read but never reported.
+ *   a small-s kernel only (s <= 5, m <= 2, both dtypes), else HOP_E_SIZE; padding
+ *   slots are read but never reported.  Every small-s sweep (both layouts, both
+ *   dtypes, blocks and trajectory form) runs the conditioned association and then
+ *   the LFT kernel in rerun mode for the problems it hands over, as the s = 13
+ *   fp64 path does; HOP_OPT_REFERENCE_ASSOC runs the LFT kernel alone.
  */
 int64_t hop_tile64_elems(int64_t batch, int32_t n_alloc, int32_t elems);
 int hop_tile64_f64(const double* src, double* dst, int64_t batch, int32_t n_alloc, int32_t elems,
@@ -209,8 +213,8 @@ int hop_lft_sweep_tile64_f32(const float* A_aug, const float* B_aug, const float
  * A wave of 64 problems then streams each step's raw blocks as contiguous spans
  * (the batch-major raw arrays are 64 scattered rows per piece).  Shared inputs
  * (xg, u_ref, Q, P, w, R_inv) and every output as hop_lft_sweep_traj_*; no
- * extra_stage_cost.  Small-s shapes only (s = n + 1; fp32: s <= 5, m <= 2;
- * fp64: s <= 4, m <= 2), else HOP_E_SIZE.
+ * extra_stage_cost.  Small-s shapes only (s = n + 1 <= 5, m <= 2, both dtypes),
+ * else HOP_E_SIZE.
  */
 int hop_lft_sweep_traj_tile64_f64(const double* A, const double* Bm, const double* a_res,
                                   const double* X, const double* U, const double* xg,

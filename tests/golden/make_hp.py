@@ -59,20 +59,22 @@ CASES = {
 PER_SYSTEM = 3
 
 
-def hp_curve(Aa, Ba, Qa, Ri, z0, QT, N):
-    """horizon_selection.py:36-86 (the reference association) in 50-digit arithmetic."""
+def hp_curve(Aa, Ba, Qa, Ri, z0, QT, N, eps_E=None):
+    """horizon_selection.py:36-86 (the reference association) in 50-digit arithmetic.
+    eps_E: {k: jitter} for stage inverses E_k = chol_inv(Q_k) that the fp64 reference
+    escalated (the jitter its ladder settled on, utils.py:81-93); 1e-9 elsewhere."""
     M = lambda a: mp.matrix(np.asarray(a, dtype=float).tolist())  # noqa: E731
     eps = mp.mpf("1e-9")
 
-    def inv(X):
+    def inv(X, e=eps):
         X = (X + X.T) / 2
-        return (X + eps * mp.eye(X.rows)) ** -1
+        return (X + e * mp.eye(X.rows)) ** -1
 
     Ri_m, z = M(Ri), M(np.asarray(z0).reshape(-1, 1))
     J = []
     for k in range(N):
         Ak, Bk = M(Aa[k]), M(Ba[k])
-        Ek = inv(M(Qa[k]))
+        Ek = inv(M(Qa[k]), mp.mpf(eps_E[k]) if eps_E and k in eps_E else eps)
         Fk = Ek * Ak.T
         Gk = Ak * Ek * Ak.T + Bk * Ri_m * Bk.T
         Gk = (Gk + Gk.T) / 2
@@ -147,5 +149,26 @@ def main():
     np.savez_compressed(os.path.join(HERE, "real_lin_hp.npz"), **d)
 
 
+def legacy_twin():
+    """legacy_twin_hp.npz: the 50-digit curve of the escalated legacy-twin problem
+    (tests/golden/legacy_twin_cases.npz, problem 0 of each tag: Q_4 needs the 1e-7
+    jitter, ilqr_propagator.py:21-31), whose later horizons the fp64 reference itself
+    gets only to ~5e-2 (E_4 ~ 2e7, cancelled by the compose)."""
+    d = np.load(os.path.join(HERE, "legacy_twin_cases.npz"))
+    out = {}
+    for tag, s, m, N in (("s13_m4_N20", 13, 4, 20), ("s5_m1_N20", 5, 1, 20)):
+        A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(int(d[f"{tag}_base_seed"]), 3, s, m, N)
+        Q = Q.copy()
+        Q[0, 4] = d[f"{tag}_Q04"]
+        Jh = hp_curve(A[0], Bm[0], Q[0], Ri[0], z0[0], QT[0], N, eps_E={4: "1e-7"})
+        out[f"{tag}_J_hp"] = Jh
+        rel = np.max(np.abs(d[f"{tag}_J"][0] - Jh) / np.abs(Jh))
+        print(f"{tag}: fp64 reference vs 50-digit {rel:.2e}")
+    np.savez_compressed(os.path.join(HERE, "legacy_twin_hp.npz"), **out)
+
+
 if __name__ == "__main__":
-    main()
+    if "--legacy-twin" in sys.argv:
+        legacy_twin()
+    else:
+        main()

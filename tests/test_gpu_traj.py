@@ -399,13 +399,14 @@ def test_linearize_tile64_equals_batch_major(dev, sid, central):
         assert torch.equal(engine.from_tile64(t.U)[:, :n_use, :, 0], Ut[:, :n_use].to(odt))
 
 
-@pytest.mark.parametrize("n,m,dt", [(4, 1, "f32"), (4, 2, "f32"), (2, 1, "f64"), (3, 1, "f64")])
+@pytest.mark.parametrize("n,m,dt", [(4, 1, "f32"), (4, 2, "f32"), (2, 1, "f64"), (3, 1, "f64"),
+                                    (4, 1, "f64"), (4, 2, "f64")])
 def test_traj_tile64_equals_batch_major_and_oracle(dev, n, m, dt):
     """hop_lft_sweep_traj_tile64_* on tile64 raw arrays (a ragged 67-problem batch):
-    fp64 (the LFT association on both layouts) bitwise the batch-major trajectory
-    kernel's J / T* / status; fp32 (tile64: the conditioned association + the LFT
-    rerun, as the augmented tile64 sweep) within the fp32 bar of it, T* equal except
-    at near-ties; the oracle on a sample at the fp64 / fp32 bars."""
+    fp64 (the conditioned association + the LFT rerun on both layouts, s up to 5)
+    bitwise the batch-major trajectory kernel's J / T* / status; fp32 (the same
+    association) within the fp32 bar of it, T* equal except at near-ties; the oracle
+    on a sample at the fp64 / fp32 bars."""
     import torch
     from time_opt_ilqr_amd import engine
     dtype = torch.float64 if dt == "f64" else torch.float32

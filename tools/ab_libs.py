@@ -37,6 +37,9 @@ def main():
                                                       t_max=200).J
     c2 = synth.device_batch(4096, 13, 4, 100, seed=4, device=dev)
     work["config2"] = lambda: engine.propagate(*c2, t_min=40, t_max=100).J
+    if "config4_shard" in args.only.split(","):  # 15 GB of blocks: only on request
+        c4 = synth.device_batch(32768, 13, 4, 100, seed=5, device=dev)
+        work["config4_shard"] = lambda: engine.propagate(*c4, t_min=40, t_max=100).J
     g = torch.Generator(device=dev)
     g.manual_seed(3)
     n, m, N, Bn = 12, 4, 100, 4096

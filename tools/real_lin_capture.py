@@ -11,7 +11,7 @@ aug_ref, aug_gen, a 32-problem oracle sample) and keeps, per system:
   bit 4   T* of aug_ref != traj
   bit 8   T* of aug (augmented blocks, product) != traj
   bit 16  T* of the oracle sample != traj or != aug_gen
-  bit 32  the largest J disagreement (aug_gen / traj_ref against traj)
+  bit 32  the largest J disagreement (aug_gen / traj_ref / aug against traj)
   bit 64  a seeded random sample of the finite problems
 
 (at most `cap` problems of each flip set, seeded), with the exact fp64 inputs the
@@ -66,7 +66,7 @@ for seed, name in enumerate(real_lin.SYSTEMS):
     n_flip["oracle"] = pick(om, 16)
     sl = slice(T_min - 1, T_max)
     Jt = r["traj"][0][:, sl]
-    for k in ("aug_gen", "traj_ref"):
+    for k in ("aug_gen", "traj_ref", "aug"):
         rel = np.max(np.abs(r[k][0][:, sl] - Jt) / np.maximum(np.abs(Jt), 1e-300), axis=1)
         rel[~ok] = -1
         why[int(np.argmax(rel))] |= 32
