@@ -54,14 +54,27 @@ def baseline_metric():
         return "batched iLQR backward sweeps/sec, Quadrotor n=13 N=100, at 1/2/4/8 GPU"
 
 
-def kernel_path(s, m, dtype, batch=4096):
+def _cu_count():
+    """CUs of the current device, as the library's dispatcher sees them (its cu_count
+    reads hipDeviceAttributeMultiprocessorCount; 256 if unknown, as the library)."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return int(torch.cuda.get_device_properties(torch.cuda.current_device())
+                       .multi_processor_count)
+    except Exception:  # noqa: BLE001 - a CPU dry run
+        pass
+    return 256
+
+
+def kernel_path(s, m, dtype, batch=4096, cus=None):
     """Which kernel libhop_amd.so dispatches for this shape, and its roofline bound.
     The s=13 kernels are compute-bound on the fp64 pipe (MI355X: vector fp64 peak ==
     matrix fp64 peak); they issue DPP-broadcast FMAs, not MFMA.  Above
-    one wave per SIMD (4 problems per wave, 4 x 256 SIMDs) the s=13 fp64 path takes the
+    one wave per SIMD (4 problems per wave, 4 SIMDs per CU) the s=13 fp64 path takes the
     packed two-waves-per-SIMD layout."""
     if dtype == "f64" and (s, m) == (13, 4):
-        packed = (batch + 3) // 4 > 4 * 256
+        packed = (batch + 3) // 4 > 4 * (cus or _cu_count())
         return f"lft_cond_kernel<{'SchedCondLSymP' if packed else 'SchedCondLSymL'},13,4>", "fp64"
     if dtype == "f32" and (s, m) == (13, 4):
         return "lft_cond_kernel<SchedCond,13,4,float>", "fp64"  # fp32 blocks, fp64 arithmetic

@@ -147,7 +147,16 @@ int hop_cu_fallbacks(void); /* CU-count queries that failed and assumed 256 (lay
  *   s = 13, m = 4, fp64, no debug outputs: two stream-ordered launches, the
  *          conditioned-prefix kernel (z0 folded into the prefix first, same J to
  *          ~1e-12) and a rerun of the problems it could not take with the
- *          reference association (status and failure semantics unchanged).
+ *          reference association (status and failure semantics unchanged): the
+ *          rerun launch first resolves hand-overs explained by non-finite inputs
+ *          (HOP_TRIAGE_ACCEPTS), then recomputes the rest, up to four problems per
+ *          workgroup of sixteen as a pipeline over the workgroup's four waves
+ *          (stage blocks and queries on four rows at once, the compose chain on two
+ *          waves), more with the one-wave LFT kernel's code; either way bitwise the
+ *          reference-association kernel's J, status, T* and J*.
+ *   s <= 5 (both dtypes, m <= 2): the one-problem-per-lane kernels, the
+ *          conditioned association and then the LFT kernel in rerun mode for the
+ *          problems it hands over.
  */
 int hop_lft_sweep_f64(const double* A_aug, const double* B_aug, const double* Q_aug,
                       const double* R, int64_t r_batch_stride, int64_t r_step_stride,

@@ -103,6 +103,7 @@ struct SchedStamped : SchedLdl {
 // linearisation each step (augmented.py:10-87), see the TRAJ paths below
 struct SchedLdlTraj : SchedLdl {
   static constexpr int TRAJ = 1;
+  static constexpr int SCALE = 1;  // equilibrated Gauss-Jordan inverses (see sweep)
 };
 struct SchedLdlTrajStamped : SchedLdlTraj {
   static constexpr int STAMP = 1;
@@ -110,6 +111,7 @@ struct SchedLdlTrajStamped : SchedLdlTraj {
 // the step's 20 LDS-DMA pieces issued from one asm block (dma_step20)
 struct SchedLdlDma : SchedLdl {
   static constexpr int DMA1 = 1;
+  static constexpr int SCALE = 1;  // equilibrated Gauss-Jordan inverses (see sweep)
 };
 struct SchedLdlDmaStamped : SchedLdlDma {
   static constexpr int STAMP = 1;
@@ -118,6 +120,7 @@ struct SchedLdlDmaStamped : SchedLdlDma {
 // dependent DPP chain per output row, rows of A_k read from the image with A^T's
 struct SchedCond : SchedLdlDma {
   static constexpr int AROW = 1;
+  static constexpr int SCALE = 0;  // first attempts only: its own sweeps (rerun on doubt)
 };
 // + the QT image reads under the E sweep, the A/B reads under the X sweep
 struct SchedCondL : SchedCond {
@@ -252,6 +255,7 @@ constexpr bool has_arow() {
 }
 // conditioned-prefix kernel on the trajectory form (lft_cond_kernel)
 struct SchedCondTraj : SchedLdlDma {
+  static constexpr int SCALE = 0;
   static constexpr int TRAJ = 1;
 };
 // fused hand-over: a wave whose problems the conditioned kernel flagged recomputes
@@ -339,9 +343,52 @@ __device__ __forceinline__ bool pivots_ok(const double (&r)[S], double dmin) {
   return (dmin > 0.0) && (x == x);
 }
 
+template <class C>
+constexpr bool has_scale() {
+  if constexpr (requires { C::SCALE; }) return C::SCALE != 0;
+  return false;
+}
+
+// The offset-form Gauss-Jordan sweep updates column p at pivot p as x (1 - (d-1)/d):
+// that cancels to an absolute error of u in the factor, u d relative, so a pivot
+// d >> 1 costs its column u d of accuracy, and every later step carries it.  The
+// reference-association kernel (the rerun of the conditioned kernels' hand-overs and
+// HOP_OPT_REFERENCE_ASSOC) meets such pivots after an escalated stage: E_k ~ 1e6 puts
+// pivots of that size into W = (E_k + Gbar)^-1, and J drifted 0.12 away from the
+// 50-digit value within 20 steps where NumPy's Cholesky inverses stay at 3e-4
+// (round 5, tools/dump_escalation_case.py; a NumPy model of the sweep reproduces the
+// 0.12).  SCALE schedules invert the equilibrated D (M + eps I) D, D = diag(M + eps
+// I)^-1/2, instead: unit diagonal, so every pivot of the SPD case is <= 1, and
+// (M + eps I)^-1 = D M'^-1 D.  The pivots keep their signs (Cholesky's test is
+// unchanged) and the rows stay independent (the retry ladder's bitwise property).
+template <int S>
+__device__ __forceinline__ void sweep_equilibrated(double (&r)[S], double& dmin, int c) {
+  double dg = 0.0;  // lane c: the offset diagonal entry r[c][c] = M_cc + eps - 1
+  static_for<S>([&](auto I) { dg = (c == (int)I) ? r[I] : dg; });
+  const double dd = 1.0 + dg;
+  const double Dc = c < S ? 1.0 / __builtin_sqrt(dd) : 0.0;  // NaN when not positive
+  // the diagonal of M' - I is 0, or NaN for an infinite M_cc (its D_c = 0 would
+  // otherwise turn the +inf into an identity row the sweep accepts, where Cholesky
+  // and the unscaled sweep fail: the ladder and the LU slot, as utils.py:69-93)
+  const double z = 0.0 * dd;
+  static_for<S>([&](auto I) {
+    const double v = (r[I] * Dc) * bcast<I>(Dc);
+    r[I] = (c == (int)I) ? z : v;  // M' - I: unit diagonal
+  });
+  SweepQ<S>::run(r, dmin);
+  static_for<S>([&](auto I) {  // -M^-1 + I = D (R' - I) D + I
+    const double v = ((r[I] - ((c == (int)I) ? 1.0 : 0.0)) * Dc) * bcast<I>(Dc);
+    r[I] = (c == (int)I) ? v + 1.0 : v;
+  });
+}
+
 template <class C, int S>
 __device__ __forceinline__ void sweep(double (&r)[S], double eps, bool& ok) {
-  if constexpr (C::PIV == 5) {
+  if constexpr (C::PIV == 5 && has_scale<C>()) {
+    double dmin = 1.0;
+    sweep_equilibrated<S>(r, dmin, (int)(threadIdx.x & 15));
+    ok = ok && pivots_ok(r, dmin);
+  } else if constexpr (C::PIV == 5) {
     double dmin = 1.0;
     SweepQ<S>::run(r, dmin);
     ok = ok && pivots_ok(r, dmin);
@@ -710,14 +757,17 @@ __device__ __forceinline__ void neg_inverse_reg(double (&r)[S], double* tile, in
 
 // Products: with the pad-free schedules only the first broadcast block of a
 // product is padded (its source may have just been written); later blocks
-// read the same, unchanged source registers.
+// read the same, unchanged source registers.  The SCALE schedules (the
+// reference-association kernels) run near the register limit, where the
+// compiler may reload a later block's source from an AGPR right before it:
+// every block is padded there (the build's hazard check found one).
 template <class C, bool NEG, int S, int K>
 __device__ __forceinline__ void gxy(double (&out)[S], const double (&x)[S], const double (&y)[K]) {
   if constexpr (C::XYROW) {
     // out[i] += sum_j bcast_j(x_i) y_j: the accumulator is forwarded between
     // consecutive FMAs (4.0 cycles each vs 4.9 for 13 independent accumulators)
     static_for<S>([&](auto I) {
-      if constexpr (I == 0) {
+      if constexpr (I == 0 || has_scale<C>()) {
         if constexpr (NEG) LaneDot<K>::fma_neg(out[I], x[I], y);
         else LaneDot<K>::fma(out[I], x[I], y);
       } else {
@@ -727,7 +777,7 @@ __device__ __forceinline__ void gxy(double (&out)[S], const double (&x)[S], cons
     });
   } else if constexpr (offset_form<C>()) {
     static_for<K>([&](auto J) {
-      if constexpr (J == 0) {
+      if constexpr (J == 0 || has_scale<C>()) {
         if constexpr (NEG) RowB<S>::template fma_neg<J>(out, x, y[J]);
         else RowB<S>::template fma<J>(out, x, y[J]);
       } else {
@@ -743,7 +793,7 @@ template <class C, bool NEG, int S, int K>
 __device__ __forceinline__ void gxty(double (&out)[S], const double (&x)[K], const double (&y)[K]) {
   if constexpr (offset_form<C>()) {
     static_for<K>([&](auto J) {
-      if constexpr (J == 0) {
+      if constexpr (J == 0 || has_scale<C>()) {
         if constexpr (NEG) LaneB<S>::fma_neg(out, x[J], y[J]);
         else LaneB<S>::fma(out, x[J], y[J]);
       } else {
@@ -1829,8 +1879,10 @@ template <class C, int S, int MM, int BS>
 __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long p) {
   using PG = PipeGeo<S, MM, BS>;
   using G = Geo<S, MM>;
-  static_assert(C::ELIM && has_qldl<C>() && offset_form<C>() && !has_traj<C>(),
-                "the LFT kernel's augmented-block schedule (SchedLdlDma)");
+  constexpr bool TRAJ = has_traj<C>();
+  static_assert(C::ELIM && has_qldl<C>() && offset_form<C>(),
+                "the LFT kernel's schedules (SchedLdlDma, SchedLdlTraj)");
+  constexpr int NN = S - 1;
   static_assert(PG::BYTES <= 160 * 1024, "one workgroup's LDS");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   unsigned char* base = smem_raw;
@@ -1845,10 +1897,9 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
 #pragma unroll 1
     for (int i = tid; i < nz; i += 256) z[i] = 0.0;
     __syncthreads();
-    const double* zp = a.z0 + p * a.z_bstride;
-    if (tid < 12 * S) {
+    if (tid < 12 * S) {  // the trajectory form's z0 is e_s (augmented.py:57)
       double* t = reinterpret_cast<double*>(base + PG::OFF_TILE) + (tid / S) * kLdsTile;
-      t[S * kLdsRow + tid % S] = zp[tid % S];
+      t[S * kLdsRow + tid % S] = TRAJ ? (tid % S == NN ? 1.0 : 0.0) : a.z0[p * a.z_bstride + tid % S];
     }
     if (tid == 0) *reinterpret_cast<int*>(base + PG::OFF_MISC + 64) = 0;  // status word
     __syncthreads();
@@ -1860,6 +1911,36 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
 #pragma unroll
     for (int i = 0; i < MM; ++i) rinv[i] = (c < MM) ? Rp[i * MM + (c < MM ? c : 0)] : 0.0;
   }
+  // trajectory form (the LFT kernel's TRAJ path, lft_v2_body): per-lane constants of
+  // the in-kernel builders (augmented.py:31-56, 77-86); each row builds its step's
+  // Q_aug / QT_aug image from them and the raw x_k, A_k, B_k, a_k, u_k
+  const bool in = c < NN;
+  const int cc = in ? c : 0, cm = c < MM ? c : 0;
+  double xg_c = 0.0, ur_c = 0.0, w2 = 0.0, qdiag = 0.0, pdiag = 0.0;
+  bool wrap_c = false;
+  const double* Qg = nullptr;
+  const double* Pg = nullptr;
+  const double* Xp = nullptr;
+  if constexpr (TRAJ) {
+    const TrajArgs<double>& t = a.tr;
+    Qg = t.Q + p * t.q_bs;
+    Pg = t.P + p * t.p_bs;
+    Xp = t.X + p * (long long)(a.nalloc + 1) * NN;
+    xg_c = in ? t.xg[p * t.xg_bs + cc] : 0.0;
+    ur_c = c < MM ? t.u_ref[p * t.ur_bs + cm] : 0.0;
+    w2 = 2.0 * t.w[p * t.w_bs];
+    wrap_c = in && ((t.wrap_mask >> c) & 1u);
+    qdiag = (0.5 * (Qg[cc * NN + cc] + Qg[cc * NN + cc]) + t.q_reg) + (1e-9 - 1.0);
+    pdiag = Pg[cc * NN + cc] + (1e-9 - 1.0);
+  }
+  auto err = [&](double x) {  // wrap_error(x - xg) on lane c (utils.py:131-137)
+    double e = in ? x - xg_c : 0.0;
+    if (a.tr.wrap_mask != 0u) {
+      const double we = wrap_angle(e);
+      e = wrap_c ? we : e;
+    }
+    return e;
+  };
   const int tw = w == 3 ? 2 : w;  // tile set of waves 0, 1, 3
   double* tile = reinterpret_cast<double*>(base + PG::OFF_TILE) + (tw * 4 + g) * kLdsTile;
   double* imQ = reinterpret_cast<double*>(base + PG::OFF_IQ + g * G::IMGM);
@@ -1876,7 +1957,66 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
   for (int b = 0; b < nb + 3; ++b) {
     if (w == 2) {  // ---- stage blocks of beat b, one step per row
       const int k = BS * b + g % BS, kc = k < N ? k : N - 1;
-      if (b < nb) {
+      if (b < nb && TRAJ) {
+        // Q_aug[k]: _sym(Q) + q_reg I, its bordered row / column Q e_k, corner
+        // e_k^T Q e_k + 2w + rho (the LFT kernel's values: Q e_k by the same 4-way split
+        // LaneDot4, the diagonal with the offset form's eps - 1 folded in); A~ row c
+        const TrajArgs<double>& t = a.tr;
+        const double* ar = t.A + (pk0 + kc) * NN * NN;
+        const double* br = t.Bm + (pk0 + kc) * NN * MM;
+        double qr[NN], qs[NN], at[S], brow[MM], rb[MM];
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+          qr[j] = in ? Qg[cc * NN + j] : 0.0;
+          qs[j] = 0.5 * (Qg[j * NN + cc] + Qg[cc * NN + j]) + (j == c ? t.q_reg : 0.0);
+          at[j] = in ? ar[cc * NN + j] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < MM; ++q) {
+          rb[q] = in ? br[cc * MM + q] : 0.0;
+          brow[q] = rb[q];
+        }
+        const double e0 = err(Xp[(long long)kc * NN + cc]);
+        const double uu = t.U[(pk0 + kc) * MM + cm];
+        const double av = in ? t.ares[(pk0 + kc) * NN + cc] : 0.0;
+        double q4[4] = {0.0, 0.0, 0.0, 0.0};
+        LaneDot4<NN>::fma(q4, e0, qr);
+        const double qe = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+        const double eqe = lane_sum<NN>(e0 * qe);
+        const double du = c < MM ? uu - ur_c : 0.0;
+        double bd = 0.0;
+        LaneDot<MM>::fma(bd, du, rb);  // (B du)[c]
+        const double atil = av - bd;
+        at[NN] = in ? atil : (c == NN ? 1.0 : 0.0);
+        if (in) {
+#pragma unroll
+          for (int i = 0; i < NN; ++i) imQ[i * S + c] = qs[i];
+          imQ[c * S + NN] = qe;
+          imQ[NN * S + c] = qe;
+          imQ[c * S + c] = qdiag;
+        } else if (c == NN) {
+          imQ[NN * S + NN] = ((eqe + w2) + t.rho_reg) + (1e-9 - 1.0);
+        }
+        wave_sync();
+        double NE[S];
+        neg_inverse<C, S, S>(NE, imQ, c, mt, st);
+        double F[S];
+        copy(F, at);
+        gxy<C, true>(F, NE, at);    // F = E A^T
+        double Gk[S];
+        zero(Gk);
+        gxty<C, false>(Gk, at, F);  // A F
+        double y[MM];
+        zero(y);
+        acc_xy<false, double, MM, MM>(y, rinv, brow);
+        acc_xty<false, double, S, MM>(Gk, brow, y);  // + B R^-1 B^T
+        if (k < N && g < BS) {
+          ring_put<S>(base, PG::OFF_NE, k % (PG::D_NE * BS), c, NE);
+          ring_put<S>(base, PG::OFF_F, k % (PG::D_F * BS), c, F);
+          ring_put<S>(base, PG::OFF_GK, k % (PG::D_GK * BS), c, Gk);
+        }
+        wave_sync();
+      } else if (b < nb) {
         const double* q = a.Q + (pk0 + kc) * SS;
         const double* am = a.A + (pk0 + kc) * SS;
         const double* bm = a.B + (pk0 + kc) * SM;
@@ -1998,16 +2138,42 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
       const int jb = b - 3;
       if (jb >= 0 && jb < nb) {
         const int k = BS * jb + g % BS, kc = k < N ? k : N - 1;
-        const double* qt = a.QT + (pk0 + kc) * SS;
-        constexpr int NQ = (SS + 15) / 16;
-        double vt[NQ];
+        if constexpr (TRAJ) {
+          // QT_aug[k] (horizon k + 1, e_{k+1}): P, its border P e, corner e^T P e + rho
+          const TrajArgs<double>& t = a.tr;
+          double pr[NN], ps[NN];
 #pragma unroll
-        for (int u = 0; u < NQ; ++u) vt[u] = qt[c + 16 * u < SS ? c + 16 * u : SS - 1];
+          for (int j = 0; j < NN; ++j) {
+            pr[j] = in ? Pg[j * NN + cc] : 0.0;  // column c of P (the LFT kernel's image reads)
+            ps[j] = Pg[j * NN + cc];
+          }
+          const double e1 = err(Xp[(long long)(kc + 1) * NN + cc]);
+          double p4[4] = {0.0, 0.0, 0.0, 0.0};
+          LaneDot4<NN>::fma(p4, e1, pr);
+          const double pe = (p4[0] + p4[1]) + (p4[2] + p4[3]);
+          const double epe = lane_sum<NN>(e1 * pe);
+          if (in) {
 #pragma unroll
-        for (int u = 0; u < NQ; ++u)
-          if (c + 16 * u < SS) imT[c + 16 * u] = vt[u];
-        wave_sync();
-        diag_add<S, S>(imT, c, 1e-9 - 1.0);
+            for (int i = 0; i < NN; ++i) imT[i * S + c] = ps[i];
+            imT[c * S + NN] = pe;
+            imT[NN * S + c] = pe;
+            imT[c * S + c] = pdiag;
+          } else if (c == NN) {
+            imT[NN * S + NN] = (epe + t.rho_reg) + (1e-9 - 1.0);
+          }
+          wave_sync();
+        } else {
+          const double* qt = a.QT + (pk0 + kc) * SS;
+          constexpr int NQ = (SS + 15) / 16;
+          double vt[NQ];
+#pragma unroll
+          for (int u = 0; u < NQ; ++u) vt[u] = qt[c + 16 * u < SS ? c + 16 * u : SS - 1];
+#pragma unroll
+          for (int u = 0; u < NQ; ++u)
+            if (c + 16 * u < SS) imT[c + 16 * u] = vt[u];
+          wave_sync();
+          diag_add<S, S>(imT, c, 1e-9 - 1.0);
+        }
         double NX[S], Gq[S], Eq[S], Hq[S];
         neg_inverse<C, S, S>(NX, imT, c, mt, st);
         ring_get<S>(base, PG::OFF_GB, kc % (PG::D_GB * BS), c, Gq);
@@ -2065,7 +2231,8 @@ __global__ __launch_bounds__(256, 1) void lft_rerun_pipe_kernel(LftArgs<double> 
   const int st_in = valid ? a.status[prob] : 0;
   bool need = valid && (st_in & (int)ST_RERUN);
   if (!(a.cond & 16) && __any(need)) {  // the whole wave (lane-0 writes, shuffles)
-    const bool resolved = nonfinite_resolve<S, MM, false>(a, lane, g, wave_prob0, need, st_in);
+    const bool resolved =
+        nonfinite_resolve<S, MM, has_traj<C>()>(a, lane, g, wave_prob0, need, st_in);
     need = need && !resolved;
   }
   int* flags = reinterpret_cast<int*>(smem_raw + PG::OFF_MISC);
@@ -3286,9 +3453,22 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return launch(v2::lft_cond_cf_kernel<v2::SchedCondTrajF, 13, 4>, bytes, c);
     }
 #endif
-    // default: closed-form stage inverses + rerun
-    return cond_rerun(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>,
-                      v2::lft_sweep_v2_kernel<v2::SchedLdlTraj, 13, 4>, bytes, true);
+    // default: closed-form stage inverses, then the pipelined rerun
+    {
+      using PipeT = v2::PipeGeo<13, 4, v2::kPipeBS>;
+      constexpr size_t bytes_pt = (size_t)PipeT::BYTES > (size_t)v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock
+                                      ? (size_t)PipeT::BYTES
+                                      : (size_t)v2::Geo<13, 4>::WAVE_BYTES_T * kWavesPerBlock;
+      static_assert(bytes_pt <= 160 * 1024, "one workgroup per CU");
+      LftArgs<double> c = a;
+      const bool force = opt(HOP_OPT_FORCE_HANDOVER);
+      c.cond = (force ? 2 : 0) | why_bit;
+      const hipError_t e = launch(v2::lft_cond_cf_kernel<v2::SchedCondTraj, 13, 4>, bytes, c);
+      if (e != hipSuccess) return e;
+      LftArgs<double> r = a;
+      r.cond = 1 | (force ? 16 : 0) | (opt(HOP_OPT_NO_RERUN) ? 8 | why_bit : 0);
+      return launch(v2::lft_rerun_pipe_kernel<v2::SchedLdlTraj, 13, 4, v2::kPipeBS>, bytes_pt, r);
+    }
   }
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
   constexpr size_t bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;

@@ -723,6 +723,7 @@ class Linearization:
     Fx: "object" = None  # [B, N, n] F(x_k, u_k) (want_fx=True)
     X: "object" = None   # tile64=True: the trajectory's x_k (k <= n_use) as Tile64
     U: "object" = None   # tile64=True: u_k (k < n_use) as Tile64
+    n_use: Optional[int] = None  # steps written (the rest of the tile64 arrays are zero)
 
 
 def linearize(system, X, U, dt: float, *, central: bool = False, n_use: Optional[int] = None,
@@ -737,15 +738,15 @@ def linearize(system, X, U, dt: float, *, central: bool = False, n_use: Optional
     tile64_dtype, default fp64; computed in fp64) -- the layout the small-s
     trajectory-form select streams (propagate_traj on Tile64 inputs)."""
     torch = _torch()
+    X = _dev(X, "X", torch.float64)
+    U = _dev(U, "U", torch.float64, X.device)
+    if X.dim() == 2:  # one problem [N+1, n]: a batch of one (both layouts)
+        X, U = X[None], U[None]
     if tile64:
         return _linearize_tile64(system, X, U, dt, central, n_use, epsx, epsu, relx, relu,
                                  tile64_dtype or torch.float64)
     sid = system_id(system)
     n, m = system_dims(sid)
-    X = _dev(X, "X", torch.float64)
-    U = _dev(U, "U", torch.float64, X.device)
-    if X.dim() == 2:
-        X, U = X[None], U[None]
     if X.dim() != 3 or U.dim() != 3 or X.shape[-1] != n or U.shape[-1] != m:
         raise ValueError(f"X must be [B, N+1, {n}] and U [B, N, {m}] for system {sid}")
     Bn, N = U.shape[0], U.shape[1]
@@ -764,7 +765,7 @@ def linearize(system, X, U, dt: float, *, central: bool = False, n_use: Optional
                                        float(relu), _lib.ptr(A), _lib.ptr(Bm), _lib.ptr(a_res),
                                        _lib.ptr(Fx), _lib.stream_handle(dev))
     _lib.check(rc)
-    return Linearization(A, Bm, a_res, Fx)
+    return Linearization(A, Bm, a_res, Fx, n_use=n_use)
 
 
 def _linearize_tile64(system, X, U, dt, central, n_use, epsx, epsu, relx, relu, odt):
@@ -785,7 +786,10 @@ def _linearize_tile64(system, X, U, dt, central, n_use, epsx, epsu, relx, relu, 
         raise TypeError("tile64_dtype must be float64 or float32")
     dev = X.device
     nt = (Bn + 63) // 64
-    mk = lambda steps, e: torch.empty((nt, steps, e, 64), dtype=odt, device=dev)  # noqa: E731
+    # steps >= n_use are not written: zero them (a later propagate_traj with its default
+    # n_use = N then streams zeros, not uninitialised memory)
+    alloc = torch.empty if n_use == N else torch.zeros
+    mk = lambda steps, e: alloc((nt, steps, e, 64), dtype=odt, device=dev)  # noqa: E731
     A, Bm, ar, Xt, Ut = mk(N, n * n), mk(N, n * m), mk(N, n), mk(N + 1, n), mk(N, m)
     fn = _lib.load().hop_linearize_tile64_f64 if odt == torch.float64 else \
         _lib.load().hop_linearize_tile64_f32
@@ -794,7 +798,7 @@ def _linearize_tile64(system, X, U, dt, central, n_use, epsx, epsu, relx, relu, 
             _lib.ptr(ar), _lib.ptr(Xt), _lib.ptr(Ut), _lib.stream_handle(dev))
     _lib.check(rc)
     return Linearization(Tile64(A, Bn, n, n), Tile64(Bm, Bn, n, m), Tile64(ar, Bn, n, 1), None,
-                         Tile64(Xt, Bn, n, 1), Tile64(Ut, Bn, m, 1))
+                         Tile64(Xt, Bn, n, 1), Tile64(Ut, Bn, m, 1), n_use=n_use)
 
 
 def dynamics(system, X, U, dt: float):
