@@ -396,6 +396,77 @@ def _quad_side(Bn, N, t_min, dev):
                      "and finite curve")}
 
 
+def _s5_aug_side(dev, Bn=4096, N=200, t_min=40):
+    """fp64 s = 5 augmented blocks, timed beside the config-2 line:
+    Bn perturbed cart-pole rollouts (systems.py:57-112 maker: its Q with the zero angle
+    weight, R, alpha, w, the angle wrap), central-difference linearisation
+    (linearization.py:177-211), the reference's builders on the device (augmented.py:
+    10-87, hop_augment_f64, rho_reg = 1e-12), then propagator_all_Jt_aug + argmin on
+    those blocks (horizon_selection.py:36-86, solver.py:521): the drop-in's path, the
+    small-s conditioned kernel + its rerun launch (hop_lft_sweep_f64).  `select_aug`
+    times the sweep alone, `augment_select_aug` the builders too; `select_aug_reference_
+    assoc` the same sweep with the reference association (HOP_OPT_REFERENCE_ASSOC); the
+    T* agreement with the trajectory-form select (hop_lft_sweep_traj_f64) on the same
+    linearisation is counted."""
+    import numpy as np
+    import torch
+    from time_opt_ilqr_amd import _lib, engine, systems
+    from time_opt_ilqr_amd.utils import as_terminal_weight
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap, _ = systems.make_cartpole_swingup(N=N)
+    g = torch.Generator(device=dev)
+    g.manual_seed(29)
+    kw = dict(device=dev, dtype=torch.float64, generator=g)
+    U = torch.as_tensor(u_ref, device=dev) + 2.0 * torch.randn((Bn, N, F.m), **kw)
+    X = engine.rollout(F.system_id, torch.as_tensor(x0, device=dev) +
+                       0.3 * torch.randn((Bn, F.n), **kw), U, F.dt)
+    t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
+    P = t(as_terminal_weight(alpha, F.n))
+    Ri = torch.linalg.inv(t(R))
+    lin = engine.linearize(F.system_id, X, U, F.dt, central=True)
+    shared = (t(xg), t(u_ref), t(Q))
+
+    def build():
+        return engine.augment(lin.A, lin.B, lin.a_res, X, U, *shared, P, w, wrap_idx=wrap)
+
+    blk = build()
+
+    def sweep(b):
+        return engine.propagate(b.A, b.B, b.Q, Ri, b.z0, b.QT, t_min=t_min, t_max=N)
+
+    def timed(fn, opts=None):
+        with _lib.options(**(opts or {})):
+            r_ = fn()
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+        return r_, e0.elapsed_time(e1) / 10
+
+    out = {}
+    r_a, ms = timed(lambda: sweep(blk))
+    for key, fn, opts in (("select_aug", None, None),
+                          ("augment_select_aug", lambda: sweep(build()), None),
+                          ("select_aug_reference_assoc", lambda: sweep(blk),
+                           {"reference_assoc": True})):
+        r_, ms_ = (r_a, ms) if fn is None else timed(fn, opts)
+        fin = torch.isfinite(r_.J).all(dim=1)
+        out[key] = {"ms": ms_, "sweeps_per_s": Bn / (ms_ * 1e-3),
+                    "problems_status_ok": int(((r_.status == 0) & fin).sum().item())}
+    tr = engine.propagate_traj(lin.A, lin.B, lin.a_res, X, U, *shared, Ri, P, w, wrap_idx=wrap,
+                               t_min=t_min, t_max=N)
+    torch.cuda.synchronize()
+    ok = torch.isfinite(r_a.J).all(dim=1) & torch.isfinite(tr.J).all(dim=1)
+    out["t_star_equal_traj_form"] = int(((r_a.t_star == tr.t_star) & ok).sum().item())
+    out["problems_finite_both"] = int(ok.sum().item())
+    out["workload"] = (f"fp64 s = 5, m = 1, N = {N}, B = {Bn}: cart-pole augmented blocks "
+                       "(rho_reg = 1e-12) through propagator_all_Jt_aug + argmin")
+    return out
+
+
 def _config5_workload(args, world, lo, hi, dev):
     import torch
     from time_opt_ilqr_amd import engine, synth
@@ -862,6 +933,12 @@ def main(argv=None):
         side_fig = (sd["name"], side_fig)
         info["side"] = None
 
+    # side figure: fp64 s = 5 augmented blocks (the drop-in's path at the cart-pole shape)
+    s5_aug = None
+    if (rank == 0 and world == 1 and wl == "lft" and (args.s, args.m, args.dtype) == (13, 4, "f64")
+            and not args.no_alt):
+        s5_aug = _s5_aug_side(dev)
+
     # side figure: the same sweep on batch-major blocks (tile64 runs only)
     alt_ms = None
     if rank == 0 and info.get("alt") is not None and not args.no_alt:
@@ -965,6 +1042,7 @@ def main(argv=None):
             "config4_shard_anchor": anchor,
             "config4_global_1gpu": anchor_g,
             **({side_fig[0]: side_fig[1]} if side_fig else {}),
+            **({"s5_f64_aug_blocks": s5_aug} if s5_aug else {}),
             "status_ok": status_ok,
         }
         print(json.dumps(line), flush=True)

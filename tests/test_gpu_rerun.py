@@ -117,7 +117,7 @@ def test_pipelined_rerun_several_per_workgroup_and_nonfinite(dev):
     """Workgroups with 1, 2, 4 and 5 escalated problems (the last above kPipeMax:
     the LFT body) and one with a non-finite stage beside an escalated one (the triage
     resolves the first, the pipeline the second), on the trajectory-free blocks path:
-    bitwise the reference-association kernel on every problem."""
+    bitwise the reference-association kernel on every recomputed problem."""
     import torch
     from time_opt_ilqr_amd import _lib, engine
     Bn, s, m, N = 96, 13, 4, 30
@@ -133,10 +133,15 @@ def test_pipelined_rerun_several_per_workgroup_and_nonfinite(dev):
     with _lib.options(reference_assoc=True):
         ref = engine.propagate(*args, **kw)
     torch.cuda.synchronize()
-    # the handed-over problems: bitwise; the rest keep the conditioned kernel's curve
-    # (the same J to ~1e-12) and status 0, as the reference-association kernel's
-    _same(res, ref, esc + [66])
+    # the recomputed problems: bitwise.  Problem 66's hand-over is explained by its
+    # non-finite stage: the triage keeps the conditioned kernel's finite prefix (J to
+    # ~1e-12 of the reference association) and NaN from the poisoned horizon on, with
+    # the reference's status word and argmin (tests/test_gpu_nonfinite.py); the rest
+    # keep the conditioned curve and status 0
+    _same(res, ref, esc)
     assert torch.equal(res.status, ref.status)
+    assert torch.equal(res.J[66].isnan(), ref.J[66].isnan()) and bool(res.J[66].isnan().any())
+    assert int(res.t_star[66]) == int(ref.t_star[66])
     rel = ((res.J - ref.J).abs() / ref.J.abs()).nan_to_num(0.0)
     assert float(rel.max()) <= 1e-9
 

@@ -35,6 +35,16 @@ __device__ __forceinline__ double small_recip(double d) {
 namespace hop {
 namespace small {
 
+// fp32 blocks (config 3's tile64 path): the query eliminates Sigma_eps + X_t directly
+// (round 3's cond_query_direct).  The congruence form exists for the augmented
+// terminal block's rho_reg = 1e-12 (sigma ~ 1e-9), which fp32 blocks cannot carry
+// anyway; on fp32 it only cost config 3 1.8 %.  The
+// fp64 kernels and the trajectory form keep the congruence query.
+#ifndef HOP_SMALL_F32_DIRECT
+#define HOP_SMALL_F32_DIRECT 1
+#endif
+constexpr bool kSmallF32Direct = HOP_SMALL_F32_DIRECT != 0;
+
 // One 16-B chunk per lane into LDS.  The blocks are read exactly once, so the
 // stream is non-temporal (nt): config 3 (B = 65536, N = 200, fp32 tile64) takes
 // 0.777 ms against 0.873 ms with the default policy (tools/ab_libs.py, same
@@ -287,7 +297,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
       for (int i = 0; i < S; ++i)
 #pragma unroll
         for (int j = 0; j < S; ++j) jk += QT.a[i][j];
-    } else if constexpr (COND) jk = cond_query<T, S, MM>(cs, QT);
+    } else if constexpr (COND) {
+      if constexpr (std::is_same_v<T, float> && kSmallF32Direct)
+        jk = cond_query_direct<T, S, MM>(cs, QT);
+      else
+        jk = cond_query<T, S, MM>(cs, QT);
+    }
     else jk = query<T, S, MM>(ps, QT, z, mt);
 #pragma unroll
     for (int i = 0; i + 1 < JR; ++i) jring[i] = jring[i + 1];

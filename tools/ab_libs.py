@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--only", default="", help="comma list of workloads")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warm", type=int, default=10, help="untimed launches after a workload switch")
     args = ap.parse_args()
     import torch
     from time_opt_ilqr_amd import _lib, engine, synth
@@ -101,8 +102,12 @@ def main():
     torch.cuda.synchronize()
     for rnd in range(args.rounds):
         for w, f in work.items():
-            # alternate the order every round: the first library timed after a
-            # workload switch measured up to 4 % faster either way (round 3)
+            # a workload switch changes the clocks: run it untimed first (round 5: the
+            # first library timed after a switch came out up to 12 % off either way)
+            _lib._lib = libs[0]
+            for _ in range(args.warm):
+                f()
+            # alternate the order every round as well
             for i in (range(L) if rnd % 2 == 0 else reversed(range(L))):
                 _lib._lib = libs[i]
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -117,7 +122,15 @@ def main():
              for i in range(L)}
         same = all(torch.equal(outs[(w, 0)].nan_to_num(7.0), outs[(w, i)].nan_to_num(7.0))
                    for i in range(1, L))
-        print(json.dumps({"workload": w, "ms": r, "bitwise_equal": same}), flush=True)
+        lo = {os.path.basename(args.libs[i]): round(min(times[(w, i)]), 4) for i in range(L)}
+        # per-round ratios to the first library: clock drift between rounds cancels
+        ratio = {os.path.basename(args.libs[i]): round(statistics.median(
+            [a / b for a, b in zip(times[(w, i)], times[(w, 0)])]), 4) for i in range(L)}
+        rounds = {os.path.basename(args.libs[i]): [round(x, 4) for x in times[(w, i)]]
+                  for i in range(L)}
+        print(json.dumps({"workload": w, "ms": r, "min_ms": lo, "ratio_to_first": ratio,
+                          "bitwise_equal": same,
+                          "rounds": rounds}), flush=True)
 
 
 if __name__ == "__main__":
