@@ -75,7 +75,12 @@ def check_hazards(objdir, verbose=True):
         n, bad = chk.check(s)
         if verbose:
             print(f"[hop] {os.path.basename(s)}: {n} DPP instructions, {len(bad)} hazards")
-        if bad:
+        report = os.environ.get("HOP_HAZARD_REPORT")  # developer A/B builds only: list, don't fail
+        if bad and report:
+            with open(report, "a") as f:
+                for fn, text, why in bad:
+                    f.write(f"{src}\t{fn}\t{text}\t{why}\n")
+        elif bad:
             raise RuntimeError(f"DPP hazard in {src}: {bad[:3]}")
 
 
