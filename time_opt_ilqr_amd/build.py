@@ -27,6 +27,11 @@ if DEV:  # a separate library (load it with HOP_LIB=<path>): the product .so sta
 EXTRA = {}
 HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hpp", "wrap.hpp", "dynamics.hpp"]
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
+# device code from its assembly, minus the DPP hazard pads the compiled code does not
+# need (tools/nop_elide.py); HOP_NO_ELIDE=1 compiles the plain way (hipcc -c)
+ELIDE = os.environ.get("HOP_NO_ELIDE", "0") in ("", "0") and os.path.exists(
+    os.path.join(REPO, "tools", "nop_elide.py"))
+LLVM_BIN = os.environ.get("HOP_LLVM_BIN", "/opt/rocm/lib/llvm/bin")
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",
          "-Wno-unused-but-set-variable"] + (["-DHOP_DEV=1"] if DEV else [])
 
@@ -49,6 +54,10 @@ def _digest():
             h.update(f.read())
     with open(os.path.join(REPO, "include", "hop.h"), "rb") as f:
         h.update(f.read())
+    if ELIDE:  # the device code is what tools/nop_elide.py leaves of the compiler's
+        with open(os.path.join(REPO, "tools", "nop_elide.py"), "rb") as f:
+            h.update(f.read())
+    h.update(b"elide" if ELIDE else b"plain")
     h.update(" ".join(FLAGS).encode())
     h.update(repr(sorted(EXTRA.items())).encode())
     return h.hexdigest()
@@ -84,6 +93,58 @@ def check_hazards(objdir, verbose=True):
             raise RuntimeError(f"DPP hazard in {src}: {bad[:3]}")
 
 
+def _run_all(cmds, verbose):
+    procs = []
+    for cmd in cmds:
+        if verbose:
+            print("[hop]", " ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+    for cmd, p in zip(cmds, procs):
+        if p.wait() != 0:
+            raise RuntimeError(f"build step failed: {' '.join(cmd[:3])} ...")
+
+
+def _compile_elided(hipcc, objdir, objs, verbose):
+    """Each source: the device assembly (hipcc --cuda-device-only -S), the hazard pads
+    it does not need dropped (tools/nop_elide.py), the hazard check on the result,
+    assembled and linked into the code object, bundled, and the host side compiled
+    around that fat binary (-fcuda-include-gpubinary: hipcc's own -c does the same
+    steps with the assembly unchanged)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import check_dpp_hazards as chk
+    import nop_elide
+    base = {src: os.path.join(objdir, src.replace(".hip", "")) for src in _sources()}
+    _run_all([[hipcc, *FLAGS, *EXTRA.get(src, []), "--cuda-device-only", "-S",
+               os.path.join(CSRC, src), "-o", base[src] + "-device-raw.s"]
+              for src in _sources()], verbose)
+    for src in _sources():
+        b = base[src]
+        checked = b + f"-hip-amdgcn-amd-amdhsa-{ARCH}.s"  # the name check_hazards reads
+        with open(b + "-device-raw.s") as f:
+            lines = f.read().split("\n")
+        out, dropped, kept = nop_elide.elide(lines, chk)
+        with open(checked, "w") as f:
+            f.write("\n".join(out))
+        if verbose:
+            print(f"[hop] {src}: {dropped} hazard-pad pairs dropped, {kept} kept")
+    check_hazards(objdir, verbose)
+    for src in _sources():
+        b = base[src]
+        checked = b + f"-hip-amdgcn-amd-amdhsa-{ARCH}.s"
+        for cmd in ([os.path.join(LLVM_BIN, "clang"), "-x", "assembler", "--target=amdgcn-amd-amdhsa",
+                     f"-mcpu={ARCH}", "-c", checked, "-o", b + "-device.o"],
+                    [os.path.join(LLVM_BIN, "lld"), "-flavor", "gnu", "-m", "elf64_amdgpu",
+                     "--no-undefined", "-shared", "-o", b + "-device.out", b + "-device.o"],
+                    [os.path.join(LLVM_BIN, "clang-offload-bundler"), "-type=o", "-bundle-align=4096",
+                     f"-targets=host-x86_64-unknown-linux-gnu,hipv4-amdgcn-amd-amdhsa--{ARCH}",
+                     "-input=/dev/null", "-input=" + b + "-device.out", "-output=" + b + ".hipfb"]):
+            subprocess.check_call(cmd)
+    _run_all([[hipcc, *FLAGS, *EXTRA.get(src, []), "--cuda-host-only", "-Xclang",
+               "-fcuda-include-gpubinary", "-Xclang", base[src] + ".hipfb", "-c",
+               os.path.join(CSRC, src), "-o", obj]
+              for src, obj in zip(_sources(), objs)], verbose)
+
+
 def build(force=False, jobs=None, verbose=True):
     """Compile every .hip source for gfx950 and link libhop_amd.so."""
     gen = os.path.join(REPO, "tools", "gen_dpp.py")
@@ -97,21 +158,22 @@ def build(force=False, jobs=None, verbose=True):
     hipcc = _hipcc()
     objdir = os.path.join(HERE, "_obj_dev" if DEV else "_obj")
     os.makedirs(objdir, exist_ok=True)
-    procs = []
-    objs = []
-    for src in _sources():
-        obj = os.path.join(objdir, src.replace(".hip", ".o"))
-        objs.append(obj)
-        # -save-temps=obj keeps the device assembly for the DPP hazard check
-        cmd = [hipcc, *FLAGS, *EXTRA.get(src, []), "-save-temps=obj", "-c",
-               os.path.join(CSRC, src), "-o", obj]
-        if verbose:
-            print("[hop]", " ".join(cmd))
-        procs.append(subprocess.Popen(cmd))
-    for p in procs:
-        if p.wait() != 0:
-            raise RuntimeError("hipcc failed")
-    check_hazards(objdir, verbose)
+    objs = [os.path.join(objdir, src.replace(".hip", ".o")) for src in _sources()]
+    if ELIDE:
+        _compile_elided(hipcc, objdir, objs, verbose)
+    else:
+        procs = []
+        for src, obj in zip(_sources(), objs):
+            # -save-temps=obj keeps the device assembly for the DPP hazard check
+            cmd = [hipcc, *FLAGS, *EXTRA.get(src, []), "-save-temps=obj", "-c",
+                   os.path.join(CSRC, src), "-o", obj]
+            if verbose:
+                print("[hop]", " ".join(cmd))
+            procs.append(subprocess.Popen(cmd))
+        for p in procs:
+            if p.wait() != 0:
+                raise RuntimeError("hipcc failed")
+        check_hazards(objdir, verbose)
     tmp = LIB + ".tmp"
     cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
     if verbose:
