@@ -841,7 +841,19 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
 
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Trajectory form: the step's 10 raw pieces (A 5, B 2, x, a, u) in one asm block
+// The LDS-DMA instruction offset is added to both addresses: the LDS destination is
+// M0 + offset + 16 lane and the memory address voffset + soffset + offset (measured,
+// tools/ubench/lds_dma_offset.hip, a wrapped voffset included).  So one M0 serves the
+// pieces of an image that lie within the 12-bit offset field: piece j of an image at
+// M0 = image + 4096 (j / 4), offset 1024 (j % 4), its voffset lowered by that offset
+// once at kernel start (dma_voff_lowered).  Two M0 writes per 6-piece image instead of
+// six, each with the wait state an M0 write needs before an LDS-DMA.
+__device__ __forceinline__ unsigned dma_voff_lowered(unsigned voff, int j) {
+  return voff - 1024u * (unsigned)(j % 4);
+}
+
+// Trajectory form: the step's 10 raw pieces (A 5, B 2, x, a, u) in one asm block;
+// va / vb lowered (dma_voff_lowered)
 template <int OA, int OB, int OX, int OV, int OU>
 __device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsigned (&vb)[2],
                                            unsigned vx, unsigned vv, unsigned vu,
@@ -850,28 +862,28 @@ __device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsign
                                            __amdgpu_buffer_rsrc_t rU, unsigned wlds, unsigned sA,
                                            unsigned sB, unsigned sX, unsigned sV, unsigned sU) {
   unsigned keep;
-#define HOP_P(R, V, OFF, SO)                                                  \
-  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
-  "], %[" #SO "] offen lds\n\t"
+#define HOP_M0(OFF) "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\t"
+#define HOP_PO(R, V, SO, IO) "buffer_load_dwordx4 %[" #V "], %[" #R "], %[" #SO "] offen offset:" #IO " lds\n\t"
   asm volatile(
-      ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
+      ".p2align 3\n\t"
       "s_mov_b32 %[keep], m0\n\t"
-      "s_nop 0\n\t"
-      HOP_P(ra, a0, %[o0], sa) HOP_P(ra, a1, %[o1], sa) HOP_P(ra, a2, %[o2], sa)
-      HOP_P(ra, a3, %[o3], sa) HOP_P(ra, a4, %[o4], sa)
-      HOP_P(rb, b0, %[p0], sb) HOP_P(rb, b1, %[p1], sb)
-      HOP_P(rx, x0, %[ox], sx) HOP_P(rv, x1, %[ov], sv) HOP_P(ru, x2, %[ou], su)
+      HOP_M0(%[o0]) HOP_PO(ra, a0, sa, 0) HOP_PO(ra, a1, sa, 1024) HOP_PO(ra, a2, sa, 2048)
+      HOP_PO(ra, a3, sa, 3072)
+      HOP_M0(%[o4]) HOP_PO(ra, a4, sa, 0)
+      HOP_M0(%[p0]) HOP_PO(rb, b0, sb, 0) HOP_PO(rb, b1, sb, 1024)
+      HOP_M0(%[ox]) HOP_PO(rx, x0, sx, 0)
+      HOP_M0(%[ov]) HOP_PO(rv, x1, sv, 0)
+      HOP_M0(%[ou]) HOP_PO(ru, x2, su, 0)
       "s_mov_b32 m0, %[keep]"
       : [keep] "=&s"(keep)
       : [w] "s"(wlds), [sa] "s"(sA), [sb] "s"(sB), [sx] "s"(sX), [sv] "s"(sV), [su] "s"(sU),
         [ra] "s"(rA), [rb] "s"(rB), [rx] "s"(rX), [rv] "s"(rV), [ru] "s"(rU),
         [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]), [a4] "v"(va[4]),
         [b0] "v"(vb[0]), [b1] "v"(vb[1]), [x0] "v"(vx), [x1] "v"(vv), [x2] "v"(vu),
-        [o0] "i"(OA), [o1] "i"(OA + 1024), [o2] "i"(OA + 2048), [o3] "i"(OA + 3072),
-        [o4] "i"(OA + 4096), [p0] "i"(OB), [p1] "i"(OB + 1024), [ox] "i"(OX), [ov] "i"(OV),
-        [ou] "i"(OU)
+        [o0] "i"(OA), [o4] "i"(OA + 4096), [p0] "i"(OB), [ox] "i"(OX), [ov] "i"(OV), [ou] "i"(OU)
       : "memory", "scc");
-#undef HOP_P
+#undef HOP_PO
+#undef HOP_M0
 }
 
 // One step's 20 LDS-DMA pieces (Q, A, B, QT images of s = 13, m = 4) in one asm
@@ -927,38 +939,35 @@ __device__ __forceinline__ void dma_step20p(const unsigned (&vm)[6], const unsig
       : "memory", "scc");
 #undef HOP_P
 }
+// vm / vb lowered (dma_voff_lowered): 7 M0 writes instead of 20
 template <int OQ, int OA, int OB, int OT>
 __device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsigned (&vb)[2],
                                            __amdgpu_buffer_rsrc_t rQ, __amdgpu_buffer_rsrc_t rA,
                                            __amdgpu_buffer_rsrc_t rB, __amdgpu_buffer_rsrc_t rT,
                                            unsigned wlds, unsigned soM, unsigned soB) {
   unsigned keep;
-#define HOP_P(R, V, OFF, SO)                                                  \
-  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
-  "], %[" #SO "] offen lds\n\t"
+#define HOP_M0(OFF) "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\t"
+#define HOP_PO(R, V, SO, IO) "buffer_load_dwordx4 %[" #V "], %[" #R "], %[" #SO "] offen offset:" #IO " lds\n\t"
+#define HOP_IMG(R, O0, O4)                                                                   \
+  HOP_M0(O0) HOP_PO(R, v0, sm, 0) HOP_PO(R, v1, sm, 1024) HOP_PO(R, v2, sm, 2048)            \
+  HOP_PO(R, v3, sm, 3072) HOP_M0(O4) HOP_PO(R, v4, sm, 0) HOP_PO(R, v5, sm, 1024)
   asm volatile(
-      ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
+      ".p2align 3\n\t"
       "s_mov_b32 %[keep], m0\n\t"
-      "s_nop 0\n\t"
-      HOP_P(rq, v0, %[q0], sm) HOP_P(rq, v1, %[q1], sm) HOP_P(rq, v2, %[q2], sm)
-      HOP_P(rq, v3, %[q3], sm) HOP_P(rq, v4, %[q4], sm) HOP_P(rq, v5, %[q5], sm)
-      HOP_P(ra, v0, %[a0], sm) HOP_P(ra, v1, %[a1], sm) HOP_P(ra, v2, %[a2], sm)
-      HOP_P(ra, v3, %[a3], sm) HOP_P(ra, v4, %[a4], sm) HOP_P(ra, v5, %[a5], sm)
-      HOP_P(rb, u0, %[b0], sb) HOP_P(rb, u1, %[b1], sb)
-      HOP_P(rt, v0, %[t0], sm) HOP_P(rt, v1, %[t1], sm) HOP_P(rt, v2, %[t2], sm)
-      HOP_P(rt, v3, %[t3], sm) HOP_P(rt, v4, %[t4], sm) HOP_P(rt, v5, %[t5], sm)
+      HOP_IMG(rq, %[q0], %[q4]) HOP_IMG(ra, %[a0], %[a4])
+      HOP_M0(%[b0]) HOP_PO(rb, u0, sb, 0) HOP_PO(rb, u1, sb, 1024)
+      HOP_IMG(rt, %[t0], %[t4])
       "s_mov_b32 m0, %[keep]"
       : [keep] "=&s"(keep)
       : [w] "s"(wlds), [sm] "s"(soM), [sb] "s"(soB), [rq] "s"(rQ), [ra] "s"(rA), [rb] "s"(rB),
         [rt] "s"(rT), [v0] "v"(vm[0]), [v1] "v"(vm[1]), [v2] "v"(vm[2]), [v3] "v"(vm[3]),
         [v4] "v"(vm[4]), [v5] "v"(vm[5]), [u0] "v"(vb[0]), [u1] "v"(vb[1]),
-        [q0] "i"(OQ), [q1] "i"(OQ + 1024), [q2] "i"(OQ + 2048), [q3] "i"(OQ + 3072),
-        [q4] "i"(OQ + 4096), [q5] "i"(OQ + 5120), [a0] "i"(OA), [a1] "i"(OA + 1024),
-        [a2] "i"(OA + 2048), [a3] "i"(OA + 3072), [a4] "i"(OA + 4096), [a5] "i"(OA + 5120),
-        [b0] "i"(OB), [b1] "i"(OB + 1024), [t0] "i"(OT), [t1] "i"(OT + 1024),
-        [t2] "i"(OT + 2048), [t3] "i"(OT + 3072), [t4] "i"(OT + 4096), [t5] "i"(OT + 5120)
+        [q0] "i"(OQ), [q4] "i"(OQ + 4096), [a0] "i"(OA), [a4] "i"(OA + 4096), [b0] "i"(OB),
+        [t0] "i"(OT), [t4] "i"(OT + 4096)
       : "memory", "scc");
-#undef HOP_P
+#undef HOP_IMG
+#undef HOP_PO
+#undef HOP_M0
 }
 
 
@@ -1435,6 +1444,16 @@ __device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
     for (int j = 0; j < G::NJU; ++j)
       voTU[j] = chunk_voff<G::CHU>(j, lane, wave_prob0, pb0, a.batch, pstU);
   }
+  // dma_step20 / dma_traj10 take the voffsets lowered by their pieces' instruction offsets
+  unsigned voMl[G::NJM], voBl[G::NJB], voTAl[G::NJA], voTRl[G::NJR];
+#pragma unroll
+  for (int j = 0; j < G::NJM; ++j) voMl[j] = dma_voff_lowered(voM[j], j);
+#pragma unroll
+  for (int j = 0; j < G::NJB; ++j) voBl[j] = dma_voff_lowered(voB[j], j);
+#pragma unroll
+  for (int j = 0; j < G::NJA; ++j) voTAl[j] = TRAJ ? dma_voff_lowered(voTA[j], j) : 0u;
+#pragma unroll
+  for (int j = 0; j < G::NJR; ++j) voTRl[j] = TRAJ ? dma_voff_lowered(voTR[j], j) : 0u;
   auto dma_step = [&](int k) {  // Q, A, B, QT of step k
     if constexpr (TRAJ) {  // A_k, B_k, x_{k+1}, a_k, u_k
       const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
@@ -1443,7 +1462,7 @@ __device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
       if constexpr (G::NJA == 5 && G::NJR == 2 && G::NJX == 1 && G::NJV == 1 && G::NJU == 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
-            voTA, voTR, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR, soX, soV,
+            voTAl, voTRl, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR, soX, soV,
             soU);
         return;
       }
@@ -1462,7 +1481,7 @@ __device__ __forceinline__ void lft_v2_body(LftArgs<double> a, int need_in) {
     const unsigned soM = (unsigned)(k * SS * 8), soB = (unsigned)(k * SM * 8);
     if constexpr (C::DMA1 && G::NJM == 6 && G::NJB == 2) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
+      dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voMl, voBl, rQ, rA, rB, rT, wlds, soM,
                                                          soB);
       return;
     }
@@ -2545,13 +2564,23 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     for (int j = 0; j < G::NJB; ++j)
       voB[j] = chunk_voff<G::CHB>(j, lane, wave_prob0, pb0, a.batch, pstrB);
   }
+  // dma_step20 / dma_traj10 take the voffsets lowered by their pieces' instruction offsets
+  unsigned voMl[G::NJM], voBl[G::NJB], voTAl[G::NJA], voTRl[G::NJR];
+#pragma unroll
+  for (int j = 0; j < G::NJM; ++j) voMl[j] = TRAJ ? 0u : dma_voff_lowered(voM[j], j);
+#pragma unroll
+  for (int j = 0; j < G::NJB; ++j) voBl[j] = TRAJ ? 0u : dma_voff_lowered(voB[j], j);
+#pragma unroll
+  for (int j = 0; j < G::NJA; ++j) voTAl[j] = TRAJ ? dma_voff_lowered(voTA[j], j) : 0u;
+#pragma unroll
+  for (int j = 0; j < G::NJR; ++j) voTRl[j] = TRAJ ? dma_voff_lowered(voTR[j], j) : 0u;
   auto dma_step = [&](int k) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if constexpr (TRAJ) {  // A_k, B_k, x_{k+1}, a_k, u_k
       const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
                      soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
       dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
-          voTA, voTR, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR,
+          voTAl, voTRl, voTX[0], voTV[0], voTU[0], rQ, rA, rT, rB, rU, wlds, soA, soR,
           soV + NN * 8, soV, soU);
     } else if constexpr (G::NJM == 6 && G::NJB == 2) {
       const unsigned soM = (unsigned)(k * SS * ES), soB = (unsigned)(k * SM * ES);
@@ -2559,8 +2588,8 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
         dma_step20p<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT, G::LASTM, G::LASTB>(
             voM, voB, rQ, rA, rB, rT, wlds, soM, soB);
       else
-        dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voM, voB, rQ, rA, rB, rT, wlds, soM,
-                                                           soB);
+        dma_step20<G::OFF_Q, G::OFF_A, G::OFF_B, G::OFF_QT>(voMl, voBl, rQ, rA, rB, rT, wlds,
+                                                           soM, soB);
     } else {
       const unsigned soM = (unsigned)(k * SS * ES), soB = (unsigned)(k * SM * ES);
 #pragma unroll
@@ -3098,12 +3127,17 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
   voTX[0] = chunk_voff<G::CHX>(0, lane, wave_prob0, pb0, a.batch, pstX);
   voTV[0] = chunk_voff<G::CHV>(0, lane, wave_prob0, pb0, a.batch, pstV);
   voTU[0] = chunk_voff<G::CHU>(0, lane, wave_prob0, pb0, a.batch, pstU);
+  unsigned voTAl[G::NJA], voTRl[G::NJR];  // lowered by the pieces' instruction offsets
+#pragma unroll
+  for (int j = 0; j < G::NJA; ++j) voTAl[j] = dma_voff_lowered(voTA[j], j);
+#pragma unroll
+  for (int j = 0; j < G::NJR; ++j) voTRl[j] = dma_voff_lowered(voTR[j], j);
   auto dma_step = [&](int k) {  // A_k, B_k, x_{k+1}, a_k, u_k
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const unsigned soA = (unsigned)(k * NN * NN * 8), soR = (unsigned)(k * NN * MM * 8),
                    soV = (unsigned)(k * NN * 8), soU = (unsigned)(k * MM * 8);
     dma_traj10<G::OFF_A, G::OFF_B, G::OFF_VX, G::OFF_VA, G::OFF_VU>(
-        voTA, voTR, voTX[0], voTV[0], voTU[0], rA, rB, rX, rV, rU, wlds, soA, soR, soV + NN * 8,
+        voTAl, voTRl, voTX[0], voTV[0], voTU[0], rA, rB, rX, rV, rU, wlds, soA, soR, soV + NN * 8,
         soV, soU);
   };
   dma_step(0);

@@ -60,8 +60,17 @@ __device__ __forceinline__ unsigned voff(int j, int lane, long long wave_prob0, 
   return (q < kProbPerWave * CH) ? (unsigned)((pe - pb0) * pstr + r * 16) : 0x7FFFFFFFu;
 }
 
-// the step's 9 LDS-DMA pieces (A 5, B 2, x, u) in one asm block; M0 saved once
-// and set per piece from the wave's LDS base plus an immediate
+// the step's 9 LDS-DMA pieces (A 5, B 2, x, u, contiguous 1-KiB pieces of the image) in
+// one asm block: the LDS-DMA instruction offset is added to both the LDS destination
+// (M0 + offset + 16 lane) and the memory address (tools/ubench/lds_dma_offset.hip), so
+// piece j goes to M0 = IMG + 4096 (j / 4) with offset 1024 (j % 4) and its voffset is
+// lowered by that offset once at kernel start (dma9_voff): 3 M0 writes (each with the
+// wait state an M0 write needs before an LDS-DMA) instead of 9
+static_assert(OFF_B == OFF_A + 5 * 1024 && OFF_X == OFF_A + 7 * 1024 && OFF_U == OFF_A + 8 * 1024,
+              "dma9: contiguous 1-KiB pieces");
+__device__ __forceinline__ unsigned dma9_voff(unsigned voff, int piece) {
+  return voff - 1024u * (unsigned)(piece % 4);
+}
 template <int IMG>
 __device__ __forceinline__ void dma9(const unsigned (&va)[5], const unsigned (&vb)[2], unsigned vx,
                                      unsigned vu, __amdgpu_buffer_rsrc_t rA,
@@ -69,26 +78,25 @@ __device__ __forceinline__ void dma9(const unsigned (&va)[5], const unsigned (&v
                                      __amdgpu_buffer_rsrc_t rU, unsigned wlds, unsigned sA,
                                      unsigned sB, unsigned sX, unsigned sU) {
   unsigned keep;
-#define HOP_P(R, V, OFF, SO)                                                  \
-  "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
-  "], %[" #SO "] offen lds\n\t"
+#define HOP_M0(OFF) "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\t"
+#define HOP_PO(R, V, SO, IO) "buffer_load_dwordx4 %[" #V "], %[" #R "], %[" #SO "] offen offset:" #IO " lds\n\t"
   asm volatile(
       "s_mov_b32 %[keep], m0\n\t"
-      HOP_P(ra, a0, %[o0], sa) HOP_P(ra, a1, %[o1], sa) HOP_P(ra, a2, %[o2], sa)
-      HOP_P(ra, a3, %[o3], sa) HOP_P(ra, a4, %[o4], sa)
-      HOP_P(rb, b0, %[p0], sb) HOP_P(rb, b1, %[p1], sb)
-      HOP_P(rx, x0, %[ox], sx) HOP_P(ru, x1, %[ou], su)
+      HOP_M0(%[m0]) HOP_PO(ra, a0, sa, 0) HOP_PO(ra, a1, sa, 1024) HOP_PO(ra, a2, sa, 2048)
+      HOP_PO(ra, a3, sa, 3072)
+      HOP_M0(%[m1]) HOP_PO(ra, a4, sa, 0) HOP_PO(rb, b0, sb, 1024) HOP_PO(rb, b1, sb, 2048)
+      HOP_PO(rx, x0, sx, 3072)
+      HOP_M0(%[m2]) HOP_PO(ru, x1, su, 0)
       "s_mov_b32 m0, %[keep]"
       : [keep] "=&s"(keep)
       : [w] "s"(wlds), [sa] "s"(sA), [sb] "s"(sB), [sx] "s"(sX), [su] "s"(sU),
         [ra] "s"(rA), [rb] "s"(rB), [rx] "s"(rX), [ru] "s"(rU),
         [a0] "v"(va[0]), [a1] "v"(va[1]), [a2] "v"(va[2]), [a3] "v"(va[3]), [a4] "v"(va[4]),
         [b0] "v"(vb[0]), [b1] "v"(vb[1]), [x0] "v"(vx), [x1] "v"(vu),
-        [o0] "i"(IMG + OFF_A), [o1] "i"(IMG + OFF_A + 1024), [o2] "i"(IMG + OFF_A + 2048),
-        [o3] "i"(IMG + OFF_A + 3072), [o4] "i"(IMG + OFF_A + 4096), [p0] "i"(IMG + OFF_B),
-        [p1] "i"(IMG + OFF_B + 1024), [ox] "i"(IMG + OFF_X), [ou] "i"(IMG + OFF_U)
+        [m0] "i"(IMG + OFF_A), [m1] "i"(IMG + OFF_A + 4096), [m2] "i"(IMG + OFF_A + 8192)
       : "memory", "scc");
-#undef HOP_P
+#undef HOP_PO
+#undef HOP_M0
 }
 
 // [A|B] rows (12 registers, column c per lane), x_c and u_c from image IMG, and
@@ -631,11 +639,13 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   constexpr int NST = JC ? 0 : 5 + (WANTV ? 14 : 0);
   unsigned va[5], vb[2], vx_, vu_;
 #pragma unroll
-  for (int j = 0; j < 5; ++j) va[j] = voff<CH_A>(j, lane, wave_prob0, pb0, a.batch, pA);
+  for (int j = 0; j < 5; ++j)  // image pieces 0 .. 4
+    va[j] = dma9_voff(voff<CH_A>(j, lane, wave_prob0, pb0, a.batch, pA), j);
 #pragma unroll
-  for (int j = 0; j < 2; ++j) vb[j] = voff<CH_B>(j, lane, wave_prob0, pb0, a.batch, pB);
-  vx_ = voff<CH_X>(0, lane, wave_prob0, pb0, a.batch, pX);
-  vu_ = voff<CH_U>(0, lane, wave_prob0, pb0, a.batch, pU);
+  for (int j = 0; j < 2; ++j)  // pieces 5, 6
+    vb[j] = dma9_voff(voff<CH_B>(j, lane, wave_prob0, pb0, a.batch, pB), 5 + j);
+  vx_ = dma9_voff(voff<CH_X>(0, lane, wave_prob0, pb0, a.batch, pX), 7);
+  vu_ = dma9_voff(voff<CH_U>(0, lane, wave_prob0, pb0, a.batch, pU), 8);
   // per-lane image addresses of [A|B] row j, x_c and u_c
   unsigned ad[S];
 #pragma unroll
