@@ -29,9 +29,11 @@ HEADERS = ["hop_device.hpp", "hop_kernels.hpp", "dpp_blocks.inc", "small_math.hp
 ARCH = os.environ.get("HOP_OFFLOAD_ARCH", "gfx950")
 # device code from its assembly, minus the DPP hazard pads the compiled code does not
 # need (tools/nop_elide.py); HOP_NO_ELIDE=1 compiles the plain way (hipcc -c)
-ELIDE = os.environ.get("HOP_NO_ELIDE", "0") in ("", "0") and os.path.exists(
-    os.path.join(REPO, "tools", "nop_elide.py"))
 LLVM_BIN = os.environ.get("HOP_LLVM_BIN", "/opt/rocm/lib/llvm/bin")
+ELIDE = (os.environ.get("HOP_NO_ELIDE", "0") in ("", "0")
+         and os.path.exists(os.path.join(REPO, "tools", "nop_elide.py"))
+         and all(os.path.exists(os.path.join(LLVM_BIN, t))
+                 for t in ("clang", "lld", "clang-offload-bundler")))
 FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-variable", "-Wno-pass-failed",
          "-Wno-unused-but-set-variable"] + (["-DHOP_DEV=1"] if DEV else [])
 
