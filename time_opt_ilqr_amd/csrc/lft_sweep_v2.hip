@@ -1117,6 +1117,37 @@ __device__ __forceinline__ void sym_load_average(double (&X)[S], const double* t
 #pragma unroll
   for (int i = 0; i < S; ++i) X[i] = __builtin_fma(hs, y[i] - X[i], X[i]);
 }
+// sym_load_average in two halves (the closed-form kernel): the transposed reads issued
+// with no wait, other work, then the wait and the average.  The compiler's own LDS
+// waits in between also wait for these reads (LDS operations complete in order), so
+// the round trip is shared with the next reads instead of paid alone.
+__device__ __forceinline__ void sym_issue13(const double* t, int c, double (&y)[13]) {
+  const int cr = c < 13 ? c : 0;
+  asm volatile(
+      "ds_read_b64 %0, %13 offset:0\n\tds_read_b64 %1, %13 offset:8\n\t"
+      "ds_read_b64 %2, %13 offset:16\n\tds_read_b64 %3, %13 offset:24\n\t"
+      "ds_read_b64 %4, %13 offset:32\n\tds_read_b64 %5, %13 offset:40\n\t"
+      "ds_read_b64 %6, %13 offset:48\n\tds_read_b64 %7, %13 offset:56\n\t"
+      "ds_read_b64 %8, %13 offset:64\n\tds_read_b64 %9, %13 offset:72\n\t"
+      "ds_read_b64 %10, %13 offset:80\n\tds_read_b64 %11, %13 offset:88\n\t"
+      "ds_read_b64 %12, %13 offset:96"
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]),
+        "=&v"(y[6]), "=&v"(y[7]), "=&v"(y[8]), "=&v"(y[9]), "=&v"(y[10]), "=&v"(y[11]),
+        "=&v"(y[12])
+      : "v"(lds_addr(t) + 8u * 13 * cr)
+      : "memory");
+}
+__device__ __forceinline__ void sym_wait_average13(double (&X)[13], double (&y)[13], int c) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]),
+                 "+v"(y[6]), "+v"(y[7]), "+v"(y[8]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]),
+                 "+v"(y[12])
+               :
+               : "memory");
+  const double hs = c < 13 ? 0.5 : 0.0;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) X[i] = __builtin_fma(hs, y[i] - X[i], X[i]);
+}
 // the step whose predict stores the rows for the symmetrisation at step k + 1
 __device__ __forceinline__ bool sym_store_step(int k, int N) { return k + 1 < N && sym_step(k + 1); }
 template <int S>
@@ -3271,10 +3302,29 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
     const double atil = av - bd;
     at[NN] = in ? atil : (c == NN ? 1.0 : 0.0);
     at[S] = e_s;
-    // the periodic symmetrisation (split: the rows were stored after the last predict)
-    if constexpr (kSymSplit && has_sym_every<C>()) {
-      if (sym_step(k))
-        sym_load_average<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
+    // the periodic symmetrisation (split: the rows were stored after the last predict);
+    // its reads share their round trip with e_{k+1}'s below (X is first needed after)
+    constexpr bool SYMI = kSymSplit && has_sym_every<C>() && S == 13;
+    double ysym[S];
+    const bool sy = sym_step(k);
+    if constexpr (SYMI) {
+      if (sy) sym_issue13(csym, c, reinterpret_cast<double (&)[13]>(ysym));
+    } else if constexpr (kSymSplit && has_sym_every<C>()) {
+      if (sy) sym_load_average<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
+    }
+    // ---- e_{k+1}: the terminal block of horizon k+1 and the next stage block
+    const double e1 = err(x1);
+    double qe1;
+    {
+      double qr[NN];
+      rows(lq, qr);
+      lane_matvec<NN>(qe1, e1, qr);
+    }
+    const double eqe1 = lane_sum<NN>(e1 * qe1);
+    if constexpr (SYMI) {
+      if (sy)
+        sym_wait_average13(reinterpret_cast<double (&)[13]>(X),
+                           reinterpret_cast<double (&)[13]>(ysym), c);
     }
     // ---- stage inverse E_k in closed form, S = Sigma_eps + E_k (non-offset)
     double r[S];
@@ -3294,15 +3344,6 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
       r[NN] = X[NN];
       LaneB<S>::fma(r, wp, vp);  // + w' v'^T
     }
-    // ---- e_{k+1}: the terminal block of horizon k+1 and the next stage block
-    const double e1 = err(x1);
-    double qe1;
-    {
-      double qr[NN];
-      rows(lq, qr);
-      lane_matvec<NN>(qe1, e1, qr);
-    }
-    const double eqe1 = lane_sum<NN>(e1 * qe1);
     // ---- update: condition the prefix on stage k's cost
     if (!kSymSplit && has_sym_every<C>() && sym_step(k))
       sym_average<S>(reinterpret_cast<double (&)[S]>(X), csym, c);
