@@ -64,6 +64,65 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
       : "memory");
 }
 
+// Tile64 blocks: the pieces of a block are contiguous 1-KiB spans in HBM and in LDS,
+// and the LDS-DMA instruction offset is added to both addresses (measured,
+// tools/ubench/lds_dma_offset.hip), so up to four pieces share one M0 and one
+// voffset: group g loads pieces 4g .. 4g+3 at M0 = block + 4096 g, offsets 0 .. 3072.
+// Five instructions per group instead of five per piece.
+template <int NL>
+__device__ __forceinline__ void dma_grp(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds,
+                                        unsigned soff) {
+  static_assert(NL >= 1 && NL <= 4, "one to four pieces per M0");
+  unsigned keep;
+#define HOP_G(OFF) "buffer_load_dwordx4 %1, %2, %4 offen offset:" #OFF " nt lds\n\t"
+  const unsigned l = __builtin_amdgcn_readfirstlane(lds), so = __builtin_amdgcn_readfirstlane(soff);
+  if constexpr (NL == 1)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
+  else if constexpr (NL == 2)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
+  else if constexpr (NL == 3)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
+                 HOP_G(2048) "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
+                 HOP_G(2048) HOP_G(3072) "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
+#undef HOP_G
+}
+// NP pieces of one tile64 block at LDS `lds`, the last one LAST lanes wide (64: full);
+// vr[r] = 1024 r + 16 lane (the block's per-piece voffsets)
+template <int NP, int LAST>
+__device__ __forceinline__ void dma_block64(const unsigned* vr, __amdgpu_buffer_rsrc_t rsrc,
+                                            unsigned lds, unsigned soff, int lane) {
+  constexpr int FULL = LAST == 64 ? NP : NP - 1;
+  static_for<(FULL + 3) / 4>([&](auto G_) {
+    constexpr int g = G_;
+    constexpr int nl = FULL - 4 * g < 4 ? FULL - 4 * g : 4;
+    dma_grp<nl>(vr[4 * g], rsrc, lds + 4096u * g, soff);
+  });
+  if constexpr (FULL < NP) {
+    if (lane < LAST) dma16(vr[NP - 1], rsrc, lds + 1024u * (NP - 1), soff);
+  }
+}
+// the same from the block's base voffset v0 (piece r at v0 + 1024 r)
+template <int NP, int LAST>
+__device__ __forceinline__ void dma_block64v(unsigned v0, __amdgpu_buffer_rsrc_t rsrc,
+                                             unsigned lds, unsigned soff, int lane) {
+  constexpr int FULL = LAST == 64 ? NP : NP - 1;
+  static_for<(FULL + 3) / 4>([&](auto G_) {
+    constexpr int g = G_;
+    constexpr int nl = FULL - 4 * g < 4 ? FULL - 4 * g : 4;
+    dma_grp<nl>(v0 + 4096u * g, rsrc, lds + 4096u * g, soff);
+  });
+  if constexpr (FULL < NP) {
+    if (lane < LAST) dma16(v0 + 1024u * (NP - 1), rsrc, lds + 1024u * (NP - 1), soff);
+  }
+}
+
 // PW problems per wave: 64 (one per lane), or 32 (lanes 32..63 recompute lanes
 // 0..31's problems and store nothing) so that a batch of 64 problems per SIMD
 // runs as two waves per SIMD that hide each other's dependency stalls
@@ -181,28 +240,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
   auto dma_stage = [&](int k) {  // Q, A, B of step k
     const unsigned soM = (unsigned)(k * SS * TS * (LY == 2 ? 64 : 1)),
                    soB = (unsigned)(k * SM * TS * (LY == 2 ? 64 : 1));
-    if (owner) {
+    if constexpr (LY == 2) {  // grouped pieces (dma_block64)
+      dma_block64<G::CM, G::LAST_M>(vMr, rQ, wlds + G::P_Q * 1024u, soM, lane);
+      dma_block64<G::CM, G::LAST_M>(vMr, rA, wlds + G::P_A * 1024u, soM, lane);
+      dma_block64<G::CB, G::LAST_B>(vBr, rB, wlds + G::P_B * 1024u, soB, lane);
+    } else if (owner) {
 #pragma unroll
-      for (int r = 0; r < G::CM; ++r)
-        if (LY != 2 || r + 1 < G::CM || lane < G::LAST_M)
-          dma16(vMr[r], rQ, wlds + (G::P_Q + r) * G::PIECE, soM);
+      for (int r = 0; r < G::CM; ++r) dma16(vMr[r], rQ, wlds + (G::P_Q + r) * G::PIECE, soM);
 #pragma unroll
-      for (int r = 0; r < G::CM; ++r)
-        if (LY != 2 || r + 1 < G::CM || lane < G::LAST_M)
-          dma16(vMr[r], rA, wlds + (G::P_A + r) * G::PIECE, soM);
+      for (int r = 0; r < G::CM; ++r) dma16(vMr[r], rA, wlds + (G::P_A + r) * G::PIECE, soM);
 #pragma unroll
-      for (int r = 0; r < G::CB; ++r)
-        if (LY != 2 || r + 1 < G::CB || lane < G::LAST_B)
-          dma16(vBr[r], rB, wlds + (G::P_B + r) * G::PIECE, soB);
+      for (int r = 0; r < G::CB; ++r) dma16(vBr[r], rB, wlds + (G::P_B + r) * G::PIECE, soB);
     }
   };
   auto dma_query = [&](int k) {  // QT of step k
     const unsigned soM = (unsigned)(k * SS * TS * (LY == 2 ? 64 : 1));
-    if (owner) {
+    if constexpr (LY == 2) {
+      dma_block64<G::CM, G::LAST_M>(vMr, rT, wlds + G::P_T * 1024u, soM, lane);
+    } else if (owner) {
 #pragma unroll
-      for (int r = 0; r < G::CM; ++r)
-        if (LY != 2 || r + 1 < G::CM || lane < G::LAST_M)
-          dma16(vMr[r], rT, wlds + (G::P_T + r) * G::PIECE, soM);
+      for (int r = 0; r < G::CM; ++r) dma16(vMr[r], rT, wlds + (G::P_T + r) * G::PIECE, soM);
     }
   };
   auto vm_wait = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
@@ -412,7 +469,16 @@ __global__ __launch_bounds__(256, 1) void lft_small_traj_kernel(LftArgs<T> a) {
                    sX = (unsigned)((k + 1) * NN * TS) * KS, sV = (unsigned)(k * NN * TS) * KS,
                    sU = (unsigned)(k * MM * TS) * KS;
     // tile64: a section's last piece is partial; its lanes past the data would write
-    // the next step's elements into the following image, so they issue nothing
+    // the next step's elements into the following image, so they issue nothing; the
+    // full pieces go four to an M0 (dma_block64v)
+    if constexpr (LY == 2) {
+      dma_block64v<G::CA, G::LAST_A>(vA, rA, wlds + G::P_A * 1024u, sA, lane);
+      dma_block64v<G::CB, G::LAST_B>(vB, rB, wlds + G::P_B * 1024u, sB, lane);
+      dma_block64v<G::CX, G::LAST_X>(vX, rX, wlds + G::P_X * 1024u, sX, lane);
+      dma_block64v<G::CX, G::LAST_X>(vV, rV, wlds + G::P_V * 1024u, sV, lane);
+      dma_block64v<G::CU, G::LAST_U>(vU, rU, wlds + G::P_U * 1024u, sU, lane);
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < G::CA; ++r)
       if (LY != 2 || r + 1 < G::CA || lane < G::LAST_A)
