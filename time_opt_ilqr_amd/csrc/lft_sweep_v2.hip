@@ -123,13 +123,6 @@ struct SchedCond : SchedLdlDma {
   static constexpr int SCALE = 0;  // first attempts only: its own sweeps (rerun on doubt)
 };
 // + the QT image reads under the E sweep, the A/B reads under the X sweep
-// developer A/B builds (tools/exp_build.py): the conditioned kernel's step DMA
-// issued as one block (0), not at all (1: the images keep step 0, timing only), or
-// split: Q / QT after the sweeps, A / B after the update (2)
-#ifndef HOP_EXP_DMA
-#define HOP_EXP_DMA 0
-#endif
-constexpr int kExpDma = HOP_EXP_DMA;
 #ifndef HOP_COND_WQ
 #define HOP_COND_WQ 1  // developer A/B builds (tools/exp_build.py): 0 = round 3's query
 #endif
@@ -2884,11 +2877,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     }
     if (dstag<C>() != 2 && !dma_late) {
       wave_sync();
-      if constexpr (kExpDma == 2 && !TRAJ && !F32 && G::NJM == 6 && G::NJB == 2 && !has_pack<C>()) {
-        if (k + 1 < N) dma_stepQT<G::OFF_Q, G::OFF_QT>(voM, rQ, rT, wlds, (unsigned)((k + 1) * SS * ES));
-      } else if constexpr (kExpDma != 1) {
-        if (k + 1 < N) dma_step(k + 1);
-      }
+      if (k + 1 < N) dma_step(k + 1);
       if constexpr (has_symlate<C>()) {
         static_assert(!TRAJ && !has_pack<C>(), "own scratch: the one-wave layout");
         if (sym_step(k)) {
@@ -2926,11 +2915,6 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     if (dma_late) {  // DSTAG 1: the odd waves' pieces, half a step after the even waves'
       wave_sync();
       if (k + 1 < N) dma_step(k + 1);
-    }
-    if constexpr (kExpDma == 2 && !TRAJ && !F32 && G::NJM == 6 && G::NJB == 2 && !has_pack<C>()) {
-      if (dstag<C>() != 2 && !dma_late && k + 1 < N)
-        dma_stepAB<G::OFF_A, G::OFF_B>(voM, voB, rA, rB, wlds, (unsigned)((k + 1) * SS * ES),
-                                       (unsigned)((k + 1) * SM * ES));
     }
     stamp(5);
     // ---- predict: Sigma_{k+1} = A Sigma' A^T + B R^-1 B^T + eps I, m_{k+1} = A m'
