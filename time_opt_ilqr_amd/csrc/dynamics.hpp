@@ -47,6 +47,22 @@ HOP_HD constexpr int control_dim(int sys) {
 
 HOP_HD inline bool finite_d(double v) { return v - v == 0.0; }  // false for NaN and +-inf
 
+// sin and cos of one angle.  On the device one sincos: ocml's sin, cos and sincos
+// run the same argument reduction and the same kernel polynomials and differ only
+// in which results they select, so the values are bitwise those of separate
+// sin/cos calls, for the reduction's cost once (the compiler does not merge two
+// inlined reductions by itself).  HOP_SINCOS=0 keeps the separate calls (A/B).
+#ifndef HOP_SINCOS
+#define HOP_SINCOS 1
+#endif
+HOP_HD inline void sin_cos(double v, double& s, double& c) {
+#if HOP_SINCOS && defined(__HIP_DEVICE_COMPILE__)
+  sincos(v, &s, &c);
+#else
+  s = sin(v), c = cos(v);
+#endif
+}
+
 // Python's max(a, b) keeps a unless b > a (so a NaN b never wins)
 HOP_HD inline double py_max(double a, double b) { return b > a ? b : a; }
 
@@ -68,7 +84,8 @@ HOP_HD inline void f_cartpole(const double* x, const double* u, double dt, doubl
   const double total_mass = m_cart + m_pole;
   const double polemass_length = m_pole * length;
   const double th_u = x[2] - 3.141592653589793;  // math.pi
-  const double costh = cos(th_u), sinth = sin(th_u);
+  double costh, sinth;
+  sin_cos(th_u, sinth, costh);
   const double temp = (u[0] + polemass_length * x[3] * x[3] * sinth) / total_mass;
   const double denom = length * (4.0 / 3.0 - m_pole * costh * costh / total_mass);
   const double th_acc = (g * sinth - costh * temp) / denom;
@@ -112,11 +129,12 @@ struct QuadTrig {
   double sphi, cphi, sth, cth, tth, spsi, cpsi;
 };
 
-HOP_HD inline void quad_trig_phi(double phi, QuadTrig& t) { t.sphi = sin(phi), t.cphi = cos(phi); }
+HOP_HD inline void quad_trig_phi(double phi, QuadTrig& t) { sin_cos(phi, t.sphi, t.cphi); }
 HOP_HD inline void quad_trig_th(double th, QuadTrig& t) {
-  t.sth = sin(th), t.cth = cos(th), t.tth = tan(th);
+  sin_cos(th, t.sth, t.cth);
+  t.tth = tan(th);
 }
-HOP_HD inline void quad_trig_psi(double psi, QuadTrig& t) { t.spsi = sin(psi), t.cpsi = cos(psi); }
+HOP_HD inline void quad_trig_psi(double psi, QuadTrig& t) { sin_cos(psi, t.spsi, t.cpsi); }
 HOP_HD inline QuadTrig quad_trig(const double* x) {
   QuadTrig t;
   quad_trig_phi(x[6], t);
@@ -232,9 +250,9 @@ HOP_HD inline void quad_trig_job(const double* x, int job, double epsx, double r
   const double h = fd_step(v, epsx, relx);
   const double w = sgn == 0 ? v + h : v - h;
   double* o = ts + kTrigBase + sgn * kTrigSet;
-  if (ax == 0) o[0] = sin(w), o[1] = cos(w);
-  else if (ax == 1) o[2] = sin(w), o[3] = cos(w), o[4] = tan(w);
-  else o[5] = sin(w), o[6] = cos(w);
+  if (ax == 0) sin_cos(w, o[0], o[1]);
+  else if (ax == 1) sin_cos(w, o[2], o[3]), o[4] = tan(w);
+  else sin_cos(w, o[5], o[6]);
 }
 
 // the QuadTrig of column j's evaluation point: the base values, with the moved

@@ -374,7 +374,8 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
       // trigonometry: roll (h = 0) or yaw (h = 1) on this lane, the pitch on both
       QuadTrig t;
       const double ang = h ? x[8] : x[6];
-      const double sa = sin(ang), ca = cos(ang);
+      double sa, ca;
+      sin_cos(ang, sa, ca);
       const double so = pair_swap(sa), co = pair_swap(ca);
       t.sphi = h ? so : sa, t.cphi = h ? co : ca;
       t.spsi = h ? sa : so, t.cpsi = h ? ca : co;
