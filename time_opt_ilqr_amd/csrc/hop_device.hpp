@@ -82,6 +82,11 @@ __device__ __forceinline__ void lds_put(T* tile, int c, const T (&x)[S]) {
   for (int i = 0; i < S; ++i) tile[i * kLdsRow + c] = x[i];
 }
 template <class T, int S>
+__device__ __forceinline__ void lds_get(const T* tile, int c, T (&x)[S]) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) x[i] = tile[i * kLdsRow + c];
+}
+template <class T, int S>
 __device__ __forceinline__ void lds_get_t(const T* tile, int c, T (&x)[S]) {
 #pragma unroll
   for (int i = 0; i < S; ++i) x[i] = tile[c * kLdsRow + i];

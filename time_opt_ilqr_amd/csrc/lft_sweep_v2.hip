@@ -1870,6 +1870,55 @@ __global__ __launch_bounds__(256, 1) void lft_sweep_v2_kernel(LftArgs<double> a)
 // ===========================================================================
 constexpr int kPipeMax = 4;  // problems per workgroup the pipeline takes (above: the LFT body)
 constexpr int kPipeBS = 4;   // steps per beat
+// The chains' products split over the four rows of the wave (HOP_PIPE_SPLIT=0: every
+// row computes the whole product, as the LFT kernel does).  Row g forms output rows
+// g, 4 + g, 8 + g (and 12 for g = 0): the i-th of them is the i-th register of a
+// four-register slice.  out[r] += sum_j bcast_j(x[r]) y[j] needs x's rows of the slice
+// and all of y; out[r] += sum_j x[j][r] y[j] is the same with x's columns of the slice
+// (read transposed from LDS).  Each output element is the same FMA chain in the same
+// order as in the whole product, so the values are bitwise the same; the slices meet
+// again through LDS where the next product needs every row.
+#ifndef HOP_PIPE_SPLIT
+#define HOP_PIPE_SPLIT 1
+#endif
+constexpr bool kPipeSplit = HOP_PIPE_SPLIT != 0;
+
+// rows 4 i + g of a matrix in LDS (row stride RS doubles; rows past S - 1 read row S - 1)
+template <int S, int RS>
+__device__ __forceinline__ void get_slice(const double* m, int g, int c, double (&x)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 4 * i + g < S ? 4 * i + g : S - 1;
+    x[i] = m[r * RS + c];
+  }
+}
+// columns 4 i + g, transposed: x[i] on lane c = M[c][4 i + g] (clamped to the matrix)
+template <int S, int RS>
+__device__ __forceinline__ void get_slice_t(const double* m, int g, int c, double (&x)[4]) {
+  const int cr = c < S ? c : S - 1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = 4 * i + g < S ? 4 * i + g : S - 1;
+    x[i] = m[cr * RS + col];
+  }
+}
+template <int S, int RS>
+__device__ __forceinline__ void put_slice(double* m, int g, int c, const double (&x)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * i + g < S) m[(4 * i + g) * RS + c] = x[i];
+}
+// the slice of a matrix held whole in registers (three lane selects per register)
+template <int S>
+__device__ __forceinline__ void sel_slice(const double (&x)[S], int g, double (&o)[4]) {
+  auto at = [&](int r) { return x[r < S ? r : S - 1]; };
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double a = (g & 1) ? at(4 * i + 1) : at(4 * i);
+    const double b = (g & 1) ? at(4 * i + 3) : at(4 * i + 2);
+    o[i] = (g & 2) ? b : a;
+  }
+}
 
 template <int S, int MM, int BS>
 struct PipeGeo {
@@ -2003,6 +2052,7 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
   const long long pk0 = p * (long long)a.nalloc;  // step 0 of problem p
   unsigned st = 0;
   double Gb[S], Eb[S], H[S];  // the chains' carried prefix (waves 0 and 1)
+  double Gbd[4], Ebd[4], Hd[4];  // their slices (kPipeSplit)
   double best = 0.0;
   int tbest = 0;
   const int nb = (N + BS - 1) / BS;
@@ -2120,6 +2170,56 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
         }
         wave_sync();
       }
+    } else if (w == 0 && kPipeSplit) {  // ---- the Gbar chain of beat b - 1, sliced products
+      const int jb = b - 1;
+      if (jb >= 0 && jb < nb) {
+        double* tiles = reinterpret_cast<double*>(base + PG::OFF_TILE);  // wave 0: tiles 0 .. 3
+#pragma unroll 1
+        for (int kk = 0; kk < BS; ++kk) {
+          const int k = BS * jb + kk;
+          if (k >= N) break;
+          const double* mF = reinterpret_cast<const double*>(base + PG::OFF_F) +
+                             (k % (PG::D_F * BS)) * S * 16;
+          const double* mG = reinterpret_cast<const double*>(base + PG::OFF_GK) +
+                             (k % (PG::D_GK * BS)) * S * 16;
+          double Gkd[4];
+          get_slice<S, 16>(mG, g, c, Gkd);
+          if (k == 0) {
+            copy(Gbd, Gkd);
+          } else {
+            const double* mE = reinterpret_cast<const double*>(base + PG::OFF_NE) +
+                               (k % (PG::D_NE * BS)) * S * 16;
+            double F[S], Fd[4], Ftd[4], NEd[4], NWd[4];
+            ring_get<S>(base, PG::OFF_F, k % (PG::D_F * BS), c, F);
+            get_slice<S, 16>(mF, g, c, Fd);
+            get_slice_t<S, 16>(mF, g, c, Ftd);
+            get_slice<S, 16>(mE, g, c, NEd);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) NWd[i] = Gbd[i] - NEd[i];  // E_k + Gbar, this row's slice
+            // every row's tile gets the whole matrix (the inverse and its ladder run per row)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) put_slice<S, kLdsRow>(tiles + gg * kLdsTile, g, c, NWd);
+            diag_add<S, kLdsRow>(tile, c, 1e-9 - 1.0 - (-1.0));
+            wave_sync();
+            double NW[S];
+            neg_inverse<C, S, kLdsRow>(NW, tile, c, mt, st);  // NW = -W
+            wave_sync();
+            if (g == 0) ring_put<S>(base, PG::OFF_NW, k % (PG::D_NW * BS), c, NW);
+            double Wd[4], Zd[4], Z[S];
+            sel_slice<S>(NW, g, Wd);
+            copy(Zd, Fd);
+            gxy<C, true>(Zd, Wd, F);  // W F, this row's slice
+            put_slice<S, kLdsRow>(tiles, g, c, Zd);
+            wave_sync();
+            lds_get<double, S>(tiles, c, Z);
+            copy(Gbd, Gkd);
+            gxy<C, true>(Gbd, Ftd, Z);  // Gbar = G - F^T W F, this row's slice
+          }
+          double* mB = reinterpret_cast<double*>(base + PG::OFF_GB) + (k % (PG::D_GB * BS)) * S * 16;
+          put_slice<S, 16>(mB, g, c, Gbd);
+        }
+        wave_sync();
+      }
     } else if (w == 0) {  // ---- the Gbar chain of beat b - 1 (all rows: the same step)
       const int jb = b - 1;
       if (jb >= 0 && jb < nb) {
@@ -2146,6 +2246,63 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
             gxty<C, true>(Gb, F, Z);    // Gbar = G - F^T W F
           }
           if (g == 0) ring_put<S>(base, PG::OFF_GB, k % (PG::D_GB * BS), c, Gb);
+        }
+        wave_sync();
+      }
+    } else if (w == 1 && kPipeSplit) {  // ---- the Ebar / Fbar^T chain of beat b - 2, sliced
+      const int jb = b - 2;
+      if (jb >= 0 && jb < nb) {
+        // rows 0 .. S-1 of wave 1's third and fourth tiles: the exchanges of W Fbar^T and
+        // of Fbar^T (row S of every tile keeps z0)
+        double* tZ = reinterpret_cast<double*>(base + PG::OFF_TILE) + 6 * kLdsTile;
+        double* tH = reinterpret_cast<double*>(base + PG::OFF_TILE) + 7 * kLdsTile;
+#pragma unroll 1
+        for (int kk = 0; kk < BS; ++kk) {
+          const int k = BS * jb + kk;
+          if (k >= N) break;
+          if (k == 0) {
+            double F[S], NE[S];
+            ring_get<S>(base, PG::OFF_F, 0, c, F);
+            ring_get<S>(base, PG::OFF_NE, 0, c, NE);
+#pragma unroll
+            for (int i = 0; i < S; ++i) Eb[i] = -NE[i];
+#pragma unroll
+            for (int i = 0; i < S; ++i) Eb[i] = (c == i) ? Eb[i] + 1.0 : Eb[i];
+            transpose(H, F, tile, c);
+#pragma unroll
+            for (int i = 0; i < S; ++i) {  // lane S: Ebar column = z0, Fbar^T column = 0
+              Eb[i] = (c == S) ? tile[S * kLdsRow + i] : Eb[i];
+              H[i] = (c == S) ? 0.0 : H[i];
+            }
+            sel_slice<S>(Eb, g, Ebd);
+            sel_slice<S>(H, g, Hd);
+            if (g == 0) lds_put(tH, c, H);
+            wave_sync();
+          } else {
+            const double* mF = reinterpret_cast<const double*>(base + PG::OFF_F) +
+                               (k % (PG::D_F * BS)) * S * 16;
+            const double* mW = reinterpret_cast<const double*>(base + PG::OFF_NW) +
+                               (k % (PG::D_NW * BS)) * S * 16;
+            double NWd[4], Ftd[4], Htd[4], Zd[4], Z[S];
+            get_slice<S, 16>(mW, g, c, NWd);
+            get_slice_t<S, 16>(mF, g, c, Ftd);
+            get_slice_t<S, kLdsRow>(tH, g, c, Htd);  // Fbar^T of the previous step, transposed
+            copy(Zd, Hd);
+            gxy<C, true>(Zd, NWd, H);   // Z = W Fbar^T, this row's slice
+            put_slice<S, kLdsRow>(tZ, g, c, Zd);
+            wave_sync();
+            lds_get<double, S>(tZ, c, Z);
+            gxy<C, true>(Ebd, Htd, Z);  // Ebar -= Fbar W Fbar^T
+            zero(Hd);
+            gxy<C, false>(Hd, Ftd, Z);  // H' = F^T W Fbar^T
+            put_slice<S, kLdsRow>(tH, g, c, Hd);
+            wave_sync();
+            lds_get<double, S>(tH, c, H);
+          }
+          double* mEb = reinterpret_cast<double*>(base + PG::OFF_EB) + (k % (PG::D_EB * BS)) * S * 16;
+          double* mH = reinterpret_cast<double*>(base + PG::OFF_H) + (k % (PG::D_H * BS)) * S * 16;
+          put_slice<S, 16>(mEb, g, c, Ebd);
+          put_slice<S, 16>(mH, g, c, Hd);
         }
         wave_sync();
       }
