@@ -78,3 +78,14 @@ def test_exec_write_window_is_five(tmp_path):
     out, dropped, kept = nop_elide.elide(_func(body), chk)
     assert (dropped, kept) == (0, 1)  # an EXEC write three states back: the pair stays
     assert _check_lines(tmp_path, out)  # (and the checker still reports the short window)
+
+
+def test_lane_swap_writes_both_operands(tmp_path):
+    """v_permlane16/32_swap (the pipelined rerun's slice gathers) rewrite both operands:
+    a DPP read of the second one right after the swap is inside its window."""
+    for op in ("v_permlane16_swap_b32_e32", "v_permlane32_swap_b32_e32"):
+        w, _ = chk.vgpr_writes(f"{op} v6, v4")
+        assert w == {6, 4}
+        body = [f"\t{op} v6, v4",
+                "\tv_fmac_f64_dpp v[0:1], v[4:5], v[2:3] row_newbcast:0 row_mask:0xf bank_mask:0xf"]
+        assert _check_lines(tmp_path, _func(body))

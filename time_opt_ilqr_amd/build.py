@@ -57,8 +57,9 @@ def _digest():
     with open(os.path.join(REPO, "include", "hop.h"), "rb") as f:
         h.update(f.read())
     if ELIDE:  # the device code is what tools/nop_elide.py leaves of the compiler's
-        with open(os.path.join(REPO, "tools", "nop_elide.py"), "rb") as f:
-            h.update(f.read())
+        for t in ("nop_elide.py", "check_dpp_hazards.py"):  # the pads it drops follow the checker's rules
+            with open(os.path.join(REPO, "tools", t), "rb") as f:
+                h.update(f.read())
     h.update(b"elide" if ELIDE else b"plain")
     h.update(" ".join(FLAGS).encode())
     h.update(repr(sorted(EXTRA.items())).encode())

@@ -2056,8 +2056,15 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
   double best = 0.0;
   int tbest = 0;
   const int nb = (N + BS - 1) / BS;
+#ifdef HOP_PIPE_STAMP  // developer timing (tools/pipe_stamps.py): per wave, the clocks busy
+  // and waiting at the beat barrier; wave 0's sliced step by section
+  unsigned long long t_busy = 0, t_wait = 0, t_sec[3] = {0, 0, 0};
+#endif
 #pragma unroll 1
   for (int b = 0; b < nb + 3; ++b) {
+#ifdef HOP_PIPE_STAMP
+    const unsigned long long t_b0 = __builtin_amdgcn_s_memtime();
+#endif
     if (w == 2) {  // ---- stage blocks of beat b, one step per row
       const int k = BS * b + g % BS, kc = k < N ? k : N - 1;
       if (b < nb && TRAJ) {
@@ -2187,6 +2194,9 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
           if (k == 0) {
             copy(Gbd, Gkd);
           } else {
+#ifdef HOP_PIPE_STAMP
+            const unsigned long long s0 = __builtin_amdgcn_s_memtime();
+#endif
             const double* mE = reinterpret_cast<const double*>(base + PG::OFF_NE) +
                                (k % (PG::D_NE * BS)) * S * 16;
             double F[S], Fd[4], Ftd[4], NEd[4], NWd[4];
@@ -2201,9 +2211,15 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
             for (int gg = 0; gg < 4; ++gg) put_slice<S, kLdsRow>(tiles + gg * kLdsTile, g, c, NWd);
             diag_add<S, kLdsRow>(tile, c, 1e-9 - 1.0 - (-1.0));
             wave_sync();
+#ifdef HOP_PIPE_STAMP
+            const unsigned long long s1 = __builtin_amdgcn_s_memtime();
+#endif
             double NW[S];
             neg_inverse<C, S, kLdsRow>(NW, tile, c, mt, st);  // NW = -W
             wave_sync();
+#ifdef HOP_PIPE_STAMP
+            const unsigned long long s2 = __builtin_amdgcn_s_memtime();
+#endif
             if (g == 0) ring_put<S>(base, PG::OFF_NW, k % (PG::D_NW * BS), c, NW);
             double Wd[4], Zd[4], Z[S];
             sel_slice<S>(NW, g, Wd);
@@ -2214,6 +2230,13 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
             lds_get<double, S>(tiles, c, Z);
             copy(Gbd, Gkd);
             gxy<C, true>(Gbd, Ftd, Z);  // Gbar = G - F^T W F, this row's slice
+#ifdef HOP_PIPE_STAMP
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned long long s3 = __builtin_amdgcn_s_memtime();
+            t_sec[0] += s1 - s0;
+            t_sec[1] += s2 - s1;
+            t_sec[2] += s3 - s2;
+#endif
           }
           double* mB = reinterpret_cast<double*>(base + PG::OFF_GB) + (k % (PG::D_GB * BS)) * S * 16;
           put_slice<S, 16>(mB, g, c, Gbd);
@@ -2410,8 +2433,24 @@ __device__ __forceinline__ void pipe_problem(const LftArgs<double>& a, long long
         wave_sync();
       }
     }
+#ifdef HOP_PIPE_STAMP
+    const unsigned long long t_b1 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();  // one beat: every ring slot written this beat is read after it
+#ifdef HOP_PIPE_STAMP
+    t_busy += t_b1 - t_b0;
+    t_wait += __builtin_amdgcn_s_memtime() - t_b1;
+#endif
   }
+#ifdef HOP_PIPE_STAMP
+  if (lane == 0) {
+    atomicAdd(&g_hop_stamp[w], t_busy);
+    atomicAdd(&g_hop_stamp[4 + w], t_wait);
+    if (w == 0)
+      for (int j = 0; j < 3; ++j) atomicAdd(&g_hop_stamp[8 + j], t_sec[j]);
+    atomicAdd(&g_hop_stamp[15], 1ull);
+  }
+#endif
   // status: the OR of every row's ladder bits (the chains' rows repeat row 0)
   unsigned* stw = reinterpret_cast<unsigned*>(base + PG::OFF_MISC + 64);
   const bool contrib = (w == 0 || w == 1) ? g == 0 : g < BS;

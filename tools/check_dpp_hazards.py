@@ -63,6 +63,8 @@ def vgpr_writes(ins):
     dst = args[0].strip()
     if dst == "exec":
         return set(), True
+    if op.startswith(("v_permlane16_swap", "v_permlane32_swap", "v_swap_b")) and len(args) > 1:
+        return regs(dst) | regs(args[1].strip()), False  # both operands are written
     return regs(dst), False
 
 
