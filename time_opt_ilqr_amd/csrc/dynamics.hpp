@@ -63,6 +63,26 @@ HOP_HD inline void sin_cos(double v, double& s, double& c) {
 #endif
 }
 
+// tan from the sin and cos already formed (device): one IEEE division instead of a
+// second argument reduction and tan's own polynomial, within an ulp or two of libm's
+// tan (NumPy's is not bitwise libm's either).  Only the line search's rollouts use it
+// (FAST); the finite-difference linearisation keeps tan, whose ulp differences its 1/h
+// would amplify, and so does hop_rollout_f64, whose trajectory the linearisation and
+// the select consume (tests/test_gpu_real_lin.py regenerates its fixtures' inputs with
+// it).  HOP_TAN_SC=0 calls tan everywhere (A/B).
+#ifndef HOP_TAN_SC
+#define HOP_TAN_SC 1
+#endif
+HOP_HD inline double tan_sc(double v, double s, double c) {
+#if HOP_TAN_SC && defined(__HIP_DEVICE_COMPILE__)
+  (void)v;
+  return s / c;
+#else
+  (void)s, (void)c;
+  return tan(v);
+#endif
+}
+
 // Python's max(a, b) keeps a unless b > a (so a NaN b never wins)
 HOP_HD inline double py_max(double a, double b) { return b > a ? b : a; }
 
@@ -130,15 +150,18 @@ struct QuadTrig {
 };
 
 HOP_HD inline void quad_trig_phi(double phi, QuadTrig& t) { sin_cos(phi, t.sphi, t.cphi); }
+template <bool FAST = false>
 HOP_HD inline void quad_trig_th(double th, QuadTrig& t) {
   sin_cos(th, t.sth, t.cth);
-  t.tth = tan(th);
+  if constexpr (FAST) t.tth = tan_sc(th, t.sth, t.cth);
+  else t.tth = tan(th);
 }
 HOP_HD inline void quad_trig_psi(double psi, QuadTrig& t) { sin_cos(psi, t.spsi, t.cpsi); }
+template <bool FAST = false>
 HOP_HD inline QuadTrig quad_trig(const double* x) {
   QuadTrig t;
   quad_trig_phi(x[6], t);
-  quad_trig_th(x[7], t);
+  quad_trig_th<FAST>(x[7], t);
   quad_trig_psi(x[8], t);
   return t;
 }
@@ -208,15 +231,17 @@ HOP_HD inline void f_quadrotor_t(const double* x, const double* u, double dt, co
   o[11] = x[11] + dt * od2;
 }
 
+template <bool FAST = false>
 HOP_HD inline void f_quadrotor(const double* x, const double* u, double dt, double* o) {
-  f_quadrotor_t(x, u, dt, quad_trig(x), o);
+  f_quadrotor_t(x, u, dt, quad_trig<FAST>(x), o);
 }
 
-template <int SYS>
+// FAST: the line search's rollouts (tan from sin / cos)
+template <int SYS, bool FAST = false>
 HOP_HD inline void eval(const double* x, const double* u, double dt, double* o) {
   if constexpr (SYS == kDI) f_di(x, u, dt, o);
   else if constexpr (SYS == kCartpole) f_cartpole(x, u, dt, o);
-  else if constexpr (SYS == kQuadrotor) f_quadrotor(x, u, dt, o);
+  else if constexpr (SYS == kQuadrotor) f_quadrotor<FAST>(x, u, dt, o);
   else if constexpr (SYS == kPointmass) f_pointmass(x, u, dt, o);
   else f_segway(x, u, dt, o);
 }

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(TPB) void rollout_kernel(RolloutArgs a) {
     double u[m], xn[n];
 #pragma unroll
     for (int i = 0; i < m; ++i) u[i] = U[k * m + i];
-    eval<SYS>(x, u, a.dt, xn);
+    eval<SYS>(x, u, a.dt, xn);  // the trajectory the linearisation and select consume
     bool ok = true;
     double ss = 0.0;
 #pragma unroll
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
       const double so = pair_swap(sa), co = pair_swap(ca);
       t.sphi = h ? so : sa, t.cphi = h ? co : ca;
       t.spsi = h ? sa : so, t.cpsi = h ? ca : co;
-      quad_trig_th(x[7], t);
+      quad_trig_th<true>(x[7], t);
       double xn[n];
       f_quadrotor_t(x, u, a.dt, t, xn);
       bool f = true;
@@ -439,7 +439,7 @@ __global__ __launch_bounds__(TPB) void linesearch_kernel(FwdArgs a) {
     if (k < T) ok = stage_inc<n, m, SH, WM>(cl, b, x, u, acc, diag) && ok;
 #pragma unroll
     for (int i = 0; i < m; ++i) Uc[k * m + i] = u[i];
-    eval<SYS>(x, u, a.dt, xn);
+    eval<SYS, true>(x, u, a.dt, xn);
     bool f = true;
 #pragma unroll
     for (int i = 0; i < n; ++i) f = f && fin(xn[i]);
