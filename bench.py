@@ -607,7 +607,7 @@ def _self_launch(args, argv):
     process has touched the GPU: torch.cuda.device_count() does not initialise it on
     this image) and exit with its return code."""
     import subprocess
-    if not args.dry_run:
+    if not args.dry_run and args.dist_backend == "nccl":
         import torch
         have = torch.cuda.device_count()
         if have < args.gpus:
@@ -670,8 +670,13 @@ def main(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo + CPU tensors + the oracle stand-in of tests/ (a "
                          "rehearsal of the rank/shard/gather path, never a measurement)")
-    ap.add_argument("--dry-out", default=None,
-                    help="--dry-run: rank 0 writes the gathered (T*, J*) here (.npz)")
+    ap.add_argument("--dry-out", "--gather-out", dest="dry_out", default=None,
+                    help="rank 0 writes the gathered (T*, J*) here (.npz); --dry-run or N > 1")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: nccl (RCCL over xGMI, one rank per GPU; the default and the "
+                         "driver's) or gloo: the real kernels with the collectives through the "
+                         "host, every rank on device LOCAL_RANK mod the visible devices -- a "
+                         "rehearsal of this path on a one-GPU box, never a scaling measurement")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the side timing of the other layout (profiling passes)")
     ap.add_argument("--no-anchor", action="store_true",
@@ -702,7 +707,8 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
     dry = args.dry_run
-    if not dry and torch.cuda.device_count() < world:
+    gloo = args.dist_backend == "gloo"
+    if not dry and not gloo and torch.cuda.device_count() < world:
         print(f"bench.py: {world} ranks but {torch.cuda.device_count()} HIP device(s) visible",
               file=sys.stderr, flush=True)
         sys.exit(2)
@@ -729,10 +735,15 @@ def main(argv=None):
             dist.init_process_group("gloo")
         dev = torch.device("cpu")
     else:
+        # gloo rehearsal: ranks share the visible devices (local mod count)
+        ldev = local % max(torch.cuda.device_count(), 1) if gloo else local
         if world > 1:
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        dev = torch.device("cuda", local if world > 1 else 0)
+            torch.cuda.set_device(ldev)
+            if gloo:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", ldev))
+        dev = torch.device("cuda", ldev if world > 1 else 0)
         if rank == 0:
             from time_opt_ilqr_amd import build as hop_build
             hop_build.build(verbose=False)
@@ -814,7 +825,7 @@ def main(argv=None):
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        hd.all_reduce_max(t)
         elapsed, kern_ms = float(t[0]), float(t[1])
     if gathered is None:
         gathered = (r.t_star, r.j_star)
@@ -828,7 +839,7 @@ def main(argv=None):
     # every rank's shard must be clean, not only rank 0's
     if world > 1:
         ok = torch.tensor([0 if status_ok else 1], dtype=torch.int32, device=dev)
-        dist.all_reduce(ok, op=dist.ReduceOp.MAX)
+        hd.all_reduce_max(ok)
         status_ok = int(ok.item()) == 0
     if dry:
         if rank == 0 and args.dry_out:
@@ -845,6 +856,10 @@ def main(argv=None):
         if world > 1:
             dist.destroy_process_group()
         return
+
+    if rank == 0 and args.dry_out and world > 1:  # the gathered selection (tests)
+        import numpy as np
+        np.savez(args.dry_out, t_star=gathered[0].cpu().numpy(), j_star=gathered[1].cpu().numpy())
 
     # the config-4-shard anchor at N=1: the per-GPU batch of the N>1 lines (32,768),
     # so a 1->N curve can compare equal per-GPU work (a side figure, not `value`)
@@ -1035,7 +1050,8 @@ def main(argv=None):
                        "N": N, "t_min": info["t_min"], "t_max": info["t_max"],
                        "layout": info.get("layout", "batch-major"),
                        **({"rho_reg": info["rho_reg"]} if "rho_reg" in info else {}),
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       **({"dist_backend": args.dist_backend} if world > 1 else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
             "h2d_inclusive": h2d,

@@ -506,6 +506,12 @@ def main_ilqr():
         ilqr_capture(*case)
 
 
+# round 6: eight problems (was two), horizons from 1 to N, so the per-step gain
+# checks of tests/test_gpu_parity.py see short, mid and full horizons
+RICCATI_SYNTH = ("n12_m4_N100", 12, 4, 100, [7000, 7001, 7002, 7003, 7004, 7005, 7006, 7007],
+                 [100, 57, 1, 13, 34, 77, 99, 64], 1e-3)
+
+
 def main():
     np.seterr(all="ignore")
     synthetic_lft("s13_m4_N100", 13, 4, 100, 1000, 4, 40, 100)
@@ -516,7 +522,7 @@ def main():
     synthetic_lft_rlist("s7_m3_N30", 7, 3, 30, 6000)
     real_capture("DI_N50", dict(N=50), ref_systems.make_double_integrator, T_min=10, T_max=50)
     real_capture("Quad_N160", {}, ref_systems.make_quadrotor, max_iter=3)
-    riccati_synth("n12_m4_N100", 12, 4, 100, [7000, 7001], [100, 57], 1e-3)
+    riccati_synth(*RICCATI_SYNTH)
     riccati_shift("n6_m2_N60", 6, 2, 60, 7100, 45, 15, 1e-6)
     riccati_fail("n4_m2_N20", 4, 2, 20, 7200)
     bruteforce_synth("n4_m2_N40", 4, 2, 40, 7300, 40, 0.05)
@@ -877,7 +883,10 @@ def main_r2():
 
 
 if __name__ == "__main__":
-    if "--r4" in sys.argv:  # round-4 fixtures only
+    if "--r6" in sys.argv:  # round-6 fixtures only
+        np.seterr(all="ignore")
+        riccati_synth(*RICCATI_SYNTH)
+    elif "--r4" in sys.argv:  # round-4 fixtures only
         main_r4()
     elif "--r3" in sys.argv:  # round-3 fixtures only
         main_r3()

@@ -823,3 +823,34 @@ def test_legacy_riccati_passes_vs_reference(dev, golden_dir, n, m):
         assert _rel(_np(r1.Vxx)[0, :L + 1], d[f"{tag}_p{i}_m1_Vxx"]) <= tol
         assert _rel(_np(r1.Vx)[0, :L + 1], d[f"{tag}_p{i}_m1_Vx"]) <= tol
         assert _rel(_np(r1.V0)[0, :L + 1], d[f"{tag}_p{i}_m1_V0"]) <= tol
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_zero_step_is_rejected_like_the_reference(dev, golden_dir, tag):
+    """the reference rolls out every candidate with the same F as the
+    current trajectory, so a zero step (K = 0, k = 0) reproduces X bit for bit and
+    J_new < J_old (strict, solver.py:233-286) rejects it.  On the device the first
+    iteration's X comes from hop_rollout_f64 and the candidates from the line search's
+    rollouts: they must be the same arithmetic, or an ulp of J accepts the step."""
+    import torch
+    from time_opt_ilqr_amd import engine
+    d, sid, wrap, obs = _case(golden_dir, tag)
+    N, dt = int(d["N"]), float(d["dt"])
+    n, m = d["Q"].shape[0], d["R"].shape[0]
+    Bn = 64
+    rng = np.random.default_rng(61)
+    x0 = d["x0"] + 0.05 * rng.standard_normal((Bn, n))
+    U = d["u_ref"].reshape(1, 1, -1) + 0.1 * rng.standard_normal((Bn, N, m))
+    X = engine.rollout(sid, _t(x0, dev), _t(U, dev), dt)
+    T = np.full(Bn, N, dtype=np.int32)
+    T[::3] = N // 2
+    K = torch.zeros((Bn, N, m, n), dtype=torch.float64, device=dev)
+    k = torch.zeros((Bn, N, m), dtype=torch.float64, device=dev)
+    r = engine.forward_linesearch(sid, X, _t(U, dev), T, K, k, _cost(d, wrap, obs, dev), dt)
+    torch.cuda.synchronize()
+    fin = np.isfinite(_np(r.J_old))
+    assert fin.any()
+    acc = _np(r.accepted)  # alpha index, -1 none accepted
+    assert (acc == -1).all(), np.nonzero(acc != -1)[0][:8]
+    assert torch.equal(r.X[torch.as_tensor(fin)], X[torch.as_tensor(fin)])
+    assert torch.equal(r.J, r.J_old)

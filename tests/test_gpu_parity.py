@@ -15,6 +15,7 @@ import os
 import numpy as np
 import pytest
 
+from gain_check import assert_per_step
 from oracle import hop_oracle as orc
 
 pytestmark = pytest.mark.gpu
@@ -251,10 +252,15 @@ def test_select_horizon_kernel(dev):
 # ---------------------------------------------------------------------------
 
 def test_riccati_truncated_and_expand_vs_reference(dev, golden_dir):
+    """Eight synthetic problems (horizons 1 .. 100) against the reference's own
+    backward_pass_truncated / value_expansions_and_gains_prefix output, every step
+    on its own (tests/gain_check.py)."""
     from time_opt_ilqr_amd import engine
     d = _load(golden_dir, "riccati_synth_n12_m4_N100.npz")
     n, m, N = int(d["n"]), int(d["m"]), int(d["N"])
     probs = [orc.synth_riccati_problem(int(sd), n, m, N) for sd in d["seeds"]]
+    cnt = len(probs)
+    assert cnt >= 8
     st = lambda j: np.stack([p[j] for p in probs])  # noqa: E731
     A, B, X, U, xg, ur, Q, R = (st(j) for j in range(8))
     Qf = np.stack([orc.terminal_weight(p[8], n) for p in probs])
@@ -262,17 +268,17 @@ def test_riccati_truncated_and_expand_vs_reference(dev, golden_dir):
     args = [_t(x, dev) for x in (A, B, X, U, xg, ur, Q, R, Qf)]
     r0 = engine.riccati(*args, T, float(d["lm"]), mode=0)
     r1 = engine.riccati(*args, T, float(d["lm"]), mode=1, w_stage=float(d["w_stage"]))
-    assert r0.status.cpu().numpy().tolist() == [0, 0]
-    assert r1.status.cpu().numpy().tolist() == [0, 0]
-    for i in range(2):
+    assert r0.status.cpu().numpy().tolist() == [0] * cnt
+    assert r1.status.cpu().numpy().tolist() == [0] * cnt
+    for i in range(cnt):
         Ti = int(T[i])
-        assert _rel(r0.k[i, :Ti].cpu().numpy(), d[f"p{i}_k"]) <= RTOL64
-        assert _rel(r0.K[i, :Ti].cpu().numpy(), d[f"p{i}_K"]) <= RTOL64
-        assert _rel(r1.K[i, :Ti].cpu().numpy(), d[f"p{i}_K2"]) <= RTOL64
-        assert _rel(r1.k[i, :Ti].cpu().numpy(), d[f"p{i}_k2"]) <= RTOL64
-        assert _rel(r1.Vxx[i, :Ti + 1].cpu().numpy(), d[f"p{i}_Vxx"]) <= RTOL64
-        assert _rel(r1.Vx[i, :Ti + 1].cpu().numpy(), d[f"p{i}_Vx"]) <= RTOL64
-        assert _rel(r1.V0[i, :Ti + 1].cpu().numpy(), d[f"p{i}_V0"]) <= RTOL64
+        assert_per_step(r0.k[i, :Ti].cpu().numpy(), d[f"p{i}_k"], RTOL64, f"{i} k")
+        assert_per_step(r0.K[i, :Ti].cpu().numpy(), d[f"p{i}_K"], RTOL64, f"{i} K")
+        assert_per_step(r1.K[i, :Ti].cpu().numpy(), d[f"p{i}_K2"], RTOL64, f"{i} K2")
+        assert_per_step(r1.k[i, :Ti].cpu().numpy(), d[f"p{i}_k2"], RTOL64, f"{i} k2")
+        assert_per_step(r1.Vxx[i, :Ti + 1].cpu().numpy(), d[f"p{i}_Vxx"], RTOL64, f"{i} Vxx")
+        assert_per_step(r1.Vx[i, :Ti + 1].cpu().numpy(), d[f"p{i}_Vx"], RTOL64, f"{i} Vx")
+        assert_per_step(r1.V0[i, :Ti + 1].cpu().numpy(), d[f"p{i}_V0"], RTOL64, f"{i} V0")
 
 
 def test_value_expansions_shift_and_wrap(dev, golden_dir):
@@ -320,8 +326,8 @@ def test_real_DI_dropins(dev, golden_dir):
                                           float(d["alpha"]), int(d["bwd_T_star"]),
                                           lm_lambda=float(d["bwd_lm"]))
     assert ok
-    assert _rel(np.array(k), d["bwd_k"]) <= RTOL64
-    assert _rel(np.array(K), d["bwd_K"]) <= RTOL64
+    assert_per_step(np.array(k), d["bwd_k"], RTOL64, "k")
+    assert_per_step(np.array(K), d["bwd_K"], RTOL64, "K")
     bf = hs.bruteforce_all_Jt_backward_expansion(
         list(d["bwd_A"]), list(d["bwd_B"]), d["bwd_X"], d["bwd_U"], d["xg"], d["u_ref"],
         d["Q"], d["R"], float(d["alpha"]), float(d["w"]), len(d["bf_J"]))

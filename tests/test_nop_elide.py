@@ -89,3 +89,122 @@ def test_lane_swap_writes_both_operands(tmp_path):
         body = [f"\t{op} v6, v4",
                 "\tv_fmac_f64_dpp v[0:1], v[4:5], v[2:3] row_newbcast:0 row_mask:0xf bank_mask:0xf"]
         assert _check_lines(tmp_path, _func(body))
+
+
+# ---------------------------------------------------------------------------
+# round 6: gfx950's other software-managed hazards (tools/check_dpp_hazards.py
+# docstring): one known-bad sequence per rule that the checker must reject, and the
+# same sequence with enough wait states that it must accept
+# ---------------------------------------------------------------------------
+
+RULES = {
+    # rule: (producer, consumer, wait states the consumer needs)
+    "trans": ("\tv_rcp_f64_e32 v[4:5], v[6:7]",
+              "\tv_fma_f64 v[8:9], v[4:5], v[10:11], v[12:13]", 1),
+    "vmemsgpr": ("\tv_readfirstlane_b32 s7, v3",
+                 "\tbuffer_load_dwordx4 v1, s[20:23], s7 offen nt lds", 5),
+    "vmemsgpr_desc": ("\tv_readlane_b32 s23, v255, 7",
+                      "\tbuffer_load_dwordx4 v1, s[20:23], s4 offen nt lds", 5),
+    "rwlane": ("\tv_cmp_gt_f64_e64 s[10:11], 0, v[50:51]",
+               "\tv_readlane_b32 s0, v254, s10", 4),
+    "divfmas": ("\tv_div_scale_f64 v[30:31], vcc, v[32:33], v[32:33], v[84:85]",
+                "\tv_div_fmas_f64 v[30:31], v[30:31], v[192:193], v[196:197]", 4),
+    "readlane": ("\tv_add_f64 v[8:9], v[10:11], v[12:13]",
+                 "\tv_readfirstlane_b32 s3, v8", 1),
+    "permlane": ("\tv_add_f64 v[8:9], v[10:11], v[12:13]",
+                 "\tv_permlane32_swap_b32_e32 v8, v20", 2),
+    "m0lds": ("\ts_mov_b32 m0, s5",
+              "\tbuffer_load_dwordx4 v1, s[20:23], s4 offen lds", 1),
+}
+
+
+def _seq(prod, cons, nops):
+    return _func([prod] + ["\ts_nop 0"] * nops + [cons])
+
+
+def test_each_rule_rejects_its_short_window_and_accepts_the_full_one(tmp_path):
+    for rule, (prod, cons, ws) in RULES.items():
+        short = _check_lines(tmp_path, _seq(prod, cons, ws - 1))
+        assert short, (rule, "short window not flagged")
+        assert any(rule.split("_")[0] in why for _, _, why in short), (rule, short)
+        assert not _check_lines(tmp_path, _seq(prod, cons, ws)), (rule, "full window flagged")
+
+
+def test_trans_rule_spares_a_trans_consumer_and_other_registers(tmp_path):
+    # a transcendental reading a transcendental's result is not the forwarding case
+    ok1 = _func(["\tv_rcp_f64_e32 v[4:5], v[6:7]", "\tv_sqrt_f64_e32 v[8:9], v[4:5]"])
+    ok2 = _func(["\tv_rcp_f64_e32 v[4:5], v[6:7]", "\tv_fma_f64 v[8:9], v[14:15], v[10:11], v[12:13]"])
+    assert not _check_lines(tmp_path, ok1) and not _check_lines(tmp_path, ok2)
+
+
+def test_vmem_window_follows_a_branch_into_the_label(tmp_path):
+    # the VALU SGPR write sits on the branch path, not the fall-through path
+    body = ["\ts_cbranch_scc1 .LBB0_9", "\ts_nop 7", "\ts_nop 7", ".LBB0_9:",
+            "\tbuffer_load_dwordx4 v1, s[20:23], s7 offen nt lds"]
+    lines = _func(["\tv_readfirstlane_b32 s7, v3"] + body)
+    assert _check_lines(tmp_path, lines)
+    # with the producer far enough back on both paths, nothing is flagged
+    assert not _check_lines(tmp_path, _func(["\tv_readfirstlane_b32 s7, v3", "\ts_nop 4"] + body))
+
+
+def test_pad_inside_a_new_rule_window_is_kept(tmp_path):
+    """The elider refuses a removal that opens any modelled window: here the pair is
+    all that separates a v_rcp_f64 result from its non-transcendental consumer."""
+    body = ["\tv_rcp_f64_e32 v[4:5], v[6:7]", HN, HN,
+            "\tv_fma_f64 v[8:9], v[4:5], v[10:11], v[12:13]"]
+    lines = _func(body)
+    out, dropped, kept = nop_elide.elide(lines, chk)
+    assert (dropped, kept) == (0, 1) and out == lines
+
+
+VM = "\ts_nop 2 ; vmnop"
+
+
+def test_vmem_pad_dropped_when_safe_and_kept_after_a_readlane(tmp_path):
+    dma = ["\ts_mov_b32 s9, m0", "\ts_mov_b32 m0, s5", "\ts_nop 0",
+           "\tbuffer_load_dwordx4 v1, s[20:23], s7 offen nt lds", "\ts_mov_b32 m0, s9"]
+    safe = _func(["\tv_readfirstlane_b32 s7, v3", "\ts_nop 4", VM] + dma)
+    out, dropped, kept = nop_elide.elide(safe, chk)
+    assert (dropped, kept) == (1, 0) and not any("vmnop" in l for l in out)
+    assert not _check_lines(tmp_path, out)
+    risky = _func(["\tv_readlane_b32 s23, v255, 7", VM] + dma)
+    out, dropped, kept = nop_elide.elide(risky, chk)
+    assert (dropped, kept) == (0, 1) and out == risky
+    assert not _check_lines(tmp_path, out)
+    assert _check_lines(tmp_path, [l for l in risky if "vmnop" not in l])
+
+
+def test_pads_split_by_an_alignment_directive_are_not_a_pair():
+    """a marked pad, a .p2align, then the next block's marked pad: removing
+    them as a pair would leave the block's 8-byte instructions at 4 mod 8."""
+    body = ["\tv_add_f64 v[8:9], v[10:11], v[12:13]",
+            "\tv_add_f64 v[14:15], v[10:11], v[12:13]",
+            "\tv_add_f64 v[16:17], v[10:11], v[12:13]",
+            HN, "\t.p2align 3", HN,
+            "\tv_fmac_f64_dpp v[0:1], v[4:5], v[2:3] row_newbcast:0 row_mask:0xf bank_mask:0xf"]
+    lines = _func(body)
+    out, dropped, kept = nop_elide.elide(lines, chk)
+    assert out == lines and dropped == 0
+
+
+def _split(between):
+    return ["\t.text", "kern:", "\t;;#ASMSTART",
+            "\tds_read_b64 v[10:11], v2 offset:0", "\tds_read_b64 v[12:13], v2 offset:8 ; hop_ldissue",
+            "\t;;#ASMEND", *between, "\t;;#ASMSTART", "\ts_waitcnt lgkmcnt(0) ; hop_ldwait",
+            "\t;;#ASMEND", "\tv_add_f64 v[20:21], v[10:11], v[12:13]", "\ts_endpgm"]
+
+
+def test_split_asm_load_destinations_untouched_until_the_wait(tmp_path):
+    """ADVICE r05 (lft_sweep_v2.hip sym_issue13 / sym_wait_average13): nothing between
+    the marked load statement and its marked wait may copy, spill or overwrite a load
+    destination."""
+    ok = _split(["\tv_add_f64 v[30:31], v[32:33], v[34:35]"])
+    assert not _check_lines(tmp_path, ok)
+    for bad in ("\tv_mov_b64_e32 v[40:41], v[12:13]",            # a copy before the data lands
+                "\tscratch_store_dwordx2 off, v[10:11], s33",    # a spill
+                "\tv_mov_b32_e32 v11, 0"):                       # the register reused
+        assert _check_lines(tmp_path, _split([bad])), bad
+    # no wait before the function ends
+    lines = _split([])
+    lines = [l for l in lines if "hop_ldwait" not in l]
+    assert _check_lines(tmp_path, lines)

@@ -79,21 +79,28 @@ def up_to_date():
 
 def check_hazards(objdir, verbose=True):
     """Fail the build if any inline-asm DPP source can be read inside its VALU
-    write hazard window (tools/check_dpp_hazards.py; hipcc does not pad asm)."""
+    write hazard window, or any other modelled gfx950 hazard is met
+    (tools/check_dpp_hazards.py; hipcc does not pad asm).  Returns the number of
+    hazards only listed (developer builds under HOP_HAZARD_REPORT); build() writes no
+    up-to-date stamp for such a library, so nothing reuses it as a checked build."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     import check_dpp_hazards as chk
+    # developer A/B builds only: list, don't fail (product builds always fail)
+    report = os.environ.get("HOP_HAZARD_REPORT") if DEV else None
+    listed = 0
     for src in _sources():
         s = os.path.join(objdir, src.replace(".hip", "") + f"-hip-amdgcn-amd-amdhsa-{ARCH}.s")
         n, bad = chk.check(s)
         if verbose:
             print(f"[hop] {os.path.basename(s)}: {n} DPP instructions, {len(bad)} hazards")
-        report = os.environ.get("HOP_HAZARD_REPORT")  # developer A/B builds only: list, don't fail
         if bad and report:
+            listed += len(bad)
             with open(report, "a") as f:
                 for fn, text, why in bad:
                     f.write(f"{src}\t{fn}\t{text}\t{why}\n")
         elif bad:
-            raise RuntimeError(f"DPP hazard in {src}: {bad[:3]}")
+            raise RuntimeError(f"hazard in {src}: {bad[:3]}")
+    return listed
 
 
 def _run_all(cmds, verbose):
@@ -130,7 +137,7 @@ def _compile_elided(hipcc, objdir, objs, verbose):
             f.write("\n".join(out))
         if verbose:
             print(f"[hop] {src}: {dropped} hazard-pad pairs dropped, {kept} kept")
-    check_hazards(objdir, verbose)
+    listed = check_hazards(objdir, verbose)
     for src in _sources():
         b = base[src]
         checked = b + f"-hip-amdgcn-amd-amdhsa-{ARCH}.s"
@@ -146,6 +153,7 @@ def _compile_elided(hipcc, objdir, objs, verbose):
                "-fcuda-include-gpubinary", "-Xclang", base[src] + ".hipfb", "-c",
                os.path.join(CSRC, src), "-o", obj]
               for src, obj in zip(_sources(), objs)], verbose)
+    return listed
 
 
 def build(force=False, jobs=None, verbose=True):
@@ -163,7 +171,7 @@ def build(force=False, jobs=None, verbose=True):
     os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, src.replace(".hip", ".o")) for src in _sources()]
     if ELIDE:
-        _compile_elided(hipcc, objdir, objs, verbose)
+        listed = _compile_elided(hipcc, objdir, objs, verbose)
     else:
         procs = []
         for src, obj in zip(_sources(), objs):
@@ -176,13 +184,18 @@ def build(force=False, jobs=None, verbose=True):
         for p in procs:
             if p.wait() != 0:
                 raise RuntimeError("hipcc failed")
-        check_hazards(objdir, verbose)
+        listed = check_hazards(objdir, verbose)
     tmp = LIB + ".tmp"
     cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp]
     if verbose:
         print("[hop]", " ".join(cmd))
     subprocess.check_call(cmd)
     os.replace(tmp, LIB)
+    if listed:  # hazards listed, not failed: no stamp (up_to_date() stays False)
+        if os.path.exists(_stamp_path()):
+            os.remove(_stamp_path())
+        print(f"[hop] {listed} hazards listed in $HOP_HAZARD_REPORT: no build stamp written")
+        return LIB
     with open(_stamp_path(), "w") as f:
         f.write(_digest())
     return LIB

@@ -65,13 +65,17 @@ HOP_HD inline void sin_cos(double v, double& s, double& c) {
 
 // tan from the sin and cos already formed (device): one IEEE division instead of a
 // second argument reduction and tan's own polynomial, within an ulp or two of libm's
-// tan (NumPy's is not bitwise libm's either).  Only the line search's rollouts use it
-// (FAST); the finite-difference linearisation keeps tan, whose ulp differences its 1/h
-// would amplify, and so does hop_rollout_f64, whose trajectory the linearisation and
-// the select consume (tests/test_gpu_real_lin.py regenerates its fixtures' inputs with
-// it).  HOP_TAN_SC=0 calls tan everywhere (A/B).
+// tan.  Off by default since round 6: the reference evaluates one F for
+// every rollout, so a zero step of its line search reproduces the current X bit for
+// bit and is rejected (J_new < J_old is strict, solver.py:233-286); with this tan in
+// the line search's rollouts only, the first iteration's zero step moved X by an ulp
+// against hop_rollout_f64's trajectory and could be accepted on rounding.  The FD
+// linearisation (1/h amplifies ulps) and hop_rollout_f64 (the fixtures of
+// tests/test_gpu_real_lin.py are its outputs) cannot take it, so every rollout keeps
+// libm's tan (the sincos above is bitwise the separate calls and stays).  It saved 4.3 %
+// of the line search (profiles/r05_tan_sc_ab.jsonl).  HOP_TAN_SC=1: the A/B.
 #ifndef HOP_TAN_SC
-#define HOP_TAN_SC 1
+#define HOP_TAN_SC 0
 #endif
 HOP_HD inline double tan_sc(double v, double s, double c) {
 #if HOP_TAN_SC && defined(__HIP_DEVICE_COMPILE__)

@@ -17,6 +17,14 @@
 #include "lu_pivot.hpp"
 #include "wrap.hpp"
 
+// Opening pad of every inline-asm statement that issues a VMEM instruction reading an
+// SGPR operand (the LDS-DMA statements): three wait states, so that no descriptor /
+// soffset SGPR is read within five wait states of a VALU write of it (v_readlane /
+// v_readfirstlane just before the statement; hipcc pads only its own pairs).  Marked
+// "vmnop": the build drops each one the compiled code around it makes unnecessary
+// (tools/nop_elide.py) and checks the result (tools/check_dpp_hazards.py).
+#define HOP_VMNOP "s_nop 2 ; vmnop\n\t"
+
 namespace hop {
 
 constexpr int kRowLanes = 16;     // lanes per problem

@@ -102,7 +102,8 @@ struct LftArgs {
   T* dbg_efg;        // [B][n][3][s][s] or null  (E_k, F_k, G_k)
   T* dbg_pre;        // [B][n][3][s][s] or null  (Ebar_k, Fbar_k, Gbar_k)
   int traj;          // 1: A/B/Q/QT unused, blocks built in-kernel from `tr`
-  int cond;          // SchedCond: bit 0 rerun launch (only ST_RERUN problems), bit 1 flag all
+  int cond;          // SchedCond: bit 0 rerun launch (only ST_RERUN problems), bit 1 flag all;
+                     // kCondRerunOnly: dispatch_lft_small launches only its LFT rerun
   int tile64;        // 1: A/B/Q/QT in the tile64 layout [B/64][nalloc][block elems][64]
   TrajArgs<T> tr;
 };
@@ -244,6 +245,11 @@ hipError_t dispatch_dynamics(const DynArgs& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_lft(const LftArgs<T>& a, hipStream_t stream);
 hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream);
+// the small-s row-group kernel's hand-overs go to lft_small.hip's LFT instantiation
+// (its rerun launch alone): LftArgs.cond = 1 | kCondRerunOnly
+constexpr int kCondRerunOnly = 64;
+// fp64 s <= 5 augmented blocks on the conditioned kernel's row groups (lft_sweep_v2.hip)
+hipError_t dispatch_cond_small(const LftArgs<double>& a, hipStream_t stream);
 hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream);
 template <class T>
 hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream);

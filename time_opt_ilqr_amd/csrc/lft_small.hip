@@ -53,6 +53,7 @@ __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc
                                       unsigned soff) {
   unsigned keep;
   asm volatile(
+      HOP_VMNOP  // (hop_device.hpp)
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
@@ -77,18 +78,18 @@ __device__ __forceinline__ void dma_grp(unsigned voff, __amdgpu_buffer_rsrc_t rs
 #define HOP_G(OFF) "buffer_load_dwordx4 %1, %2, %4 offen offset:" #OFF " nt lds\n\t"
   const unsigned l = __builtin_amdgcn_readfirstlane(lds), so = __builtin_amdgcn_readfirstlane(soff);
   if constexpr (NL == 1)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) "s_mov_b32 m0, %0"
+    asm volatile(HOP_VMNOP "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) "s_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
   else if constexpr (NL == 2)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
+    asm volatile(HOP_VMNOP "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
                  "s_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
   else if constexpr (NL == 3)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
+    asm volatile(HOP_VMNOP "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
                  HOP_G(2048) "s_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
   else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
+    asm volatile(HOP_VMNOP "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" HOP_G(0) HOP_G(1024)
                  HOP_G(2048) HOP_G(3072) "s_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(voff), "s"(rsrc), "s"(l), "s"(so) : "memory");
 #undef HOP_G
@@ -719,7 +720,7 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
   // 0: the LFT association alone (HOP_OPT_REFERENCE_ASSOC)
   const int cmode = opt(HOP_OPT_REFERENCE_ASSOC) ? 0 : g_opt_variant == 62 ? 2 : 1;
   auto go2 = [&](auto kc, auto kl, LaunchGeo g) {
-    if (cmode == 0) return go1(kl, g);
+    if (cmode == 0 || (a.cond & kCondRerunOnly)) return go1(kl, g);
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
     const hipError_t e = launch(kc, g, c);
@@ -797,7 +798,9 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
   // the trajectory form run the same arithmetic.  HOP_OPT_REFERENCE_ASSOC: the LFT
   // kernel alone (the reference association; comparator for the tests and tools)
   auto gocond = [&](auto kc, auto kl, LaunchGeo g) {
-    if (opt(HOP_OPT_REFERENCE_ASSOC)) return go1(kl, g);
+    // the rerun launch alone: the hand-overs of lft_sweep_v2.hip's small-s row-group
+    // kernel (a.cond = 1 | kCondRerunOnly)
+    if (opt(HOP_OPT_REFERENCE_ASSOC) || (a.cond & kCondRerunOnly)) return go1(kl, g);
     LftArgs<T> c = a;
     c.cond = opt(HOP_OPT_FORCE_HANDOVER) ? 2 : 0;  // 2: hand every problem over (tests)
     const hipError_t e = launch(kc, g, c);

@@ -240,6 +240,22 @@ constexpr bool has_peps() {
   return false;
 }
 
+// small-s row groups (s <= 5 fp64 augmented blocks at batches that leave the
+// one-problem-per-lane kernel most SIMDs idle): the
+// conditioned kernel's own layout -- four problems per wave, one per 16-lane DPP row,
+// s of its lanes busy -- so B = 4,096 runs 1,024 waves instead of 64.  Unhalved
+// symmetric sums (SYM2) and the congruence query (WQ, the terminal block's X sweep
+// stopped one pivot short: SweepQP) like the s = 13 default; the image reads are
+// plain (no LDS-pipelined sweeps: SweepQSym / SweepQAB exist for s = 13 only).
+struct SchedCondSmall : SchedCond {
+  static constexpr int SYM2 = 1, NEWT = 0, PEPS = 0, WQ = 1, SMALLS = 1;
+};
+template <class C>
+constexpr bool has_smalls() {
+  if constexpr (requires { C::SMALLS; }) return C::SMALLS != 0;
+  return false;
+}
+
 // fp32 blocks (config 5): the predict's two products A~ and A T on the f32 matrix
 // cores, one problem per v_mfma_f32_16x16x4_f32 tile
 struct SchedCondMfma : SchedCond {
@@ -816,10 +832,17 @@ __device__ unsigned long long g_hop_stamp[16];
 // ---------------------------------------------------------------------------
 // LDS-DMA streaming of one step's blocks into the wave's images
 // ---------------------------------------------------------------------------
+// Every LDS-DMA statement opens with HOP_VMNOP: three wait states, so that with the
+// M0 write and its own s_nop 0 no buffer_load reads a descriptor or soffset SGPR within
+// five wait states of a VALU write of it (the compiler reloads spilled SGPRs with
+// v_readlane right before the statement; it pads only its own instruction pairs).
+// The build drops every such pad the compiled code around it makes unnecessary
+// (tools/nop_elide.py) and checks the result (tools/check_dpp_hazards.py).
 __device__ __forceinline__ void dma16(unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned lds,
                                       unsigned soff) {
   unsigned keep;
   asm volatile(
+      HOP_VMNOP         // VALU SGPR write -> VMEM read (tools/check_dpp_hazards.py)
       ".p2align 3\n\t"  // the 8-byte buffer_load at 0 mod 8 (code placement)
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %0, m0\n\t"
@@ -858,6 +881,7 @@ __device__ __forceinline__ void dma_traj10(const unsigned (&va)[5], const unsign
 #define HOP_M0(OFF) "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\t"
 #define HOP_PO(R, V, SO, IO) "buffer_load_dwordx4 %[" #V "], %[" #R "], %[" #SO "] offen offset:" #IO " lds\n\t"
   asm volatile(
+      HOP_VMNOP
       ".p2align 3\n\t"
       "s_mov_b32 %[keep], m0\n\t"
       HOP_M0(%[o0]) HOP_PO(ra, a0, sa, 0) HOP_PO(ra, a1, sa, 1024) HOP_PO(ra, a2, sa, 2048)
@@ -899,6 +923,7 @@ __device__ __forceinline__ void dma_step20p(const unsigned (&vm)[6], const unsig
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      HOP_VMNOP
       ".p2align 3\n\t"
       "s_mov_b32 %[keep], m0\n\t"
       "s_mov_b32 %[elo], exec_lo\n\t"
@@ -945,6 +970,7 @@ __device__ __forceinline__ void dma_step20(const unsigned (&vm)[6], const unsign
   HOP_M0(O0) HOP_PO(R, v0, sm, 0) HOP_PO(R, v1, sm, 1024) HOP_PO(R, v2, sm, 2048)            \
   HOP_PO(R, v3, sm, 3072) HOP_M0(O4) HOP_PO(R, v4, sm, 0) HOP_PO(R, v5, sm, 1024)
   asm volatile(
+      HOP_VMNOP
       ".p2align 3\n\t"
       "s_mov_b32 %[keep], m0\n\t"
       HOP_IMG(rq, %[q0], %[q4]) HOP_IMG(ra, %[a0], %[a4])
@@ -974,6 +1000,7 @@ __device__ __forceinline__ void dma_stepQT(const unsigned (&vm)[6], __amdgpu_buf
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      HOP_VMNOP
       ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %[keep], m0\n\t"
@@ -1000,6 +1027,7 @@ __device__ __forceinline__ void dma_stepAB(const unsigned (&vm)[6], const unsign
   "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\tbuffer_load_dwordx4 %[" #V "], %[" #R \
   "], %[" #SO "] offen lds\n\t"
   asm volatile(
+      HOP_VMNOP
       ".p2align 3\n\t"  // every piece's 8-byte buffer_load at 0 mod 8 (code placement)
       "s_waitcnt lgkmcnt(0)\n\t"
       "s_mov_b32 %[keep], m0\n\t"
@@ -1022,7 +1050,9 @@ __device__ __forceinline__ void dma_stepAB(const unsigned (&vm)[6], const unsign
 // carry data only, so nothing is written past an image) and the tile slot cut to the
 // zero area the lanes past s - 1 read: 19,400 B per wave at s = 13 fp64, so two 4-wave
 // workgroups fit a CU's 160 KiB
-template <int S, int MM, int ES = 8, bool PACK = false>  // ES: bytes per streamed element
+// SMALLT (the small-s row-group schedule): the tile slot cut to the zero area, as
+// PACK's (the conditioned kernel reads nothing else from it)
+template <int S, int MM, int ES = 8, bool PACK = false, bool SMALLT = false>  // ES: bytes per element
 struct Geo {
   static constexpr int SS = S * S;
   static constexpr int CHM = (SS * ES + 15) / 16;     // 16-B chunks per S x S block
@@ -1038,7 +1068,7 @@ struct Geo {
   // lanes of the last piece that carry data (PACK masks the rest)
   static constexpr int LASTM = kProbPerWave * CHM - 64 * (NJM - 1);
   static constexpr int LASTB = kProbPerWave * CHB - 64 * (NJB - 1);
-  static constexpr int TILE_W = PACK ? 8 * (SS + 8) : kProbPerWave * kLdsTile * 8;
+  static constexpr int TILE_W = (PACK || SMALLT) ? 8 * (SS + 8) : kProbPerWave * kLdsTile * 8;
   // per-wave layout: [Q][A][QT][B][tiles]
   static constexpr int OFF_Q = 0, OFF_A = IMGM_W, OFF_QT = 2 * IMGM_W, OFF_B = 3 * IMGM_W;
   static constexpr int OFF_T = 3 * IMGM_W + IMGB_W;
@@ -1111,7 +1141,11 @@ __device__ __forceinline__ void sym_load_average(double (&X)[S], const double* t
   for (int i = 0; i < S; ++i) X[i] = __builtin_fma(hs, y[i] - X[i], X[i]);
 }
 // sym_load_average in two halves (the closed-form kernel): the transposed reads issued
-// with no wait, other work, then the wait and the average.  The compiler's own LDS
+// with no wait, other work, then the wait and the average.  The two statements are
+// marked (hop_ldissue / hop_ldwait): the build's hazard check fails any code object in
+// which an instruction between them reads or writes a destination of the reads (a
+// copy, spill or reuse of a register whose data has not landed, which hipcc cannot
+// see: the loads are inside an asm statement; tools/check_dpp_hazards.py).  The compiler's own LDS
 // waits in between also wait for these reads (LDS operations complete in order), so
 // the round trip is shared with the next reads instead of paid alone.
 __device__ __forceinline__ void sym_issue13(const double* t, int c, double (&y)[13]) {
@@ -1123,7 +1157,7 @@ __device__ __forceinline__ void sym_issue13(const double* t, int c, double (&y)[
       "ds_read_b64 %6, %13 offset:48\n\tds_read_b64 %7, %13 offset:56\n\t"
       "ds_read_b64 %8, %13 offset:64\n\tds_read_b64 %9, %13 offset:72\n\t"
       "ds_read_b64 %10, %13 offset:80\n\tds_read_b64 %11, %13 offset:88\n\t"
-      "ds_read_b64 %12, %13 offset:96"
+      "ds_read_b64 %12, %13 offset:96 ; hop_ldissue"
       : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(y[4]), "=&v"(y[5]),
         "=&v"(y[6]), "=&v"(y[7]), "=&v"(y[8]), "=&v"(y[9]), "=&v"(y[10]), "=&v"(y[11]),
         "=&v"(y[12])
@@ -1131,7 +1165,7 @@ __device__ __forceinline__ void sym_issue13(const double* t, int c, double (&y)[
       : "memory");
 }
 __device__ __forceinline__ void sym_wait_average13(double (&X)[13], double (&y)[13], int c) {
-  asm volatile("s_waitcnt lgkmcnt(0)"
+  asm volatile("s_waitcnt lgkmcnt(0) ; hop_ldwait"
                : "+v"(y[0]), "+v"(y[1]), "+v"(y[2]), "+v"(y[3]), "+v"(y[4]), "+v"(y[5]),
                  "+v"(y[6]), "+v"(y[7]), "+v"(y[8]), "+v"(y[9]), "+v"(y[10]), "+v"(y[11]),
                  "+v"(y[12])
@@ -2682,7 +2716,7 @@ template <class C, int S, int MM, class T = double>
 __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(LftArgs<T> a) {
   constexpr int ES = (int)sizeof(T);
   constexpr bool F32 = ES == 4;
-  using G = Geo<S, MM, ES, has_pack<C>()>;
+  using G = Geo<S, MM, ES, has_pack<C>(), has_smalls<C>()>;
   static_assert(!has_pack<C>() || (!F32 && !has_traj<C>() && G::NJM == 6 && G::NJB == 2 &&
                                    2 * kWavesPerBlock * G::WAVE_BYTES <= 160 * 1024),
                 "packed images: s = 13 fp64 blocks, two workgroups per CU");
@@ -2731,7 +2765,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   constexpr double DOFF = has_sym2<C>() ? 1e-9 - 0.5 : 1e-9 - 1.0;  // image diagonal offset
   constexpr double KOFF = has_sym2<C>() ? 2.0 : 1.0;  // update / query diagonal offset
   // the congruence query (has_wq): the ldspipe schedules on augmented images only
-  constexpr bool WQ = has_wq<C>() && has_ldspipe<C>() && !TRAJ && !MF;
+  constexpr bool WQ = has_wq<C>() && (has_ldspipe<C>() || has_smalls<C>()) && !TRAJ && !MF;
   const double kmask = c < S - 1 ? -KOFF : 0.0;     // P11^-1 - KOFF I on lanes < S-1
   const double e_last = c == S - 1 ? 1.0 : 0.0;
   const T* imQ = reinterpret_cast<const T*>(wbase + G::OFF_Q + g * G::IMGM);
@@ -3015,7 +3049,8 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     {
       double d1 = 1.0, d2 = 1.0;
       SweepQ<S>::run(NE, d1);
-      SweepQ<S>::run(NX, d2);
+      if constexpr (WQ) SweepQP<S>::run(NX, d2);  // pivots 0 .. S-2 (the congruence query)
+      else SweepQ<S>::run(NX, d2);
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
       flag(!pivots_ok(NE, d1) || !pivots_ok(NX, d2), 1, k + 1);
     }
@@ -3650,6 +3685,58 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
 
 }  // namespace v2
 
+// Small-s row groups (SchedCondSmall): fp64 augmented blocks at s <= 5, batch-major,
+// when the batch leaves lft_small.hip's one-problem-per-lane kernel most SIMDs idle
+// (B / 64 waves).  Four problems per wave (one per DPP row),
+// so B = 4,096 runs 1,024 waves.  Its hand-overs go to lft_small.hip's LFT
+// instantiation (the rerun launch alone: cond = 1 | kCondRerunOnly), whose chol_inv
+// ladders and status bits are the reference's.  Larger batches (and tile64 blocks, the
+// trajectory form, per-step R, debug outputs) stay on lft_small.hip.
+// The crossover batch (tools/bench_small_rg.py measures both kernels by batch size;
+// the environment variable HOP_SMALL_RG_MAX, read once, moves it for such A/B runs).
+#ifndef HOP_SMALL_RG_MAX
+#define HOP_SMALL_RG_MAX 16384
+#endif
+static long long small_rg_max() {
+  static const long long v = [] {
+    const char* e = getenv("HOP_SMALL_RG_MAX");
+    return e ? atoll(e) : (long long)HOP_SMALL_RG_MAX;
+  }();
+  return v;
+}
+namespace v2 {
+template <int S, int MM>
+hipError_t launch_cond_small(const LftArgs<double>& a, hipStream_t stream) {
+  using G = Geo<S, MM, 8, false, true>;
+  static_assert(G::WAVE_BYTES * kWavesPerBlock <= 64 * 1024, "several workgroups per CU");
+  const long long blocks = (a.batch + kProbPerBlock - 1) / kProbPerBlock;
+  const bool force = opt(HOP_OPT_FORCE_HANDOVER);
+  LftArgs<double> c = a;
+  c.cond = (force ? 2 : 0) | ((kDevBuild && opt(HOP_OPT_NO_RERUN)) ? 4 : 0);
+  hipLaunchKernelGGL((lft_cond_kernel<SchedCondSmall, S, MM>), dim3((unsigned)blocks), dim3(256),
+                     (size_t)(G::WAVE_BYTES * kWavesPerBlock), stream, c);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess || opt(HOP_OPT_NO_RERUN)) return e;  // hand-over words left in status
+  LftArgs<double> r = a;
+  r.cond = 1 | kCondRerunOnly;
+  return dispatch_lft_small<double>(r, stream);
+}
+}  // namespace v2
+hipError_t dispatch_cond_small(const LftArgs<double>& a, hipStream_t stream) {
+  if (a.traj || a.tile64 || a.batch > small_rg_max() || opt(HOP_OPT_REFERENCE_ASSOC))
+    return hipErrorNotSupported;
+#ifdef HOP_DEV
+  if (g_opt_variant == 80) return hipErrorNotSupported;  // A/B: the lane-per-problem kernel
+#endif
+  if (a.s == 2 && a.m == 1) return v2::launch_cond_small<2, 1>(a, stream);
+  if (a.s == 3 && a.m == 1) return v2::launch_cond_small<3, 1>(a, stream);
+  if (a.s == 4 && a.m == 1) return v2::launch_cond_small<4, 1>(a, stream);
+  if (a.s == 4 && a.m == 2) return v2::launch_cond_small<4, 2>(a, stream);
+  if (a.s == 5 && a.m == 1) return v2::launch_cond_small<5, 1>(a, stream);
+  if (a.s == 5 && a.m == 2) return v2::launch_cond_small<5, 2>(a, stream);
+  return hipErrorNotSupported;
+}
+
 // exact-size fast path: returns hipErrorNotSupported when the shape has none.
 // Product builds: the conditioned-prefix kernel + the rerun launch of the
 // reference association for the problems it flagged (HOP_OPT_REFERENCE_ASSOC:
@@ -3744,6 +3831,7 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
       return launch(v2::lft_rerun_pipe_kernel<v2::SchedLdlTraj, 13, 4, v2::kPipeBS>, bytes_pt, r);
     }
   }
+  if (a.s <= 5) return dispatch_cond_small(a, stream);  // (lft_small.hip when not taken)
   if (a.s != 13 || a.m != 4) return hipErrorNotSupported;
   constexpr size_t bytes = v2::Geo<13, 4>::WAVE_BYTES * kWavesPerBlock;
   // + the symmetrisation scratch of SchedCondLSymL past the four waves' areas

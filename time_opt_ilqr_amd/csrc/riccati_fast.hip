@@ -81,6 +81,7 @@ __device__ __forceinline__ void dma9(const unsigned (&va)[5], const unsigned (&v
 #define HOP_M0(OFF) "s_add_u32 m0, %[w], " #OFF "\n\ts_nop 0\n\t"
 #define HOP_PO(R, V, SO, IO) "buffer_load_dwordx4 %[" #V "], %[" #R "], %[" #SO "] offen offset:" #IO " lds\n\t"
   asm volatile(
+      HOP_VMNOP
       "s_mov_b32 %[keep], m0\n\t"
       HOP_M0(%[m0]) HOP_PO(ra, a0, sa, 0) HOP_PO(ra, a1, sa, 1024) HOP_PO(ra, a2, sa, 2048)
       HOP_PO(ra, a3, sa, 3072)
@@ -556,6 +557,18 @@ __device__ __forceinline__ double diag_sum4_off12(const double (&x)[4]) {
   return acc;
 }
 
+// acc[r] += bcast_{12 + r}(d) * y[r], r < 4: rows of the packed [Qux | Quu] block scaled
+// by a per-row factor that lives on lanes 12..15 (the equilibration below)
+__device__ __forceinline__ void row_scale12(double (&acc)[4], double d, const double (&y)[4]) {
+  asm(HOP_NOP2
+      "v_fmac_f64_dpp %0, %4, %5 row_newbcast:12" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %1, %4, %6 row_newbcast:13" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %2, %4, %7 row_newbcast:14" HOP_DPP_TAIL
+      "v_fmac_f64_dpp %3, %4, %8 row_newbcast:15" HOP_DPP_TAIL
+      : "+&v"(acc[0]), "+&v"(acc[1]), "+&v"(acc[2]), "+&v"(acc[3])
+      : "v"(d), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]));
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   const unsigned nrec = bytes > 0xFFFFFFF0ll ? 0xFFFFFFF0u : (unsigned)(bytes > 0 ? bytes : 0);
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)nrec,
@@ -695,16 +708,13 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   const double xg_c = c < S ? xgp[cq] : 0.0;
   // PK: u and u_ref ride on lanes 12..15 as well (du, R du, Qu, k of the packed rows)
   const double ur_c = c < MM ? urp[cr] : ((PK && c >= S) ? urp[c - S] : 0.0);
-  double rpk[PK ? MM : 1], rrow12[PK ? MM : 1], dgc[PK ? MM : 1];
+  double rpk[PK ? MM : 1], rrow12[PK ? MM : 1];
   if constexpr (PK) {
-    const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
     const int cs = c >= S ? c - S : 0;
 #pragma unroll
     for (int r = 0; r < MM; ++r) {
       rpk[r] = c >= S ? Rp[r * MM + cs] : 0.0;     // lanes 12..15: row r of R
       rrow12[r] = c >= S ? Rp[cs * MM + r] : 0.0;  // lanes 12..15: column r of R
-      // the offset-form diagonal of Quu_reg + eps I (chol_solve's first try)
-      dgc[r] = (c == S + r) ? lam1 + (1e-9 - 1.0) : 0.0;
     }
   }
   const bool wrap_c = (c < S) && ((a.wrap_mask >> c) & 1u);
@@ -870,19 +880,51 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
       lds_sym_packed4(P, PT, twa, tw2, tr2);  // lanes 12..15 of PT: Quu^T; lanes < 12: Qux
       stamp(6);
       bool solved;
-      double rj[MM];
+      // rj: the sweep's rows, scaled (see below); rk: (Quu_reg + eps I)^-1 Qux = -K on
+      // lanes 0..11; dq: the row scale D_c on lanes 12..15 (1 elsewhere)
+      double rj[MM], rk[MM], dq;
       {
-        // lanes < 12 stay Qux exactly (0.5 (Qux + Qux)); lanes 12..15: _sym(Quu) + the
-        // offset-form lam + eps diagonal
+        // Equilibrated solve (round 6).  The offset-form sweep keeps -(M)^-1 + I: an
+        // entry of M^-1 ~ 1/d next to the 1 loses u d of its relative accuracy, and so
+        // does row p of the Qux lanes at a pivot d.  On a real quadrotor linearisation
+        // near the pitch singularity Vxx reaches 3e10 and Quu's diagonal 2e11, which
+        // left mode 1's Vxx 5e-6 off the reference where NumPy's Cholesky solve stays
+        // at 2e-9 of the 40-digit value (tests/test_gpu_gains.py).  So the sweep runs on
+        // M' = D M D, D = diag(M)^-1/2 (unit diagonal: every pivot of the SPD case is
+        // <= 1, and M'^-1 has entries >= 1 on its diagonal), with the Qux lanes scaled
+        // by the same D_r: the sweep leaves M'^-1 D Qux there, and M^-1 Qux = D (that),
+        // M^-1 = D M'^-1 D.  The pivots keep their signs (the PD test is unchanged);
+        // a non-positive or non-finite diagonal gives D = NaN, a failed first attempt
+        // and the ladder, as before.  M = _sym(Quu) + (lam + 1e-9) I.
+        const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+        double qs[MM];
 #pragma unroll
-        for (int r = 0; r < MM; ++r) rj[r] = __builtin_fma(0.5, P[r] + PT[r], dgc[r]);
+        for (int r = 0; r < MM; ++r) qs[r] = 0.5 * (P[r] + PT[r]);  // lanes < 12: Qux
+        double mdg = 0.0;
+        static_for<MM>([&](auto R) { mdg = (c == S + (int)R) ? qs[R] : mdg; });
+        const double dd = mdg + (lam1 + 1e-9);
+        dq = c >= S ? 1.0 / __builtin_sqrt(dd) : 1.0;
+        const double zd = 0.0 * dd;  // 0, or NaN for an infinite diagonal entry
+#pragma unroll
+        for (int r = 0; r < MM; ++r) {
+          qs[r] *= dq;  // column scale (lanes 12..15)
+          rj[r] = 0.0;
+        }
+        row_scale12(rj, dq, qs);  // row scale
+#pragma unroll
+        for (int r = 0; r < MM; ++r) rj[r] = (c == S + r) ? zd : rj[r];  // M' - I: unit diagonal
         double dj = 1.0;
         SweepQColChainOff<MM, S, S>::run(rj, dj, Qxx, ab, VA);
         const bool okj = (dj > 0.0) && (bcast<S>(rj[0]) == bcast<S>(rj[0]));
-        const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+#pragma unroll
+        for (int r = 0; r < MM; ++r) rk[r] = 0.0;
+        row_scale12(rk, dq, rj);  // lanes < 12: D_r (M'^-1 D Qux)_r = (M^-1 Qux)_r
         bool ok0 = true;
         if constexpr (MODE == 0) {
-          const double tr = 4.0 - diag_sum4_off12(rj);  // trace((M + eps I)^-1)
+          // trace((M + eps I)^-1) = sum_c D_c^2 (1 - rj[c]_cc)
+          double dgi = 0.0;
+          static_for<MM>([&](auto R) { dgi = (c == S + (int)R) ? 1.0 - rj[R] : dgi; });
+          const double tr = lane_sum_off<MM, S>(dgi * (dq * dq));
           const bool sure = okj && (tr < 1e6);
           if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
             double rc[MM];
@@ -921,7 +963,8 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
               if (!done) lam *= 10.0;
             }
           }
-          // back to the packed form: lanes 0..11 Ql Qux, lanes 12..15 I - Ql
+          // back to the packed form (unscaled, D = 1): lanes 0..11 Ql Qux, lanes
+          // 12..15 I - Ql
 #pragma unroll
           for (int r = 0; r < MM; ++r) {
             double y = 0.0;
@@ -929,33 +972,38 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
             const double il = ror_row<S>(Ql[r]);
             const double rl = c < S ? y : (((c == S + r) ? 1.0 : 0.0) - il);
             rj[r] = ladder ? rl : rj[r];
+            rk[r] = ladder ? rl : rk[r];
           }
+          dq = ladder ? 1.0 : dq;
           solved = ladder ? good : solved;
         }
       }
       fail_row = act && (bad || !solved);
       stamp(7);
-      // gains: K = -rj (lanes < 12); k = -(M + eps I)^-1 Qu on lanes 12..15 from the
-      // offset form: -Qu + sum_j Qu_j rj[j]
-      double kv = -qu;
-      LaneDotOff<MM, S>::fma(kv, qu, rj);
+      // gains: K = -rk (lanes < 12); k = -(M + eps I)^-1 Qu = -D M'^-1 (D Qu) on lanes
+      // 12..15, with M'^-1 y = y - sum_j y_j rj[j] (M' has unit diagonal, so |M'^-1 y|
+      // >= |y| / 4: no cancellation)
+      const double yq = dq * qu;
+      double kv = -yq;
+      LaneDotOff<MM, S>::fma(kv, yq, rj);
+      kv *= dq;
       stamp(8);
       if constexpr (MODE == 0) {
-        LaneDotOff<MM, S>::fma_neg(vxn, qu, rj);  // + K^T Qu
+        LaneDotOff<MM, S>::fma_neg(vxn, qu, rk);  // + K^T Qu
         LaneDotOff<MM, S>::fma(vxn, kv, P);       // + Qux^T k
         double qk = 0.0;
         LaneDotOff<MM, S>::fma(qk, kv, PT);       // (Quu k) on lanes 12..15
-        LaneDotOff<MM, S>::fma_neg(vxn, qk, rj);  // + K^T Quu k
+        LaneDotOff<MM, S>::fma_neg(vxn, qk, rk);  // + K^T Quu k
         double QK[MM];
         copy(QK, P);
-        static_for<MM>([&](auto R) { LaneDotOff<MM, S>::fma_neg(QK[R], P[R], rj); });  // Qux + Quu K
+        static_for<MM>([&](auto R) { LaneDotOff<MM, S>::fma_neg(QK[R], P[R], rk); });  // Qux + Quu K
         static_for<S>([&](auto R) {
-          ColChain<MM>::template fma_negq<R>(Vn[R], rj, QK);  // + K^T (Qux + Quu K)
-          ColChain<MM>::template fma_negq<R>(Vn[R], P, rj);   // + Qux^T K
+          ColChain<MM>::template fma_negq<R>(Vn[R], rk, QK);  // + K^T (Qux + Quu K)
+          ColChain<MM>::template fma_negq<R>(Vn[R], P, rk);   // + Qux^T K
         });
       } else {
         static_for<S>([&](auto R) {  // Qxx - Qux^T Quu^-1 Qux
-          ColChain<MM>::template fma_negq<R>(Vn[R], P, rj);
+          ColChain<MM>::template fma_negq<R>(Vn[R], P, rk);
         });
         LaneDotOff<MM, S>::fma(vxn, kv, P);  // Qx - Qux^T Quu^-1 Qu
         v0n = l0 + v0 + 0.5 * lane_sum_off<MM, S>(qu * kv);
@@ -963,7 +1011,7 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
 #pragma unroll
       for (int r = 0; r < MM; ++r) {
         Uq[r] = P[r];
-        Kq[r] = rj[r];
+        Kq[r] = rk[r];
       }
       kvq = kv;
     } else {

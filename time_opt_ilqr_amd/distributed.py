@@ -27,6 +27,37 @@ def shard_bounds(total: int, rank: int, world: int):
     return lo, hi
 
 
+def _host_collective(group, dev) -> bool:
+    """gloo all-gathers host tensors only: a device tensor goes through the host for
+    the collective (the real kernels under gloo, several ranks on one GPU: the bench's
+    --dist-backend gloo rehearsal and tests/test_gpu_distributed.py).  RCCL keeps them
+    on the device."""
+    import torch.distributed as dist
+    return dev.type != "cpu" and dist.get_backend(group) == "gloo"
+
+
+def _all_gather_packed(out, packed, group):
+    import torch.distributed as dist
+    if _host_collective(group, packed.device):
+        host = out.cpu()
+        dist.all_gather_into_tensor(host, packed.cpu(), group=group)
+        out.copy_(host)
+    else:
+        dist.all_gather_into_tensor(out, packed, group=group)
+
+
+def all_reduce_max(t, group=None):
+    """In-place MAX all-reduce (through the host under gloo, as above)."""
+    import torch.distributed as dist
+    if _host_collective(group, t.device):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t
+
+
 def gather_selection(t_star, j_star, total: int, group=None):
     """All-gather every rank's (T*, J*) shard into full [total] tensors.
 
@@ -45,7 +76,7 @@ def gather_selection(t_star, j_star, total: int, group=None):
     packed[: t_star.numel(), 0] = t_star.to(torch.float64)
     packed[: j_star.numel(), 1] = j_star.to(torch.float64)
     out = torch.empty((world * cap, 2), dtype=torch.float64, device=dev)
-    dist.all_gather_into_tensor(out, packed, group=group)
+    _all_gather_packed(out, packed, group)
     parts = [out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)]
     full = torch.cat(parts, 0)
     return full[:, 0].to(torch.int32), full[:, 1].to(j_star.dtype)
@@ -64,7 +95,7 @@ def gather_curves(J, total: int, group=None):
     # every rank must pack the same width: an empty shard may hold a [0] tensor, so
     # the curve length is agreed on by one max all-reduce first
     n_loc = torch.tensor([J.shape[1] if J.dim() == 2 else 0], dtype=torch.int64, device=J.device)
-    dist.all_reduce(n_loc, op=dist.ReduceOp.MAX, group=group)
+    all_reduce_max(n_loc, group)
     N = int(n_loc.item())
     if J.dim() != 2:
         J = J.reshape(0, N)
@@ -73,7 +104,7 @@ def gather_curves(J, total: int, group=None):
     packed = torch.full((cap, N), float("nan"), dtype=J.dtype, device=J.device)
     packed[: J.shape[0]] = J
     out = torch.empty((world * cap, N), dtype=J.dtype, device=J.device)
-    dist.all_gather_into_tensor(out, packed, group=group)
+    _all_gather_packed(out, packed, group)
     return torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
 
 
@@ -93,7 +124,7 @@ def gather_columns(cols, total: int, group=None):
     for j, c in enumerate(cols):
         packed[: c.numel(), j] = c.to(torch.float64)
     out = torch.empty((world * cap, len(cols)), dtype=torch.float64, device=dev)
-    dist.all_gather_into_tensor(out, packed, group=group)
+    _all_gather_packed(out, packed, group)
     full = torch.cat([out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(sizes)], 0)
     return [full[:, j].to(c.dtype) for j, c in enumerate(cols)]
 

@@ -90,6 +90,10 @@ def main():
     P = tt(lQf)
     work["augment_quad"] = lambda: engine.augment(lin.A, lin.B, lin.a_res, Xq, Uq, tt(lxg),
                                                   tt(lur), tt(lQ), P, lw).Q
+    # fp64 s = 5 blocks at B = 4,096 (round 6: the row-group kernel against the lane
+    # kernel of the libraries before it); synthetic SPD blocks, N = 200
+    s5 = synth.device_batch(4096, 5, 1, 200, seed=6, device=dev)
+    work["small_s5_f64_4096"] = lambda: engine.propagate(*s5, t_min=40, t_max=200).J
     if args.only:
         work = {w: f for w, f in work.items() if w in args.only.split(",")}
     L = len(libs)

@@ -1,17 +1,28 @@
-"""Drop the DPP hazard pads that the compiled code makes unnecessary.
+"""Drop the hazard pads that the compiled code makes unnecessary.
 
 The generated DPP blocks (dpp_blocks.inc) open with two wait states of padding,
 "s_nop 0 ; hnop" twice, because the block cannot know how recently the compiler
 wrote its first broadcast source; the generated sweeps pad their own internal
-read-after-write distances the same way.  In the compiled device assembly the
-distance is known.  This pass walks every function of a device `.s` file and
-removes each consecutive PAIR of marked pads whose removal leaves no DPP source
-read inside its hazard window (the rules of tools/check_dpp_hazards.py: two wait
-states after a VALU write of the source, five after a VALU write of EXEC, a label
-inside the window counts as a violation).  Pairs only: the blocks keep their
-8-byte instructions at 0 mod 8 (an unpaired removal would shift them; the
-alignment pads, unmarked, are never touched).  The build assembles the result and
-runs the full hazard check on it.
+read-after-write distances the same way.  The LDS-DMA statements open with
+"s_nop 2 ; vmnop" (HOP_VMNOP, hop_device.hpp) for the VALU-SGPR-write -> VMEM window.
+In the compiled device assembly the distances are known.  This pass walks every
+function of a device `.s` file and removes
+
+  * each consecutive PAIR of "hnop" pads (no directive or label between them in the
+    raw lines: a `.p2align` between two pads would make the pair's removal shift the
+    instructions after the directive off their 8-byte alignment), and
+  * each single "vmnop" pad (it sits before its statement's `.p2align`, so the
+    alignment of the statement does not depend on it),
+
+whose removal leaves every modelled hazard window intact: every rule of
+tools/check_dpp_hazards.py (DPP source and EXEC, transcendental forwarding,
+VALU SGPR -> VMEM, lane select, VCC -> v_div_fmas, readlane, permlane, M0 -> LDS-DMA),
+checked on the instructions that follow the pad, and on those after the target of
+any branch within five wait states of it (a pad whose removal could shorten a window
+on a path the re-check cannot follow is kept).  Pairs only for
+"hnop": the blocks keep their 8-byte instructions at 0 mod 8 (an unpaired removal
+would shift them; the alignment pads, unmarked, are never touched).  The build
+assembles the result and runs the full hazard check on it.
 
     python tools/nop_elide.py in.s out.s
 """
@@ -19,7 +30,9 @@ import re
 import sys
 
 HNOP = re.compile(r"^\s*s_nop\s+0\s*;\s*hnop\s*$")
-LOOKAHEAD = 12  # instructions after a removed pair whose DPP reads are re-checked
+VMNOP = re.compile(r"^\s*s_nop\s+\d+\s*;\s*vmnop\s*$")
+LOOKAHEAD = 12  # instructions after a removed pad whose hazard windows are re-checked
+BRANCH_WINDOW = 5  # wait states after a pad within which a branch target is re-checked too
 
 
 def _classify(lines):
@@ -36,80 +49,88 @@ def _classify(lines):
         elif s.startswith(".LBB") and s.endswith(":"):
             out.append(("label", s[:-1]))
         elif s.startswith("."):
-            out.append(None)
+            out.append(("dir", s))
         else:
             out.append(("ins", s))
     return out
 
 
 def elide(lines, chk):
-    """Returns (new_lines, pairs_removed, pairs_kept)."""
+    """Returns (new_lines, pads_removed, pads_kept); a removed / kept "hnop" pair counts
+    once, as does a single "vmnop" pad."""
     kinds = _classify(lines)
     n = len(lines)
-    alive = [True] * n
-    # instruction indices per function, in order
-    seq = [i for i in range(n) if kinds[i] is not None]
+    alive = [k is not None and k[0] != "dir" for k in kinds]
+    entries = [k if k is not None else ("dir", "") for k in kinds]
+    cfg = chk.Cfg(entries)
+    is_alive = alive.__getitem__
 
-    def hazard_at(pos_list, k):
-        """Is the DPP instruction at pos_list[k] inside a hazard window, looking back
-        over the live entries of pos_list?"""
-        kind, text = kinds[pos_list[k]]
-        if kind != "ins":
-            return False
-        src = chk.dpp_source(text)
-        if src is None:
-            return False
-        ws = 0
-        j = k - 1
-        seen = 0
-        while j >= 0 and seen < 16:
-            i = pos_list[j]
-            j -= 1
-            if not alive[i]:
-                continue
-            kk, t = kinds[i]
-            seen += 1
-            if kk == "func":
-                return False
-            if kk == "label":
-                return ws < 2
-            written, wexec = chk.vgpr_writes(t)
-            if written & src and ws < 2:
-                return True
-            if wexec and ws < 5:
-                return True
-            ws += chk.wait_states(t)
-            if ws >= 5:
-                return False
-        return False
+    def next_live(i):
+        j = i + 1
+        while j < n and not alive[j]:
+            j += 1
+        return j
+
+    def window_ok(j, depth):
+        """No hazard window violated in the LOOKAHEAD live instructions from entry j on,
+        nor (depth permitting) after the target of a branch met within BRANCH_WINDOW
+        wait states."""
+        seen, ws = 0, 0
+        while j < n and seen < LOOKAHEAD:
+            kind, t = entries[j]
+            if kind == "func":
+                break
+            if kind == "ins":
+                seen += 1
+                if cfg.violations(j, is_alive):
+                    return False
+                m = chk.BRANCH.match(t)
+                if m and ws < BRANCH_WINDOW:
+                    tgt = cfg.label_at.get(m.group(2))
+                    if tgt is None or depth == 0 or not window_ok(tgt + 1, depth - 1):
+                        return False
+                    if t.startswith("s_branch"):
+                        break  # no fall-through
+                ws += chk.wait_states(t)
+            j = next_live(j)
+        return True
+
+    def safe_without(pads):
+        """With `pads` removed, no hazard window is violated in the instructions that
+        follow them (window_ok)."""
+        for p in pads:
+            alive[p] = False
+        ok = window_ok(next_live(max(pads)), 2)
+        if not ok:
+            for p in pads:
+                alive[p] = True
+        return ok
 
     removed = kept = 0
-    k = 0
-    while k + 1 < len(seq):
-        a, b = seq[k], seq[k + 1]
-        if HNOP.match(lines[a]) and HNOP.match(lines[b]) and alive[a] and alive[b]:
-            alive[a] = alive[b] = False
-            # re-check the DPP reads that follow (their windows may have shrunk)
-            bad = False
-            m, seen = k + 2, 0
-            while m < len(seq) and seen < LOOKAHEAD:
-                if alive[seq[m]]:
-                    seen += 1
-                    if kinds[seq[m]][0] == "func":
-                        break
-                    if hazard_at(seq, m):
-                        bad = True
-                        break
-                m += 1
-            if bad:
-                alive[a] = alive[b] = True
-                kept += 1
-            else:
+    i = 0
+    while i < n:
+        if alive[i] and VMNOP.match(lines[i]):
+            if safe_without([i]):
                 removed += 1
-            k += 2
+            else:
+                kept += 1
+            i += 1
             continue
-        k += 1
-    return [l for i, l in enumerate(lines) if alive[i]], removed, kept
+        if alive[i] and HNOP.match(lines[i]):
+            # its partner: the next line that is not blank / a pure comment
+            j = i + 1
+            while j < n and kinds[j] is None:
+                j += 1
+            if j < n and alive[j] and HNOP.match(lines[j]):
+                if safe_without([i, j]):
+                    removed += 1
+                else:
+                    kept += 1
+                i = j + 1
+                continue
+        i += 1
+    return [l for i, l in enumerate(lines) if alive[i] or kinds[i] is None or kinds[i][0] == "dir"], \
+        removed, kept
 
 
 def main(argv):
@@ -120,7 +141,7 @@ def main(argv):
     lines = open(src).read().split("\n")
     out, removed, kept = elide(lines, chk)
     open(dst, "w").write("\n".join(out))
-    print(f"{os.path.basename(src)}: {removed} hazard-pad pairs dropped, {kept} kept")
+    print(f"{os.path.basename(src)}: {removed} hazard pads dropped, {kept} kept")
     return 0
 
 
