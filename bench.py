@@ -372,7 +372,7 @@ def _quad_side(Bn, N, t_min, dev):
     X = engine.rollout(F.system_id, torch.as_tensor(x0, device=dev) +
                        0.1 * torch.randn((Bn, F.n), **kw), U, F.dt)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
-    shared = (t(xg), t(u_ref), t(Q), torch.linalg.inv(t(R)), t(as_terminal_weight(alpha, F.n)),
+    shared = (t(xg), t(u_ref), t(Q), torch.linalg.inv(t(R)).contiguous(), t(as_terminal_weight(alpha, F.n)),
               t([w]))
 
     def lin():
@@ -421,7 +421,7 @@ def _s5_aug_side(dev, Bn=4096, N=200, t_min=40):
                        0.3 * torch.randn((Bn, F.n), **kw), U, F.dt)
     t = lambda a: torch.as_tensor(np.asarray(a, dtype=np.float64), device=dev)  # noqa: E731
     P = t(as_terminal_weight(alpha, F.n))
-    Ri = torch.linalg.inv(t(R))
+    Ri = torch.linalg.inv(t(R)).contiguous()
     lin = engine.linearize(F.system_id, X, U, F.dt, central=True)
     shared = (t(xg), t(u_ref), t(Q))
 
@@ -527,7 +527,7 @@ def _select_gains_workload(args, world, lo, hi, dev):
     M = torch.randn((n, n), **kw)
     Q = M @ M.T / n + 0.5 * eye
     R = torch.diag(0.5 + 1.5 * torch.rand((m,), **kw))
-    Rinv = torch.linalg.inv(R)
+    Rinv = torch.linalg.inv(R).contiguous()  # linalg.inv is column-major: a copy per call otherwise
     P = torch.diag(1.0 + 9.0 * torch.rand((n,), **kw))
     w = 0.5
     t_min = min(args.t_min, N)

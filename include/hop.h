@@ -76,6 +76,10 @@ const char* hop_last_error(void);
  *                           triage: a hand-over explained by non-finite inputs
  *                           gets the reference's outcome (ST_NONFINITE, NaN from
  *                           the first affected horizon) and is not counted
+ *   HOP_OPT_SMALL_LANE      fp64 s <= 5 block sweeps of at most 16,384 problems on
+ *                           the lane-per-problem kernel (lft_small.hip) instead of
+ *                           the row-group kernel (lft_sweep_v2.hip SchedCondSmall):
+ *                           the A/B and cross-check of the two
  * `variant` selects an A/B schedule; only developer builds (HOP_DEV_BUILD=1 at
  * build time, hop_build_flags() & 1) compile them -- product builds return
  * HOP_E_ARG for variant != 0 or HOP_OPT_STAMPS.
@@ -86,6 +90,7 @@ const char* hop_last_error(void);
 #define HOP_OPT_TRAJ_UNFUSED 8u
 #define HOP_OPT_STAMPS 16u
 #define HOP_OPT_NO_RERUN 32u
+#define HOP_OPT_SMALL_LANE 64u
 #define HOP_ST_HANDOVER 16 /* status bit, set only under HOP_OPT_NO_RERUN */
 /*
  * The hand-over word: the status a conditioned-prefix kernel leaves for a problem

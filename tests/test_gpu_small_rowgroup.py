@@ -55,6 +55,14 @@ def test_rowgroup_matches_lane_kernel(dev, s, m, N):
     assert rel <= 1e-12, rel
     assert not np.array_equal(Jr, Jl)  # two kernels, not one
     assert np.array_equal(rg.t_star.cpu().numpy(), lane.t_star[h].cpu().numpy())
+    # HOP_OPT_SMALL_LANE puts a batch under the crossover on the lane kernel: bitwise
+    # the same problems in the batch above it (one problem per lane, batch-independent)
+    from time_opt_ilqr_amd import _lib
+    q = slice(0, 256)
+    with _lib.options(small_lane=True):
+        ln = engine.propagate(A[q].contiguous(), Bm[q].contiguous(), Q[q].contiguous(),
+                              Ri[q].contiguous(), z0, QT[q].contiguous(), t_min=t_min, t_max=N)
+    assert torch.equal(ln.J, lane.J[q]) and torch.equal(ln.t_star, lane.t_star[q])
 
 
 @pytest.mark.parametrize("s,m", [(5, 1), (3, 1), (4, 2)])

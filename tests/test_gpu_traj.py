@@ -274,20 +274,28 @@ def _traj_nonfinite_and_tiny_horizons(dev):
                                         (2, 1, "f64", 1e-9), (1, 1, "f64", 1e-9)])
 def test_traj_small_fused_vs_unfused_and_oracle(dev, unfused, n, m, dt, tol):
     """Small s: the in-register builders of lft_small_traj_kernel against
-    hop_augment + the small-s sweep and against the oracle (tails: 67 problems)."""
+    hop_augment + the small-s sweep and against the oracle (tails: 67 problems).
+    fp64 batches up to kSmallRowGroupMax run unfused by default (augment + the
+    row-group kernel); HOP_OPT_SMALL_LANE keeps them on the fused lane kernel."""
     import torch
-    from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib, engine
     dtype = torch.float64 if dt == "f64" else torch.float32
     N = 45
     ps, st = _batch(range(1200, 1267), n, m, N)
     args = (*_dev_args(st, dev, dtype), _t(st["R_inv"], dev, dtype), _t(st["P"], dev, dtype),
             _t(st["w"], dev, dtype))
     kw = dict(wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=N)
-    a = engine.propagate_traj(*args, **kw)
+    with _lib.options(small_lane=True):
+        a = engine.propagate_traj(*args, **kw)  # fused, one problem per lane
     with unfused():
         b = engine.propagate_traj(*args, **kw)
+    d = engine.propagate_traj(*args, **kw)
     Ja, Jb = a.J.double().cpu().numpy(), b.J.double().cpu().numpy()
     assert _rel(Ja, Jb) <= (1e-11 if dt == "f64" else 2e-3)  # fp32: the 2e-3 bar
+    if dt == "f64" and (n + 1, m) in ((2, 1), (3, 1), (4, 1), (4, 2), (5, 1), (5, 2)):
+        assert torch.equal(d.J, b.J)  # the default is the unfused row-group path
+    else:
+        assert torch.equal(d.J, a.J)
     for i in (0, 33, 66):
         _, o = _oracle(ps[i], 1.0)
         assert _rel(Ja[i], o["J"]) <= tol
@@ -409,6 +417,7 @@ def test_traj_tile64_equals_batch_major_and_oracle(dev, n, m, dt):
     on a sample at the fp64 / fp32 bars."""
     import torch
     from time_opt_ilqr_amd import engine
+    from time_opt_ilqr_amd import _lib
     dtype = torch.float64 if dt == "f64" else torch.float32
     N = 45
     ps, st = _batch(range(1300, 1367), n, m, N)
@@ -416,12 +425,17 @@ def test_traj_tile64_equals_batch_major_and_oracle(dev, n, m, dt):
     shared = (raw[5], raw[6], raw[7], _t(st["R_inv"], dev, dtype), _t(st["P"], dev, dtype),
               _t(st["w"], dev, dtype))
     kw = dict(wrap_idx=st["wrap_idx"], rho_reg=1.0, t_min=3, t_max=N)
-    bm = engine.propagate_traj(*raw[:5], *shared, **kw)
+    with _lib.options(small_lane=True):  # fp64: the fused lane kernel, like tile64's
+        bm = engine.propagate_traj(*raw[:5], *shared, **kw)
     t64 = [engine.to_tile64(x if x.dim() == 4 else x[..., None]) for x in raw[:5]]
     tl = engine.propagate_traj(*t64, *shared, **kw)
     if dt == "f64":
         assert torch.equal(tl.J, bm.J) and torch.equal(tl.t_star, bm.t_star)
         assert torch.equal(tl.status, bm.status) and (tl.status == 0).all()
+        # the batch-major default (hop_augment + the row-group kernel): within 1e-11
+        d = engine.propagate_traj(*raw[:5], *shared, **kw)
+        assert _rel(d.J.cpu().numpy(), tl.J.cpu().numpy()) <= 1e-11
+        assert torch.equal(d.t_star, tl.t_star)
     else:
         from test_gpu_configs import _same_sweep
         _same_sweep(tl, bm, False, tol=2e-3)

@@ -620,6 +620,11 @@ def test_traj_entry_validation_and_workspace_query(lib):
     ws = lib.hop_lft_sweep_traj_workspace_bytes
     assert ws(4096, 100, 12, 4, 8, 0) == 0          # Quadrotor shape, fp64: fused
     assert ws(65536, 200, 4, 1, 4, 0) == 0          # Cartpole shape, fp32: fused (small s)
+    assert ws(16385, 200, 4, 1, 8, 0) == 0          # fp64 above kSmallRowGroupMax: fused
+    assert ws(16384, 200, 4, 1, 8, 0) >= 8 * 16384 * 200 * (3 * 25 + 5)  # augment + row groups
+    from time_opt_ilqr_amd import _lib
+    with _lib.options(small_lane=True):
+        assert ws(4096, 200, 4, 1, 8, 0) == 0       # HOP_OPT_SMALL_LANE: the fused lane kernel
     assert ws(4096, 100, 12, 4, 8, 1) > 0           # extra_stage_cost: builder + sweep
     s, m, steps = 16, 6, 7 * 30
     need = ws(7, 30, 15, 6, 8, 0)

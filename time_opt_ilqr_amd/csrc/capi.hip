@@ -281,11 +281,16 @@ hop::TrajArgs<T> traj_args(const T* A, const T* Bm, const T* a_res, const T* X, 
 }
 
 // the sweep builds the blocks itself (no workspace) for these shapes: the
-// exact-size s = 13 kernel (fp64) and the small-s instantiations (lft_small.hip)
-bool traj_fused(int32_t n, int32_t m, int32_t elem_bytes, bool has_extra) {
+// exact-size s = 13 kernel (fp64) and the small-s instantiations (lft_small.hip).
+// fp64 small-s batches the row-group kernel takes go through hop_augment + that
+// kernel instead: one problem per lane fills B / 64 SIMDs, and the blocks' round
+// trip through HBM costs less than the idle chip below kSmallRowGroupMax (2.7x at
+// B = 4,096 on the cart-pole, profiles/r06_small_rg_crossover.jsonl)
+bool traj_fused(int32_t n, int32_t m, int32_t elem_bytes, bool has_extra, int64_t batch) {
   if (hop::opt(HOP_OPT_FORCE_GENERIC | HOP_OPT_TRAJ_UNFUSED) || has_extra) return false;
   if (elem_bytes == 8 && n == 12 && m == 4) return true;
   const int s = n + 1;
+  if (elem_bytes == 8 && hop::cond_small_takes(s, m, batch)) return false;
   return (s == 2 && m == 1) || (s == 3 && m == 1) || (s == 4 && (m == 1 || m == 2)) ||
          (s == 5 && (m == 1 || m == 2));
 }
@@ -323,7 +328,7 @@ int lft_traj_entry(const hop::TrajArgs<T>& t, const T* R_inv, int64_t r_bs, int6
   if (!R_inv) return fail(HOP_E_ARG, "null R_inv");
   const int32_t n = t.n, m = t.m, s = n + 1;
   const bool extra = t.qxx_extra || t.qx_extra || t.c_extra;
-  if (traj_fused(n, m, (int32_t)sizeof(T), extra)) {
+  if (traj_fused(n, m, (int32_t)sizeof(T), extra, batch)) {
     // the augmented blocks never touch HBM: the sweep builds them per step
     return lft_entry<T>(nullptr, nullptr, nullptr, R_inv, r_bs, 0, 1, nullptr, nullptr, 0,
                         batch, n_alloc, n_use, s, m, max_tries, t_min, t_max, J, status,
@@ -353,7 +358,8 @@ extern "C" {
 
 int hop_set_options(uint32_t flags, int32_t variant) {
   if (flags & ~(HOP_OPT_FORCE_GENERIC | HOP_OPT_FORCE_HANDOVER | HOP_OPT_REFERENCE_ASSOC |
-                HOP_OPT_TRAJ_UNFUSED | HOP_OPT_STAMPS | HOP_OPT_NO_RERUN))
+                HOP_OPT_TRAJ_UNFUSED | HOP_OPT_STAMPS | HOP_OPT_NO_RERUN |
+                HOP_OPT_SMALL_LANE))
     return fail(HOP_E_ARG, "unknown option flag");
   if (!hop::kDevBuild && (variant != 0 || (flags & HOP_OPT_STAMPS)))
     return fail(HOP_E_ARG, "A/B schedules and stamps exist only in developer builds "
@@ -549,7 +555,7 @@ int hop_augment_f32(const float* A, const float* Bm, const float* a_res, const f
 int64_t hop_lft_sweep_traj_workspace_bytes(int64_t batch, int32_t n_use, int32_t n, int32_t m,
                                            int32_t elem_bytes, int32_t has_extra) {
   if (batch <= 0 || n_use <= 0) return 0;
-  if (traj_fused(n, m, elem_bytes, has_extra != 0)) return 0;
+  if (traj_fused(n, m, elem_bytes, has_extra != 0, batch)) return 0;
   return traj_ws_bytes(batch, n_use, n, m, elem_bytes);
 }
 

@@ -249,6 +249,14 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream);
 // (its rerun launch alone): LftArgs.cond = 1 | kCondRerunOnly
 constexpr int kCondRerunOnly = 64;
 // fp64 s <= 5 augmented blocks on the conditioned kernel's row groups (lft_sweep_v2.hip)
+// for batches up to kSmallRowGroupMax (above it lft_small.hip's one problem per lane
+// fills the chip and wins: profiles/r06_small_rg_crossover.jsonl); HOP_OPT_SMALL_LANE
+// and HOP_OPT_REFERENCE_ASSOC keep every batch on lft_small.hip
+constexpr long long kSmallRowGroupMax = 16384;
+inline bool cond_small_takes(int s, int m, long long batch) {
+  if (batch > kSmallRowGroupMax || opt(HOP_OPT_REFERENCE_ASSOC | HOP_OPT_SMALL_LANE)) return false;
+  return (m == 1 && s >= 2 && s <= 5) || (m == 2 && (s == 4 || s == 5));
+}
 hipError_t dispatch_cond_small(const LftArgs<double>& a, hipStream_t stream);
 hipError_t dispatch_lft_v2_f32(const LftArgs<float>& a, hipStream_t stream);
 template <class T>

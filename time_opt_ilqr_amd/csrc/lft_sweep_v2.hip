@@ -3692,18 +3692,7 @@ __global__ __launch_bounds__(256, 1) void lft_cond_cf_kernel(LftArgs<double> a) 
 // instantiation (the rerun launch alone: cond = 1 | kCondRerunOnly), whose chol_inv
 // ladders and status bits are the reference's.  Larger batches (and tile64 blocks, the
 // trajectory form, per-step R, debug outputs) stay on lft_small.hip.
-// The crossover batch (tools/bench_small_rg.py measures both kernels by batch size;
-// the environment variable HOP_SMALL_RG_MAX, read once, moves it for such A/B runs).
-#ifndef HOP_SMALL_RG_MAX
-#define HOP_SMALL_RG_MAX 16384
-#endif
-static long long small_rg_max() {
-  static const long long v = [] {
-    const char* e = getenv("HOP_SMALL_RG_MAX");
-    return e ? atoll(e) : (long long)HOP_SMALL_RG_MAX;
-  }();
-  return v;
-}
+// The crossover batch (kSmallRowGroupMax, hop_kernels.hpp): tools/bench_small_rg.py.
 namespace v2 {
 template <int S, int MM>
 hipError_t launch_cond_small(const LftArgs<double>& a, hipStream_t stream) {
@@ -3723,8 +3712,7 @@ hipError_t launch_cond_small(const LftArgs<double>& a, hipStream_t stream) {
 }
 }  // namespace v2
 hipError_t dispatch_cond_small(const LftArgs<double>& a, hipStream_t stream) {
-  if (a.traj || a.tile64 || a.batch > small_rg_max() || opt(HOP_OPT_REFERENCE_ASSOC))
-    return hipErrorNotSupported;
+  if (a.traj || a.tile64 || !cond_small_takes(a.s, a.m, a.batch)) return hipErrorNotSupported;
 #ifdef HOP_DEV
   if (g_opt_variant == 80) return hipErrorNotSupported;  // A/B: the lane-per-problem kernel
 #endif

@@ -708,13 +708,20 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
   const double xg_c = c < S ? xgp[cq] : 0.0;
   // PK: u and u_ref ride on lanes 12..15 as well (du, R du, Qu, k of the packed rows)
   const double ur_c = c < MM ? urp[cr] : ((PK && c >= S) ? urp[c - S] : 0.0);
-  double rpk[PK ? MM : 1], rrow12[PK ? MM : 1];
+  double rpk[PK ? MM : 1], rrow12[PK ? MM : 1], dgc[PK ? MM : 1], ohr[PK ? MM : 1],
+      nd[PK ? MM : 1];
   if constexpr (PK) {
+    const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
     const int cs = c >= S ? c - S : 0;
 #pragma unroll
     for (int r = 0; r < MM; ++r) {
       rpk[r] = c >= S ? Rp[r * MM + cs] : 0.0;     // lanes 12..15: row r of R
       rrow12[r] = c >= S ? Rp[cs * MM + r] : 0.0;  // lanes 12..15: column r of R
+      // lane 12 + r of register r (the packed block's diagonal): lam + eps (chol_solve's
+      // first try), a one-hot and the offset form's -1
+      dgc[r] = (c == S + r) ? lam1 + 1e-9 : 0.0;
+      ohr[r] = (c == S + r) ? 1.0 : 0.0;
+      nd[r] = -ohr[r];
     }
   }
   const bool wrap_c = (c < S) && ((a.wrap_mask >> c) & 1u);
@@ -895,24 +902,28 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
         // by the same D_r: the sweep leaves M'^-1 D Qux there, and M^-1 Qux = D (that),
         // M^-1 = D M'^-1 D.  The pivots keep their signs (the PD test is unchanged);
         // a non-positive or non-finite diagonal gives D = NaN, a failed first attempt
-        // and the ladder, as before.  M = _sym(Quu) + (lam + 1e-9) I.
+        // and the ladder, as before.  M = _sym(Quu) + (lam + 1e-9) I.  Cost: +8 % on
+        // mode 0 and the J curve with 1/sqrt and exact-zero diagonals, less with the
+        // rsq form below (profiles/r06_ab_riccati_equilibration.jsonl).
         const double lam1 = MODE == 0 ? lam0 : (lam0 > 1e-12 ? lam0 : 1e-12);
+        // M = _sym(Quu) + (lam + eps) I on lanes 12..15 (Qux on lanes < 12, exactly)
         double qs[MM];
 #pragma unroll
-        for (int r = 0; r < MM; ++r) qs[r] = 0.5 * (P[r] + PT[r]);  // lanes < 12: Qux
-        double mdg = 0.0;
-        static_for<MM>([&](auto R) { mdg = (c == S + (int)R) ? qs[R] : mdg; });
-        const double dd = mdg + (lam1 + 1e-9);
-        dq = c >= S ? 1.0 / __builtin_sqrt(dd) : 1.0;
-        const double zd = 0.0 * dd;  // 0, or NaN for an infinite diagonal entry
+        for (int r = 0; r < MM; ++r) qs[r] = __builtin_fma(0.5, P[r] + PT[r], dgc[r]);
+        // D_c = diag(M)^-1/2 on lanes 12..15 (1 elsewhere).  Any positive D is exact
+        // algebra (the same D scales and unscales), so one v_rsq_f64 serves; the offset
+        // diagonal below is D_c^2 M_cc - 1 as computed, not an assumed 0.  A non-positive
+        // diagonal gives NaN, +inf gives D = 0 and a NaN diagonal: a failed first try.
+        double mdg = qs[0] * ohr[0];
+#pragma unroll
+        for (int r = 1; r < MM; ++r) mdg = __builtin_fma(qs[r], ohr[r], mdg);
+        dq = c >= S ? __builtin_amdgcn_rsq(mdg) : 1.0;
 #pragma unroll
         for (int r = 0; r < MM; ++r) {
           qs[r] *= dq;  // column scale (lanes 12..15)
-          rj[r] = 0.0;
+          rj[r] = nd[r];
         }
-        row_scale12(rj, dq, qs);  // row scale
-#pragma unroll
-        for (int r = 0; r < MM; ++r) rj[r] = (c == S + r) ? zd : rj[r];  // M' - I: unit diagonal
+        row_scale12(rj, dq, qs);  // row scale, minus I: M' - I
         double dj = 1.0;
         SweepQColChainOff<MM, S, S>::run(rj, dj, Qxx, ab, VA);
         const bool okj = (dj > 0.0) && (bcast<S>(rj[0]) == bcast<S>(rj[0]));
@@ -922,9 +933,11 @@ __device__ __forceinline__ void ric_body(const RiccatiArgs<double>& a, long long
         bool ok0 = true;
         if constexpr (MODE == 0) {
           // trace((M + eps I)^-1) = sum_c D_c^2 (1 - rj[c]_cc)
-          double dgi = 0.0;
-          static_for<MM>([&](auto R) { dgi = (c == S + (int)R) ? 1.0 - rj[R] : dgi; });
-          const double tr = lane_sum_off<MM, S>(dgi * (dq * dq));
+          const double d2 = dq * dq;
+          double wt[MM];
+#pragma unroll
+          for (int r = 0; r < MM; ++r) wt[r] = __builtin_fma(-rj[r], d2, d2);
+          const double tr = diag_sum4_off12(wt);
           const bool sure = okj && (tr < 1e6);
           if (__any(!sure && act)) {  // the exact jitter-free check (rows that step)
             double rc[MM];

@@ -7,6 +7,7 @@ All compute happens in libhop_amd.so; torch only owns memory and streams.
 from __future__ import annotations
 
 import numbers
+import struct
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -357,13 +358,37 @@ def _bstride(t, per, name, Bn):
     raise ValueError(f"{name} has unexpected shape {tuple(t.shape)}")
 
 
+_CONST = {}
+
+
+def _const_fill(v, n, dtype, dev):
+    """A read-only [n] device tensor filled with the scalar v, made once and reused:
+    a per-call torch.full is a fill kernel on the stream every step (the select +
+    gains step carried two, 9 us of its 459, tools/launch_gaps.py).  Keyed by the
+    value's bits (so -0.0 and 0.0, NaN payloads stay distinct).  During a graph
+    capture a plain fill is returned (a cached tensor would come from the capture's
+    pool); a new entry is synchronised once so another stream can read it at once."""
+    torch = _torch()
+    val = float(v) if dtype.is_floating_point else int(v)
+    if torch.cuda.is_current_stream_capturing():
+        return torch.full((n,), val, dtype=dtype, device=dev)
+    key = (struct.pack("<d", val) if dtype.is_floating_point else val, n, dtype, str(dev))
+    t = _CONST.get(key)
+    if t is None:
+        if len(_CONST) >= 64:
+            _CONST.clear()
+        t = torch.full((n,), val, dtype=dtype, device=dev)
+        torch.cuda.current_stream(dev).synchronize()
+        _CONST[key] = t
+    return t
+
+
 def _per_problem(v, Bn, dtype, dev, name):
-    """[Bn] device tensor from a scalar (a device fill: no host-device copy that
-    would stall the launch queue), a tensor, or an array."""
+    """[Bn] device tensor from a scalar (a cached device fill, _const_fill: no
+    host-device copy that would stall the launch queue), a tensor, or an array."""
     torch = _torch()
     if isinstance(v, numbers.Real) and not isinstance(v, bool):
-        return torch.full((Bn,), float(v) if dtype.is_floating_point else int(v), dtype=dtype,
-                          device=dev)
+        return _const_fill(v, Bn, dtype, dev)
     t = v if isinstance(v, torch.Tensor) else torch.as_tensor(v)
     return _dev(t.to(device=dev, dtype=dtype).reshape(-1).expand(Bn), name)
 
@@ -372,7 +397,7 @@ def _scalar_or_vec(v, dtype, dev, name):
     """[1] (a device fill) or [n] device tensor."""
     torch = _torch()
     if isinstance(v, numbers.Real) and not isinstance(v, bool):
-        return torch.full((1,), float(v), dtype=dtype, device=dev)
+        return _const_fill(v, 1, dtype, dev)
     t = v if isinstance(v, torch.Tensor) else torch.as_tensor(v)
     return _dev(t.to(device=dev, dtype=dtype).reshape(-1), name)
 

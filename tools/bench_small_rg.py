@@ -4,11 +4,15 @@ SchedCondSmall, four problems per wave) against the lane-per-problem kernel
 
     python tools/bench_small_rg.py [--out file.jsonl] [--batches 1,64,...]
 
-Each batch size runs in two child processes: the default library (the row-group
-kernel up to HOP_SMALL_RG_MAX, read once per process) and HOP_SMALL_RG_MAX=0 (the lane
-kernel for every batch).  Workloads: synthetic SPD blocks of s = 5, m = 1, N = 200
+Each batch size runs in two child processes: the default dispatch (the row-group
+kernel up to kSmallRowGroupMax) and HOP_OPT_SMALL_LANE (the lane kernel for every
+batch).  Workloads: synthetic SPD blocks of s = 5, m = 1, N = 200
 (synth.device_batch) and the bench's cart-pole augmented blocks at rho_reg = 1e-12
-(bench._s5_aug_side's construction: the drop-in's path at B = 4,096).  HIP events
+(bench._s5_aug_side's construction: the drop-in's path at B = 4,096), and the same
+cart-pole linearisation through the trajectory form (propagate_traj: the default
+dispatch -- hop_augment + the row-group sweep up to kSmallRowGroupMax, the fused
+lane-per-problem kernel above --, HOP_OPT_SMALL_LANE: the fused lane kernel at every
+batch, HOP_OPT_TRAJ_UNFUSED: hop_augment + the block sweep at every batch).  HIP events
 around 20 launches after 3 warm-ups, on torch's current stream.
 """
 import argparse
@@ -32,6 +36,7 @@ def child(batches, kind):
         N, t_min = 200, 40
         if kind == "synthetic":
             A, Bm, Q, Ri, z0, QT = synth.device_batch(Bn, 5, 1, N, seed=5, device=dev)
+            lin = X = U = None
         else:
             F, x0, xg, u_ref, Qc, R, alpha, w, _, _, _, wrap, _ = systems.make_cartpole_swingup(N=N)
             g = torch.Generator(device=dev)
@@ -45,10 +50,24 @@ def child(batches, kind):
             blk = engine.augment(lin.A, lin.B, lin.a_res, X, U, t(xg), t(u_ref), t(Qc),
                                  t(as_terminal_weight(alpha, F.n)), w, wrap_idx=wrap)
             A, Bm, Q, QT, z0 = blk.A, blk.B, blk.Q, blk.QT, blk.z0
-            Ri = torch.linalg.inv(t(R))
+            Ri = torch.linalg.inv(t(R)).contiguous()
+
+        lane = os.environ.get("HOP_BENCH_SMALL_LANE", "0") == "1"
 
         def run():
-            return engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=N)
+            from time_opt_ilqr_amd import _lib
+            with _lib.options(small_lane=lane):
+                return engine.propagate(A, Bm, Q, Ri, z0, QT, t_min=t_min, t_max=N)
+
+        if kind == "cartpole_traj":  # the trajectory form: fused (lane) or unfused (blocks)
+            unf = os.environ.get("HOP_BENCH_TRAJ_UNFUSED", "0") == "1"
+
+            def run():  # noqa: F811
+                from time_opt_ilqr_amd import _lib
+                with _lib.options(traj_unfused=unf, small_lane=lane):
+                    return engine.propagate_traj(lin.A, lin.B, lin.a_res, X, U, t(xg), t(u_ref),
+                                                 t(Qc), Ri, t(as_terminal_weight(alpha, F.n)), w,
+                                                 wrap_idx=wrap, t_min=t_min, t_max=N)
 
         r = run()
         for _ in range(3):
@@ -65,7 +84,7 @@ def child(batches, kind):
         out.append(dict(kind=kind, batch=Bn, ms=ms, sweeps_per_s=Bn / (ms * 1e-3),
                         status_ok=int(((r.status == 0) & fin).sum().item()),
                         t_star_sum=int(r.t_star.long().sum().item())))
-        del A, Bm, Q, QT, r
+        del A, Bm, Q, QT, r, lin, X, U
         torch.cuda.empty_cache()
     print(json.dumps(out), flush=True)
 
@@ -82,8 +101,11 @@ def main():
         child(batches, a.kind)
         return
     rows = []
-    for kind in ("synthetic", "cartpole_aug"):
-        for label, env in (("default", {}), ("lane", {"HOP_SMALL_RG_MAX": "0"})):
+    for kind in ("synthetic", "cartpole_aug", "cartpole_traj"):
+        paths = ((("default", {}), ("lane", {"HOP_BENCH_SMALL_LANE": "1"})) if kind != "cartpole_traj"
+                 else (("default", {}), ("traj_fused_lane", {"HOP_BENCH_SMALL_LANE": "1"}),
+                       ("traj_unfused", {"HOP_BENCH_TRAJ_UNFUSED": "1"})))
+        for label, env in paths:
             e = dict(os.environ, **env)
             p = subprocess.run([sys.executable, __file__, "--child", "1", "--kind", kind,
                                 "--batches", a.batches], env=e, capture_output=True, text=True,
