@@ -677,6 +677,9 @@ def main(argv=None):
                          "driver's) or gloo: the real kernels with the collectives through the "
                          "host, every rank on device LOCAL_RANK mod the visible devices -- a "
                          "rehearsal of this path on a one-GPU box, never a scaling measurement")
+    ap.add_argument("--event-every", type=int, default=0,
+                    help="HIP event pair around every k-th timed step for kernel_ms (0: "
+                         "K // 256, at least 1; 1: every step)")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the side timing of the other layout (profiling passes)")
     ap.add_argument("--no-anchor", action="store_true",
@@ -806,23 +809,29 @@ def main(argv=None):
     sync()
     K = args.steps
     # HIP events on the stream the kernels are launched on (engine launches on
-    # torch's current stream)
-    ev = [(event(), event()) for _ in range(K)]
+    # torch's current stream), around every `every`-th step of the timed region: an
+    # event pair on every step costs ~0.9 % of the step (tools/ab_step_events.py,
+    # profiles/r06_step_events.json), a sample of >= 256 steps averages the same
+    every = max(1, K // 256) if args.event_every <= 0 else args.event_every
+    ev = [(event(), event()) for _ in range(0, K, every)]
     if world > 1:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for i in range(K):
-        ev[i][0].record()
-        r = launch()
-        ev[i][1].record()
+        if i % every == 0:
+            ev[i // every][0].record()
+            r = launch()
+            ev[i // every][1].record()
+        else:
+            r = launch()
         if world > 1:
             gathered = hd.gather_selection(r.t_star, r.j_star, total_b)
     sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         hd.all_reduce_max(t)
@@ -994,7 +1003,8 @@ def main(argv=None):
                 cpu["note"] = "LFT sweep only (the Riccati gains are not in the CPU sample)"
         roof = {"bound": info["bound"], "achieved": achieved, "peak": peak, "unit": unit,
                 "frac": achieved / peak, "traffic": traffic, "kernel": info["kernel"],
-                "kernel_ms": kern_ms, "flops_per_sweep": info["flops"],
+                "kernel_ms": kern_ms, "kernel_ms_samples": len(ev),
+                "flops_per_sweep": info["flops"],
                 "alg_bytes_per_sweep": info["bytes"]}
         if info["executed"] and info["bound"] != "hbm":
             ex = info["executed"] * per_launch / (kern_ms * 1e-3) / 1e12
