@@ -122,6 +122,18 @@ struct SchedCond : SchedLdlDma {
   static constexpr int AROW = 1;
   static constexpr int SCALE = 0;  // first attempts only: its own sweeps (rerun on doubt)
 };
+#ifndef HOP_COND_DMAI
+#define HOP_COND_DMAI 0  // A/B builds (tools/exp_build.py): the DMA pieces inside the update
+#endif
+constexpr bool kCondDmai = HOP_COND_DMAI != 0;
+#ifndef HOP_FMA3
+#define HOP_FMA3 0  // A/B builds: the congruence query's row offsets as inline-asm v_fma_f64
+#endif
+constexpr bool kFma3 = HOP_FMA3 != 0;
+#ifndef HOP_SMALL_SWEEP2
+#define HOP_SMALL_SWEEP2 1  // small-s row groups: the two stage sweeps as one interleaved block
+#endif
+constexpr bool kSmallSweep2 = HOP_SMALL_SWEEP2 != 0;
 // + the QT image reads under the E sweep, the A/B reads under the X sweep
 #ifndef HOP_COND_WQ
 #define HOP_COND_WQ 1  // developer A/B builds (tools/exp_build.py): 0 = round 3's query
@@ -3048,9 +3060,13 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     stamp(2);
     {
       double d1 = 1.0, d2 = 1.0;
-      SweepQ<S>::run(NE, d1);
-      if constexpr (WQ) SweepQP<S>::run(NX, d2);  // pivots 0 .. S-2 (the congruence query)
-      else SweepQ<S>::run(NX, d2);
+      if constexpr (WQ && has_smalls<C>() && kSmallSweep2) {
+        SweepQ2<S>::run(NE, d1, NX, d2);  // both sweeps, pivot blocks interleaved
+      } else {
+        SweepQ<S>::run(NE, d1);
+        if constexpr (WQ) SweepQP<S>::run(NX, d2);  // pivots 0 .. S-2 (the congruence query)
+        else SweepQ<S>::run(NX, d2);
+      }
       bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
       flag(!pivots_ok(NE, d1) || !pivots_ok(NX, d2), 1, k + 1);
     }
@@ -3091,6 +3107,10 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     }
     at[S] = e_s;
     const bool dma_late = dstag<C>() == 1 && (w & 1);
+    // the step's DMA pieces spread through the update block instead of one burst
+    // before it (HOP_COND_DMAI, SchedCondLSymL only)
+    constexpr bool dmai = kCondDmai && has_symlate<C>() && has_sym2<C>() && !has_newt<C>() &&
+                          !TRAJ && !F32 && !has_pack<C>() && S == 13 && MM == 4;
     if constexpr (dstag<C>() == 2) {
       wave_sync();
       if (k + 1 < N)
@@ -3108,7 +3128,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     }
     if (dstag<C>() != 2 && !dma_late) {
       wave_sync();
-      if (k + 1 < N) dma_step(k + 1);
+      if (k + 1 < N && !dmai) dma_step(k + 1);
       if constexpr (has_symlate<C>()) {
         static_assert(!TRAJ && !has_pack<C>(), "own scratch: the one-wave layout");
         if (sym_step(k)) {
@@ -3135,7 +3155,32 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
           Ht[i] = X[i];
       }
       double dmin = 1.0;
-      if constexpr (has_sym2<C>() && has_newt<C>()) CondLdl2<S>::run(r, Ht, X, dmin);
+      if constexpr (dmai) {  // the next step's pieces issued inside the update block
+        {
+          // the last step re-reads its own blocks (in L2 / MALL), so the update has
+          // one form (two copies of the block spilled 40 VGPRs)
+          const int kn = k + 1 < N ? k + 1 : k;
+          DmaStep20 q;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) q.v[j] = voMl[j];
+          q.u[0] = voBl[0];
+          q.u[1] = voBl[1];
+          q.rq = rQ;
+          q.ra = rA;
+          q.rb = rB;
+          q.rt = rT;
+          q.so_m = (unsigned)(kn * SS * ES);
+          q.so_b = (unsigned)(kn * SM * ES);
+          q.m0[0] = wlds + G::OFF_Q;
+          q.m0[1] = wlds + G::OFF_Q + 4096;
+          q.m0[2] = wlds + G::OFF_A;
+          q.m0[3] = wlds + G::OFF_A + 4096;
+          q.m0[4] = wlds + G::OFF_B;
+          q.m0[5] = wlds + G::OFF_QT;
+          q.m0[6] = wlds + G::OFF_QT + 4096;
+          CondLdlO2R0D<S>::run(r, Ht, X, dmin, q);
+        }
+      } else if constexpr (has_sym2<C>() && has_newt<C>()) CondLdl2<S>::run(r, Ht, X, dmin);
       else if constexpr (has_sym2<C>()) CondLdlO2R0<S>::run(r, Ht, X, dmin);
       else if constexpr (has_newt<C>()) CondLdlO1R1<S>::run(r, Ht, X, dmin);
       else CondLdl<S>::run(r, Ht, X, dmin);
@@ -3233,7 +3278,13 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       // it is added before the congruence (no copy of Sigma's rows needed)
       double rq[S];
 #pragma unroll
-      for (int i = 0; i < S - 1; ++i) rq[i] = __builtin_fma(kmask, NX[i], X[i]);
+      for (int i = 0; i < S - 1; ++i) {
+        // one three-address v_fma_f64 (hipcc emitted a copy of X[i] + v_fmac: 12 moves)
+        if constexpr (kFma3)
+          asm("v_fma_f64 %0, %1, %2, %3" : "=v"(rq[i]) : "v"(kmask), "v"(NX[i]), "v"(X[i]));
+        else
+          rq[i] = __builtin_fma(kmask, NX[i], X[i]);
+      }
       rq[S - 1] = X[S - 1];
       RowB<S>::template sweep<S - 1>(rq, ub);  // (.) W^-1
       LaneB<S - 1>::fma(reinterpret_cast<double (&)[S - 1]>(rq), ub, rq[S - 1]);  // W^-T (.)
