@@ -166,6 +166,10 @@ def build(force=False, jobs=None, verbose=True):
         if verbose:
             print("[hop] libhop_amd.so up to date")
         return LIB
+    # the digest of the sources as compiled: taken before compiling, so a source edited
+    # while the build runs leaves a stale stamp (the next build recompiles) instead of
+    # a stamp that claims the edit is in the library
+    digest = _digest()
     hipcc = _hipcc()
     objdir = os.path.join(HERE, "_obj_dev" if DEV else "_obj")
     os.makedirs(objdir, exist_ok=True)
@@ -197,7 +201,7 @@ def build(force=False, jobs=None, verbose=True):
         print(f"[hop] {listed} hazards listed in $HOP_HAZARD_REPORT: no build stamp written")
         return LIB
     with open(_stamp_path(), "w") as f:
-        f.write(_digest())
+        f.write(digest)
     return LIB
 
 
