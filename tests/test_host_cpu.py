@@ -240,6 +240,54 @@ def test_hand_scheduled_blocks_emulated(n):
     assert abs(regs[n][n] - q) <= 1e-12 * abs(q)
 
 
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 6])
+def test_small_dual_sweep_block_emulated(n):
+    """SweepQ2<n> (the small-s row-group kernel's stage and terminal sweeps as one
+    interleaved block) computes exactly what SweepQ<n> and SweepQP<n>
+    compute separately, register for register (CPU emulation of the instruction
+    strings, tools/emu_dpp.py), and SweepQ's part is the offset-form negated inverse."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(40 + n)
+    eps = 1e-9
+
+    def rows(M):
+        out = []
+        for i in range(n):
+            col = rng.standard_normal(16)
+            col[:n] = M[i]
+            col[i] += eps - 1.0
+            out.append(col)
+        return out
+
+    def spd():
+        M = rng.standard_normal((n, n))
+        return M @ M.T + n * np.eye(n)
+    M1, M2 = spd(), spd()
+    r1, r2 = rows(M1), rows(M2)
+    both = {}
+    for i in range(n):
+        both[i], both[n + 8 + i] = r1[i].copy(), r2[i].copy()
+    both[n], both[2 * n + 8] = np.ones(16), np.ones(16)
+    for j in range(7):
+        both[n + 1 + j] = np.full(16, np.nan)
+        both[2 * n + 9 + j] = np.full(16, np.nan)
+    E.run(E.extract(inc, "SweepQ2", n), both)
+    for name, r0, base, dm in (("SweepQ", r1, 0, n), ("SweepQP", r2, n + 8, 2 * n + 8)):
+        sep = {i: r0[i].copy() for i in range(n)}
+        sep[n] = np.ones(16)
+        for j in range(7):
+            sep[n + 1 + j] = np.full(16, np.nan)
+        E.run(E.extract(inc, name, n), sep)
+        for i in range(n):
+            assert np.array_equal(both[base + i], sep[i]), (name, i)
+        assert np.array_equal(both[dm], sep[n])
+    got = np.array([both[i][:n] for i in range(n)])
+    assert np.abs(got - (np.eye(n) - np.linalg.inv(M1 + eps * np.eye(n)))).max() < 1e-12
+
+
 @pytest.mark.parametrize("n", [3, 13])
 def test_query_ldl_block_emulated(n):
     """QueryLdl<n>: X0 = Ebar - H^T (Mt + eps I)^-1 H from the offset-form Mt
