@@ -130,6 +130,10 @@ constexpr bool kCondDmai = HOP_COND_DMAI != 0;
 #define HOP_FMA3 0  // A/B builds: the congruence query's row offsets as inline-asm v_fma_f64
 #endif
 constexpr bool kFma3 = HOP_FMA3 != 0;
+#ifndef HOP_COND_SWEEP2
+#define HOP_COND_SWEEP2 0  // A/B: the s = 13 kernel's two sweeps as one interleaved block
+#endif
+constexpr bool kCondSweep2 = HOP_COND_SWEEP2 != 0;
 #ifndef HOP_SMALL_SWEEP2
 #define HOP_SMALL_SWEEP2 1  // small-s row groups: the two stage sweeps as one interleaved block
 #endif
@@ -3004,6 +3008,38 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       }
 #pragma unroll
       for (int q = 0; q < MM; ++q) brow[q] = (double)o2[2 * S + q];
+      stamp(3);
+    } else if constexpr (has_ldspipe<C>() && !TRAJ && kCondSweep2 && WQ && has_sym2<C>() &&
+                         S == 13 && MM == 4 && dstag<C>() == 0) {
+      // Q's and QT's symmetric sums behind one LDS round trip, then the two independent
+      // sweeps as one interleaved block (each sweep's pivot chains hide behind the
+      // other's FMAs) with A_k's / B_k's reads underneath
+      const bool in = c < S;
+      const unsigned iq = lds_addr(imQ), it = lds_addr(imT);
+      const unsigned a4[4] = {in ? iq + 8u * c : zaddr, in ? iq + 8u * S * c : zaddr,
+                              in ? it + 8u * c : zaddr, in ? it + 8u * S * c : zaddr};
+      double qq[4 * S];
+      LdsSym2<S, S>::run(a4, qq);
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        NE[i] = qq[i] + qq[S + i];
+        NX[i] = qq[2 * S + i] + qq[3 * S + i];
+      }
+      stamp(2);
+      double d1 = 1.0, d2 = 1.0;
+      double o2[2 * S + MM];
+      const unsigned ab[3] = {in ? lds_addr(imA) + 8u * S * c : zaddr, lds_addr(imA) + 8u * c,
+                              in ? lds_addr(imB) + 8u * MM * c : zaddr};
+      SweepQ2AB<S>::run(NE, d1, NX, d2, o2, ab);  // X: pivots 0 .. S-2 (the congruence query)
+      bad = bad || !pivots_ok(NE, d1) || !pivots_ok(NX, d2);
+      flag(!pivots_ok(NE, d1) || !pivots_ok(NX, d2), 1, k + 1);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        at[j] = o2[j];
+        if constexpr (has_arow<C>()) ar[j] = o2[S + j];
+      }
+#pragma unroll
+      for (int q = 0; q < MM; ++q) brow[q] = o2[2 * S + q];
       stamp(3);
     } else if constexpr (has_ldspipe<C>() && !TRAJ) {
       // QT's sym reads ride under the E sweep, A_k / B_k's under the X sweep
