@@ -134,6 +134,10 @@ constexpr bool kFma3 = HOP_FMA3 != 0;
 #define HOP_COND_SWEEP2 0  // A/B: the s = 13 kernel's two sweeps as one interleaved block
 #endif
 constexpr bool kCondSweep2 = HOP_COND_SWEEP2 != 0;
+#ifndef HOP_COND_MFMA64
+#define HOP_COND_MFMA64 0  // A/B: the s = 13 fp64 predict on v_mfma_f64_16x16x4_f64
+#endif
+constexpr bool kCondMfma64 = HOP_COND_MFMA64 != 0;
 #ifndef HOP_SMALL_SWEEP2
 #define HOP_SMALL_SWEEP2 1  // small-s row groups: the two stage sweeps as one interleaved block
 #endif
@@ -2755,13 +2759,28 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   static_assert(!MF || (F32 && S == 13 && MM == 4), "MFMA predict: fp32 blocks, s = 13");
   // MFMA: the zero area grows to 2,880 B (a zero and a 1.0f for every problem's
   // image offset p * IMGM, p < 4) and the f32 staging region follows it
-  constexpr int ZB = MF ? 2880 : 8 * (S * S + 8);
+  // MF64 (HOP_COND_MFMA64, A/B): the fp64 predict's two products on v_mfma_f64_16x16x4_f64,
+  // one problem per 16 x 16 tile; [Sigma' | m'] staged through the Q image and the result
+  // through the QT image (both read by then), so the step's DMA moves after the predict.
+  // Zero area: zeros at every p * 1360 (image offsets) and p * 1472 (staging offsets),
+  // a 1.0 at 1416 + p * 1360 (A~'s (13, 13), the m' pass-through), p < 4.
+  constexpr bool MF64 = kCondMfma64 && has_symlate<C>() && has_sym2<C>() && !has_newt<C>() &&
+                        !has_peps<C>() && !TRAJ && !F32 && !has_pack<C>() && S == 13 && MM == 4 &&
+                        dstag<C>() == 0;
+  constexpr int M6XP = 1472, M6ONE = 1416;  // staging stride per problem, 1.0 offset (bytes)
+  static_assert(!MF64 || (G::IMGM == 1360 && M6ONE + 3 * G::IMGM + 8 <= G::TILE_W &&
+                          4 * M6XP <= G::IMGM_W && 8 * (S * S + 8) <= M6ONE),
+                "fp64 MFMA staging: Q / QT image areas, ones past the sym zero area");
+  constexpr int ZB = MF ? 2880 : (MF64 ? 3 * M6XP + 8 : 8 * (S * S + 8));
   constexpr int MFB = 2880, MFP = 1152;  // staging region offset, bytes per problem
   static_assert(!MF || (MFB + 4 * MFP <= G::TILE_W && 800 + 3 * G::IMGM + 4 <= ZB &&
                         G::IMGM == 688),
                 "MFMA staging in the tile slot");
 #pragma unroll 1
   for (int i = lane; i < ZB / 8; i += 64) zarea[i] = 0.0;
+  if constexpr (MF64) {
+    if (lane < 4) zarea[(M6ONE + lane * G::IMGM) / 8] = 1.0;
+  }
   if constexpr (MF) {
     float* mz = reinterpret_cast<float*>(wbase + G::OFF_T + MFB);
 #pragma unroll 1
@@ -2945,6 +2964,34 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       const bool in = c < S && kx < S;
       ma_b[kk] = in ? ia + 4u * (S * c + kx) : (c == S && kx == S ? zaddr + 800u : zaddr);
       ma_a[kk] = in ? ia + 4u * (S * c + kx) : zaddr;
+    }
+  }
+
+  // MF64 operand addresses (problem p at an immediate offset: p * M6XP in the staging,
+  // p * IMGM in the A image; invalid lanes read the zero area at the same offsets):
+  //   f64 MFMA C/D map (cdna_hip_programming.md): lane (g, c) holds row g + 4 r, column c
+  //   of register r; A / B as the f32 16x16x4 form (A[c][k], B[k][c], k = lane group).
+  //   product 1 (T = [Sigma' | m'] A~^T), slice kk: lane (g, c) carries k = 4 g + kk:
+  //     A operand X[c][k] (staged [p][row][14]), B operand A~^T[k][c] = A[c][k] (+ the 1.0);
+  //   product 2 (A T), slice kk: k = g + 4 kk, so the B operand is register kk of T's
+  //     accumulator (row g + 4 kk, column c) and the A operand A[c][g + 4 kk];
+  //   the result (row g + 4 r, column c) goes to the QT image as [p][column][13].
+  unsigned m6_xw = 0, m6_xa[4] = {}, m6_aa[4] = {}, m6_ab[4] = {}, m6_dw = 0, m6_xr = 0;
+  if constexpr (MF64) {
+    const unsigned qb = lds_addr(imQ) - (unsigned)(g * G::IMGM);  // the wave's Q image area
+    const unsigned tb = lds_addr(imT) - (unsigned)(g * G::IMGM);
+    const unsigned ab = lds_addr(imA) - (unsigned)(g * G::IMGM);
+    m6_xw = qb + (unsigned)(g * M6XP) + 8u * c;
+    m6_dw = tb + 8u * (S * c + g);
+    m6_xr = c < S + 1 ? tb + (unsigned)(g * M6XP) + 8u * S * c : zaddr;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int kx = 4 * g + kk;
+      m6_xa[kk] = (c < S && kx < S + 1) ? qb + 8u * ((S + 1) * c + kx) : zaddr;
+      const bool in = c < S && kx < S;
+      m6_ab[kk] = in ? ab + 8u * (S * c + kx) : (c == S && kx == S ? zaddr + M6ONE : zaddr);
+      const int k2 = g + 4 * kk;  // product 2's k (the accumulator's row map)
+      m6_aa[kk] = (c < S && k2 < S) ? ab + 8u * (S * c + k2) : zaddr;
     }
   }
 
@@ -3164,7 +3211,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     }
     if (dstag<C>() != 2 && !dma_late) {
       wave_sync();
-      if (k + 1 < N && !dmai) dma_step(k + 1);
+      if (k + 1 < N && !dmai && !MF64) dma_step(k + 1);
       if constexpr (has_symlate<C>()) {
         static_assert(!TRAJ && !has_pack<C>(), "own scratch: the one-wave layout");
         if (sym_step(k)) {
@@ -3267,6 +3314,49 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
           X[I] = (double)*reinterpret_cast<const float*>(lds_ptr(ms_r + 4u * I)) +
                  sel_lane<I>(0.0, 1e-9);
         });
+      } else if constexpr (MF64) {
+        typedef double d4 __attribute__((ext_vector_type(4)));
+        if (c < S + 1) {  // stage [Sigma' | m'] rows: [p][row][14] doubles in the Q image
+#pragma unroll
+          for (int i = 0; i < S; ++i)
+            *reinterpret_cast<double*>(lds_ptr(m6_xw + 8u * (S + 1) * i)) = X[i];
+        }
+        wave_sync();
+        double xa[4][4], aa[4][4], bb[4][4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            xa[kk][q] = *reinterpret_cast<const double*>(lds_ptr(m6_xa[kk] + q * M6XP));
+            aa[kk][q] = *reinterpret_cast<const double*>(lds_ptr(m6_aa[kk] + q * G::IMGM));
+            bb[kk][q] = *reinterpret_cast<const double*>(lds_ptr(m6_ab[kk] + q * G::IMGM));
+          }
+        d4 D1[4], D2[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) D1[q] = D2[q] = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            D1[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[kk][q], bb[kk][q], D1[q], 0, 0, 0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            D2[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(aa[kk][q], D1[q][kk], D2[q], 0, 0, 0);
+        wave_sync();  // the staging reads are done: the QT image takes the result
+        if (c < S + 1) {  // rows g + 4 r < S of column c, as [p][column][13]
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (g + 4 * r < S)
+                *reinterpret_cast<double*>(lds_ptr(m6_dw + q * M6XP + 32u * r)) = D2[q][r];
+        }
+        wave_sync();
+        static_for<S>([&](auto I) {
+          X[I] = *reinterpret_cast<const double*>(lds_ptr(m6_xr + 8u * I)) + sel_lane<I>(0.0, 1e-9);
+        });
       } else if constexpr (has_peps<C>()) {
         PredictEps<S>::run(Xs, Tm, at, ar, eps_addr);  // eps I + A [Sigma' | m'] A~^T
       } else {
@@ -3293,6 +3383,10 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
                                (w * kProbPerWave + g) * S * S,
                        c);
       }
+    }
+    if constexpr (MF64) {  // the Q / QT / A images are read: the next step's pieces
+      wave_sync();
+      if (k + 1 < N) dma_step(k + 1);
     }
     stamp(6);
     // ---- query horizon t = k + 1: [Sigma_eps + X_t - I | m] by bordered elimination
