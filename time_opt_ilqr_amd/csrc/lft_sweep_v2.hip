@@ -4092,9 +4092,9 @@ hipError_t dispatch_lft_v2(const LftArgs<double>& a, hipStream_t stream) {
   }
   // default (variant 40): conditioned prefix + rerun of the problems it flagged; the
   // stage / terminal inverses of the unhalved symmetric sums (SYM2: 1-2 % faster than
-  // the halved sums, profiles/r03_ab1_cond_schedules.txt, r03_ab_pe.txt); the periodic
+  // the halved sums, profiles/history/r03_ab1_cond_schedules.txt, r03_ab_pe.txt); the periodic
   // symmetrisation after the step's DMA issue, in its own LDS scratch (SchedCondLSymL:
-  // 0.4 % faster than before it, bitwise equal, profiles/r04_p18_ab_symlate.txt)
+  // 0.4 % faster than before it, bitwise equal, profiles/history/r04_p18_ab_symlate.txt)
   return cond_pipe(v2::lft_cond_kernel<v2::SchedCondLSymL, 13, 4>, bytes_symlate);
 }
 

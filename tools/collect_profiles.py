@@ -1,4 +1,4 @@
-"""Copy one tools/prof_r02.sh pass into profiles/ (tracked): bench lines, rocprofv3
+"""Copy one tools/archive/prof_r02.sh pass into profiles/ (tracked): bench lines, rocprofv3
 kernel stats per workload, a PMC summary per kernel, and the PMC traffic entries of
 profiles/traffic.json.
 
