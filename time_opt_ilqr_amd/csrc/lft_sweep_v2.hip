@@ -267,8 +267,16 @@ constexpr bool has_peps() {
 // symmetric sums (SYM2) and the congruence query (WQ, the terminal block's X sweep
 // stopped one pivot short: SweepQP) like the s = 13 default; the image reads are
 // plain (no LDS-pipelined sweeps: SweepQSym / SweepQAB exist for s = 13 only).
+#ifndef HOP_SMALL_QPIPE
+#define HOP_SMALL_QPIPE 0  // small-s row groups: step k's query under step k+1's sweeps (A/B)
+#endif
+constexpr bool kSmallQPipe = HOP_SMALL_QPIPE != 0;
+#ifndef HOP_SMALL_STAMP
+#define HOP_SMALL_STAMP 0  // diagnostic builds: section stamps (tools/stamps_small.py)
+#endif
 struct SchedCondSmall : SchedCond {
   static constexpr int SYM2 = 1, NEWT = 0, PEPS = 0, WQ = 1, SMALLS = 1;
+  static constexpr int STAMP = HOP_SMALL_STAMP;
 };
 template <class C>
 constexpr bool has_smalls() {
@@ -2999,13 +3007,59 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
   double best = 0.0, jprev = 0.0;
   int tbest = 0;
   const bool fuse_argmin = a.t_max > 0;
+  // QPIPE (small-s row groups): the query of horizon k + 1 runs in step k + 1, its
+  // ElimQ interleaved with that step's two sweeps (SweepQ2ElimQ): at s <= 5 each of
+  // them is a chain of short pivot blocks.  Same operations on the same values (the
+  // query reads Sigma before the next step's symmetrisation and update, as before), so
+  // J and T* are bitwise the in-step query's; flags keep their horizons.
+  constexpr bool QPIPE = WQ && has_smalls<C>() && kSmallSweep2 && kSmallQPipe;
+  double NXp[S];  // the terminal block's sweep of the pending query
+#pragma unroll
+  for (int i = 0; i < S; ++i) NXp[i] = 0.0;
+  // the query's congruence prelude (see the in-step query below) and its tail
+  auto query_prelude = [&](const double (&nx)[S], double (&rq)[S], double& gam, int kq) {
+    const double ub = c < S - 1 ? nx[S - 1] : 0.0;
+    const double sg = (bcast<S - 1>(nx[S - 1]) + 1.0) * (1.0 / KOFF);
+    bad = bad || !(sg > 0.0);
+    flag(!(sg > 0.0), 1, kq + 1);
+#pragma unroll
+    for (int i = 0; i < S - 1; ++i) rq[i] = __builtin_fma(kmask, nx[i], X[i]);
+    rq[S - 1] = X[S - 1];
+    RowB<S>::template sweep<S - 1>(rq, ub);
+    LaneB<S - 1>::fma(reinterpret_cast<double (&)[S - 1]>(rq), ub, rq[S - 1]);
+    rq[S - 1] = __builtin_fma(e_last, recip_nr(sg) - KOFF, rq[S - 1]);
+    gam = bcast<S>(X[S]);
+  };
+  auto query_tail = [&](double acc, double dmin, double gam, int kq) {
+    const double q = bcast<S>(acc);
+    bad = bad || !(dmin > 0.0) || (q != q);
+    flag(!(dmin > 0.0) || (q != q), 16, kq + 1);
+    const double jk = 0.5 * (q - gam);
+    bad = bad || !finite_val(jk);
+    flag(!finite_val(jk), 32, kq + 1);
+    kf1 = (bad && kf1 == 0) ? kq + 2 : kf1;
+    if (valid && c == 0) a.J[prob * N + kq] = (T)jk;
+    if (fuse_argmin) {
+      const int t = kq + 1;
+      if (t == a.t_min) {
+        best = jk;
+        tbest = t;
+      } else if (t > a.t_min && t <= a.t_max) {
+        const bool bnan = best != best, jnan = jk != jk;
+        if (!bnan && (jnan || jk < best)) {
+          best = jk;
+          tbest = t;
+        }
+      }
+    }
+  };
 #pragma unroll 1
   for (int k = 0; k < N; ++k) {
     stamp(-1);
     dma_wait();
     wave_sync();
     stamp(0);
-    if (k > 0 && valid && c == 0) a.J[prob * N + k - 1] = (T)jprev;
+    if (!QPIPE && k > 0 && valid && c == 0) a.J[prob * N + k - 1] = (T)jprev;
     double atil = 0.0;
     if constexpr (F32) {
     } else if constexpr (TRAJ) {
@@ -3143,7 +3197,16 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     stamp(2);
     {
       double d1 = 1.0, d2 = 1.0;
-      if constexpr (WQ && has_smalls<C>() && kSmallSweep2) {
+      if constexpr (QPIPE) {
+        if (k > 0) {  // step k - 1's query under this step's sweeps
+          double rq[S], gam, accq = 0.0, dminq = 1.0;
+          query_prelude(NXp, rq, gam, k - 1);
+          SweepQ2ElimQ<S>::run(NE, d1, NX, d2, rq, accq, dminq, KOFF);
+          query_tail(accq, dminq, gam, k - 1);
+        } else {
+          SweepQ2<S>::run(NE, d1, NX, d2);
+        }
+      } else if constexpr (WQ && has_smalls<C>() && kSmallSweep2) {
         SweepQ2<S>::run(NE, d1, NX, d2);  // both sweeps, pivot blocks interleaved
       } else {
         SweepQ<S>::run(NE, d1);
@@ -3389,6 +3452,12 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
       if (k + 1 < N) dma_step(k + 1);
     }
     stamp(6);
+    if constexpr (QPIPE) {  // the query runs in the next step (or after the loop)
+#pragma unroll
+      for (int i = 0; i < S; ++i) NXp[i] = NX[i];
+      kf1 = (bad && kf1 == 0) ? k + 2 : kf1;  // this step's stage flags: horizon k + 1
+      continue;
+    }
     // ---- query horizon t = k + 1: [Sigma_eps + X_t - I | m] by bordered elimination
     double jk;
     if constexpr (WQ) {
@@ -3459,6 +3528,14 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     }
     jprev = jk;
   }
+  if constexpr (QPIPE) {  // the last step's query
+    if (N > 0) {
+      double rq[S], gam, acc = 0.0, dmin = 1.0;
+      query_prelude(NXp, rq, gam, N - 1);
+      ElimQ<S>::run(rq, acc, dmin, KOFF);
+      query_tail(acc, dmin, gam, N - 1);
+    }
+  }
   dma_wait();
   if constexpr (C::STAMP) {
     if (lane == 0) {
@@ -3467,7 +3544,7 @@ __global__ __launch_bounds__(256, has_pack<C>() ? 2 : 1) void lft_cond_kernel(Lf
     }
   }
   if (valid && c == 0) {
-    if (N > 0) a.J[prob * N + N - 1] = (T)jprev;
+    if (!QPIPE && N > 0) a.J[prob * N + N - 1] = (T)jprev;
     // the hand-over word (include/hop.h); the developer reason field under cond & 4
     a.status[prob] = bad ? ((a.cond & 4) ? (int)ST_RERUN | why << HOP_HANDOVER_REASON_SHIFT
                                          : HOP_HANDOVER_WORD(kf1 - 1))
