@@ -288,6 +288,64 @@ def test_small_dual_sweep_block_emulated(n):
     assert np.abs(got - (np.eye(n) - np.linalg.inv(M1 + eps * np.eye(n)))).max() < 1e-12
 
 
+@pytest.mark.parametrize("n", [3, 5])
+def test_small_sweeps_with_query_block_emulated(n):
+    """SweepQ2ElimQ<n> (the A/B switch HOP_SMALL_QPIPE: a step's query interleaved with
+    the next step's two sweeps) computes exactly SweepQ2<n> and ElimQ<n> run one after
+    the other, register for register (CPU emulation, tools/emu_dpp.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import emu_dpp as E
+    inc = open(os.path.join(REPO, "time_opt_ilqr_amd", "csrc", "dpp_blocks.inc")).read()
+    rng = np.random.default_rng(70 + n)
+
+    def rows(off):
+        M = rng.standard_normal((n, n))
+        M = M @ M.T + n * np.eye(n)
+        out = []
+        for i in range(n):
+            col = rng.standard_normal(16)
+            col[:n] = M[i]
+            col[i] += off
+            out.append(col)
+        return out
+    r1, r2, q = rows(1e-9 - 1.0), rows(1e-9 - 1.0), rows(0.0)
+    for col, z in zip(q, rng.standard_normal(n)):
+        col[n] = z
+    eps = 2.0
+    both = {}
+    for i in range(n):
+        both[i], both[n + 8 + i], both[2 * n + 16 + i] = r1[i].copy(), r2[i].copy(), q[i].copy()
+    both[n], both[2 * n + 8] = np.ones(16), np.ones(16)
+    both[3 * n + 16], both[3 * n + 17] = np.zeros(16), np.ones(16)
+    for j in range(7):
+        both[n + 1 + j] = np.full(16, np.nan)
+        both[2 * n + 9 + j] = np.full(16, np.nan)
+    for j in range(8):
+        both[3 * n + 18 + j] = np.full(16, np.nan)
+    both[3 * n + 26] = np.full(16, eps)
+    E.run(E.extract(inc, "SweepQ2ElimQ", n), both)
+    two = {}
+    for i in range(n):
+        two[i], two[n + 8 + i] = r1[i].copy(), r2[i].copy()
+    two[n], two[2 * n + 8] = np.ones(16), np.ones(16)
+    for j in range(7):
+        two[n + 1 + j] = np.full(16, np.nan)
+        two[2 * n + 9 + j] = np.full(16, np.nan)
+    E.run(E.extract(inc, "SweepQ2", n), two)
+    el = {i: q[i].copy() for i in range(n)}
+    el[n], el[n + 1] = np.zeros(16), np.ones(16)
+    for j in range(8):
+        el[n + 2 + j] = np.full(16, np.nan)
+    el[n + 10] = np.full(16, eps)
+    E.run(E.extract(inc, "ElimQ", n), el)
+    for i in range(n):
+        assert np.array_equal(both[i], two[i]) and np.array_equal(both[n + 8 + i], two[n + 8 + i])
+        assert np.array_equal(both[2 * n + 16 + i], el[i])
+    assert np.array_equal(both[n], two[n]) and np.array_equal(both[2 * n + 8], two[2 * n + 8])
+    assert np.array_equal(both[3 * n + 16], el[n]) and np.array_equal(both[3 * n + 17], el[n + 1])
+
+
 @pytest.mark.parametrize("n", [3, 13])
 def test_query_ldl_block_emulated(n):
     """QueryLdl<n>: X0 = Ebar - H^T (Mt + eps I)^-1 H from the offset-form Mt
