@@ -854,3 +854,28 @@ def test_zero_step_is_rejected_like_the_reference(dev, golden_dir, tag):
     assert (acc == -1).all(), np.nonzero(acc != -1)[0][:8]
     assert torch.equal(r.X[torch.as_tensor(fin)], X[torch.as_tensor(fin)])
     assert torch.equal(r.J, r.J_old)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_ilqr_outer_loop_host_callables_vs_reference(dev, golden_dir, tag):
+    """solver.ilqr_timeopt with the dynamics as a plain Python callable F(x, u) (the
+    oracle's NumPy dynamics, the reference's bit for bit) and, for the point mass, the
+    obstacle cost as a plain callable too: the host evaluates F and the stage cost per
+    problem (host_dynamics.py) while the select, Riccati and accept steps run on the
+    device.  Same bars as the device-dynamics run above."""
+    from time_opt_ilqr_amd import solver, systems
+    d, sid, wrap, obs = _case(golden_dir, tag)
+    mk = list(systems.MAKERS.values())[sid]
+    Fd, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap_idx, extra = mk(N=int(d["N"]))
+    F = dyn._scalar_F(sid, Fd.dt)
+    cost = None
+    if extra:
+        cost = lambda x, u: io.obstacle_cost(x, obs)  # noqa: E731
+    sol = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, int(d["N"]), int(d["T_min"]),
+                              int(d["T_max"]), max_iter=int(d["max_iter"]), wrap_idx=wrap_idx,
+                              use_central_diff=bool(d["central"]), extra_stage_cost=cost)
+    tol = 1e-8 if tag == "cartpole" else 1e-9
+    assert sol["T_hist"] == [int(t) for t in d["T_hist"]]
+    assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= tol
+    assert sol["T_star"] == int(d["T_star"])
+    assert _rel(np.nan_to_num(sol["X"]), np.nan_to_num(d["X"])) <= 100 * tol

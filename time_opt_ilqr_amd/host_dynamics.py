@@ -1,0 +1,180 @@
+"""Caller-side dynamics and stage costs given as Python callables (the reference's own
+call form, ``F(x, u) -> x_next`` and ``extra_stage_cost(x, u) -> (c, cx, cxx)``).
+
+The device outer loop (``solver.ilqr_timeopt_batch``) runs the built-in systems'
+dynamics, FD linearisation and line search on the GPU.  A user system the device has
+no kernel for arrives as a Python callable; these helpers evaluate it on the host,
+one problem at a time as the reference does, and hand the arrays to the same device
+select (LFT sweep + argmin), truncated Riccati pass and accept / LM / stop step.  The
+hot path stays on the GPU; only the callable's own evaluations run here.
+
+Semantics follow the reference functions they stand in for:
+  rollout               /root/reference/solver.py:40-59 (divergence check, NaN tail)
+  linearize             /root/reference/linearization.py:177-262 (central and forward
+                        differences, h = max(eps, rel * max(1, |v|))) and :269-270
+                        (affine residuals F(x_k, u_k) - x_{k+1})
+  cost_true             /root/reference/solver.py:65-102
+  linesearch            /root/reference/solver.py:233-286
+"""
+from dataclasses import dataclass
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+
+from .utils import wrap_error
+
+
+@dataclass
+class HostDynamics:
+    """A user dynamics callable ``F(x, u) -> x_next`` with its state / control sizes."""
+    F: Callable
+    n: int
+    m: int
+    name: str = "host"
+
+    def __call__(self, x, u):
+        return np.asarray(self.F(x, u), dtype=float).reshape(-1)
+
+
+def rollout(F, x0, U, *, max_state_norm: float = 1e6) -> np.ndarray:
+    """One problem: X [N+1, n]; the first non-finite, wrong-sized or too-large state
+    and everything after it are NaN."""
+    x0 = np.asarray(x0, dtype=float).reshape(-1)
+    U = np.asarray(U, dtype=float)
+    N, n = U.shape[0], x0.size
+    X = np.full((N + 1, n), np.nan)
+    X[0] = x0
+    for k in range(N):
+        xn = np.asarray(F(X[k], U[k]), dtype=float).reshape(-1)
+        if xn.size != n or not np.all(np.isfinite(xn)) or float(np.linalg.norm(xn)) > max_state_norm:
+            break
+        X[k + 1] = xn
+    return X
+
+
+def _step(v, eps, rel):
+    return max(float(eps), float(rel) * max(1.0, abs(float(v))))
+
+
+def linearize(F, X, U, *, central: bool = True, epsx: float = 1e-5, epsu: float = 1e-5,
+              relx: float = 1e-6, relu: float = 1e-6):
+    """One problem: A [N, n, n], B [N, n, m] by finite differences and the affine
+    residuals a [N, n] = F(x_k, u_k) - x_{k+1} (non-finite states propagate as NaN,
+    quietly)."""
+    with np.errstate(all="ignore"):
+        return _linearize(F, X, U, central, epsx, epsu, relx, relu)
+
+
+def _linearize(F, X, U, central, epsx, epsu, relx, relu):
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float)
+    N, n, m = U.shape[0], X.shape[1], U.shape[1]
+    A = np.zeros((N, n, n))
+    Bm = np.zeros((N, n, m))
+    a = np.zeros((N, n))
+    for k in range(N):
+        x, u = X[k], U[k]
+        f0 = np.asarray(F(x, u), dtype=float).reshape(-1)
+        a[k] = f0 - X[k + 1]
+        if central:
+            for i in range(n):
+                h = _step(x[i], epsx, relx)
+                xp, xm = x.copy(), x.copy()
+                xp[i] += h
+                xm[i] -= h
+                A[k, :, i] = (np.asarray(F(xp, u), dtype=float).reshape(-1) -
+                              np.asarray(F(xm, u), dtype=float).reshape(-1)) / (2.0 * h)
+            for j in range(m):
+                h = _step(u[j], epsu, relu)
+                up, um = u.copy(), u.copy()
+                up[j] += h
+                um[j] -= h
+                Bm[k, :, j] = (np.asarray(F(x, up), dtype=float).reshape(-1) -
+                               np.asarray(F(x, um), dtype=float).reshape(-1)) / (2.0 * h)
+        else:
+            if not np.all(np.isfinite(f0)):  # the forward form marks the whole step
+                A[k] = np.nan
+                Bm[k] = np.nan
+                continue
+            for i in range(n):
+                h = _step(x[i], epsx, relx)
+                e = np.zeros(n)
+                e[i] = h
+                A[k, :, i] = (np.asarray(F(x + e, u), dtype=float).reshape(-1) - f0) / h
+            for j in range(m):
+                h = _step(u[j], epsu, relu)
+                e = np.zeros(m)
+                e[j] = h
+                Bm[k, :, j] = (np.asarray(F(x, u + e), dtype=float).reshape(-1) - f0) / h
+    return A, Bm, a
+
+
+def stage_cost_terms(extra_stage_cost, X, U):
+    """extra_stage_cost at every (x_k, u_k), k < N: c [N], cx [N, n], cxx [N, n, n]
+    (the qxx_extra / qx_extra / c_extra arrays of the device select and Riccati)."""
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float)
+    N, n = U.shape[0], X.shape[1]
+    c = np.zeros(N)
+    cx = np.zeros((N, n))
+    cxx = np.zeros((N, n, n))
+    for k in range(N):
+        ck, gk, hk = extra_stage_cost(X[k], U[k])
+        c[k] = float(ck)
+        cx[k] = np.asarray(gk, dtype=float).reshape(n)
+        cxx[k] = np.asarray(hk, dtype=float).reshape(n, n)
+    return c, cx, cxx
+
+
+def cost_true(X, U, xg, u_ref, Q, R, Qf, w, T_star: int, wrap_idx: Optional[Sequence[int]] = None,
+              extra_stage_cost=None) -> float:
+    """Running cost up to T_star plus the terminal cost at T_star (Qf = the terminal
+    weight already expanded, as_terminal_weight(alpha))."""
+    T = int(T_star)
+    if T <= 0:
+        return float("inf")
+    if not np.all(np.isfinite(X[:T + 1])) or not np.all(np.isfinite(U[:T])):
+        return float("inf")
+    c = 0.0
+    for k in range(T):
+        e = np.atleast_1d(wrap_error(X[k] - xg, wrap_idx)).reshape(-1)
+        du = np.atleast_1d(U[k] - u_ref).reshape(-1)
+        if not np.all(np.isfinite(e)) or not np.all(np.isfinite(du)):
+            return float("inf")
+        c += 0.5 * float(e @ (Q @ e)) + 0.5 * float(du @ (R @ du)) + float(w)
+        if extra_stage_cost is not None:
+            c += float(extra_stage_cost(X[k], U[k])[0])
+    eT = np.atleast_1d(wrap_error(X[T] - xg, wrap_idx)).reshape(-1)
+    if not np.all(np.isfinite(eT)):
+        return float("inf")
+    return float(c + 0.5 * float(eT @ (Qf @ eT)))
+
+
+def linesearch(F, X, U, T_star: int, K, kff, cost_args, alphas, extra_stage_cost=None):
+    """One problem: the first step size whose rollout (controls U + alpha k + K dx up
+    to T_star, U beyond) is finite and strictly cheaper than the current trajectory.
+    Returns (X', U', J, J_old, index of the accepted step size or -1)."""
+    xg, u_ref, Q, R, Qf, w, wrap_idx = cost_args
+    T = int(T_star)
+    J_old = cost_true(X, U, xg, u_ref, Q, R, Qf, w, T, wrap_idx, extra_stage_cost)
+    N = len(U)
+    for ai, al in enumerate(alphas):
+        Un = U.copy()
+        Xn = np.zeros_like(X)
+        Xn[0] = X[0]
+        ok = True
+        for k in range(N):
+            if k < T:
+                dx = wrap_error((Xn[k] - X[k]).reshape(-1), wrap_idx)
+                Un[k] = U[k] + ((np.asarray(K[k]) @ dx).reshape(-1)
+                                + float(al) * np.asarray(kff[k]).reshape(-1))
+            Xn[k + 1] = np.asarray(F(Xn[k], Un[k]), dtype=float).reshape(-1)
+            if not np.all(np.isfinite(Xn[k + 1])):
+                ok = False
+                break
+        if not ok:
+            continue
+        J_new = cost_true(Xn, Un, xg, u_ref, Q, R, Qf, w, T, wrap_idx, extra_stage_cost)
+        if J_new < J_old:
+            return Xn, Un, J_new, J_old, ai
+    return X, U, J_old, J_old, -1

@@ -12,21 +12,25 @@ to stop early.
 
 The reference-shaped single-problem drop-ins (same names and arguments as
 solver.py) are ``rollout``, ``cost_timeopt_true``, ``forward_linesearch_fixedT``
-and ``ilqr_timeopt`` / ``ilqr_timeopt_ourmethod``.  F must be a
+and ``ilqr_timeopt`` / ``ilqr_timeopt_ourmethod``.  F is a
 :class:`time_opt_ilqr_amd.systems.DeviceDynamics` (the make_* makers of
-:mod:`time_opt_ilqr_amd.systems` return one), and ``extra_stage_cost`` may be
-None or the point-mass obstacle cost of those makers: arbitrary Python callables
-cannot run on the device.
+:mod:`time_opt_ilqr_amd.systems` return one: everything on the device) or any
+Python callable F(x, u) -> x_next, and ``extra_stage_cost`` None, the point-mass
+obstacle cost of those makers, or any callable (x, u) -> (c, cx, cxx).  A callable
+the device has no kernel for is evaluated on the host per problem (rollouts, FD
+linearisation, line search: host_dynamics.py, the reference's own call form) while
+the select, the Riccati pass and the accept / LM / stop step stay on the device.
 """
 from __future__ import annotations
 
 import time
 from dataclasses import dataclass
+from types import SimpleNamespace
 from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
 
-from . import _lib, engine
+from . import _lib, engine, host_dynamics
 from .utils import _sym, as_terminal_weight, chol_inv
 
 ALPHAS = engine.ALPHAS
@@ -67,10 +71,11 @@ def _obstacle_rows(extra_stage_cost):
 
 
 def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T_max: int, *,
-                       dt: float, U_init=None, max_iter: int = 15, lm_init: float = 1e-3,
+                       dt: float = 0.0, U_init=None, max_iter: int = 15, lm_init: float = 1e-3,
                        wrap_idx: Optional[Sequence[int]] = None, use_central_diff: bool = True,
                        obstacles=None, alphas=ALPHAS, device=None,
-                       stage_timers: bool = True, method: str = "propagator") -> Dict[str, Any]:
+                       stage_timers: bool = True, method: str = "propagator",
+                       extra_stage_cost=None) -> Dict[str, Any]:
     """Batched ilqr_timeopt(method="propagator" | "bruteforce") (solver.py:449-765).
 
     The select step is the LFT sweep of the augmented system (propagator) or the
@@ -83,13 +88,30 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     crashed, plus per-stage wall times in ``timers`` (the reference's timers dict;
     each stage is synchronised for it -- stage_timers=False skips those syncs and
     leaves the host waiting only on the once-per-iteration "all done" flag).
+
+    ``system`` is a device system (id, name or systems.DeviceDynamics, with ``dt``) or
+    a host_dynamics.HostDynamics wrapping a Python callable F(x, u): then the rollouts,
+    the FD linearisation and the line search evaluate F on the host per problem (the
+    reference's own call form, host_dynamics.py) and the select, Riccati and accept
+    steps stay on the device.  ``extra_stage_cost``: a Python callable (x, u) ->
+    (c, cx, cxx) evaluated on the host the same way (host systems only; the device
+    systems take the point-mass ``obstacles`` table).
     """
     torch = _torch()
     if method not in ("propagator", "bruteforce"):
         raise NotImplementedError(f"method={method!r}: the device outer loop implements "
                                   "'propagator' and 'bruteforce'")
-    sid = engine.system_id(system)
-    n, m = engine.system_dims(sid)
+    host = isinstance(system, host_dynamics.HostDynamics)
+    if host:
+        sid, n, m = None, int(system.n), int(system.m)
+        if obstacles is not None and len(obstacles) > 0:
+            raise ValueError("host dynamics: pass the stage cost as extra_stage_cost")
+    else:
+        if extra_stage_cost is not None:
+            raise ValueError("device dynamics take the point-mass obstacles table; a "
+                             "Python extra_stage_cost needs host dynamics")
+        sid = engine.system_id(system)
+        n, m = engine.system_dims(sid)
     dev = device or torch.device("cuda", torch.cuda.current_device())
     f64 = torch.float64
     tt = lambda a: torch.as_tensor(np.asarray(a, dtype=float) if not isinstance(  # noqa: E731
@@ -142,8 +164,19 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
             torch.cuda.synchronize(dev)
             timers[key] += time.perf_counter() - t0
 
+    if host:
+        if not all(t.dim() == d for t, d in ((xg_t, 1), (ur_t, 1), (Q_t, 2), (Qf_t, 2))):
+            raise ValueError("host dynamics: xg, u_ref, Q and Qf shared by the batch")
+        # the host line search's cost arguments (solver.py:65-102 with Qf expanded)
+        cost_np = (xg_t.cpu().numpy(), ur_t.cpu().numpy().reshape(-1), Q_t.cpu().numpy(),
+                   R_np, Qf_t.cpu().numpy(), float(w), wrap_idx)
     t0 = time.perf_counter()
-    X = engine.rollout(sid, x0, U, dt)
+    if host:
+        x0h = x0.reshape(-1, n).expand(Bn, n).cpu().numpy()
+        Uh = U.cpu().numpy()
+        X = tt(np.stack([host_dynamics.rollout(system, x0h[b], Uh[b]) for b in range(Bn)]))
+    else:
+        X = engine.rollout(sid, x0, U, dt)
     if stage_timers:
         torch.cuda.synchronize(dev)
         t_rollout = time.perf_counter() - t0
@@ -172,13 +205,27 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     def iterate(s, warm):
         """one update (solver.py:541-553 when warm, else 578-752) of the problems in s"""
         t0 = time.perf_counter()
-        lin = engine.linearize(sid, s.X, s.U, dt, central=use_central_diff)
+        if host:
+            Xh, Uh = s.X.cpu().numpy(), s.U.cpu().numpy()
+            parts = [host_dynamics.linearize(system, Xh[b], Uh[b], central=use_central_diff)
+                     for b in range(Xh.shape[0])]
+            lin = SimpleNamespace(A=tt(np.stack([q[0] for q in parts])),
+                                  B=tt(np.stack([q[1] for q in parts])),
+                                  a_res=tt(np.stack([q[2] for q in parts])))
+        else:
+            lin = engine.linearize(sid, s.X, s.U, dt, central=use_central_diff)
         clock("linearize", t0)
         t0 = time.perf_counter()
         ex = {}
         if obs is not None:
             c, cx, cxx = engine.obstacle_cost(s.X[:, :N], obs)
             ex = dict(qxx_extra=cxx, qx_extra=cx, c_extra=c)
+        elif host and extra_stage_cost is not None:
+            parts = [host_dynamics.stage_cost_terms(extra_stage_cost, Xh[b], Uh[b])
+                     for b in range(Xh.shape[0])]
+            ex = dict(qxx_extra=tt(np.stack([q[2] for q in parts])),
+                      qx_extra=tt(np.stack([q[1] for q in parts])),
+                      c_extra=tt(np.stack([q[0] for q in parts])))
         if method == "propagator":
             sel = engine.propagate_traj(lin.A, lin.B, lin.a_res, s.X, s.U, xg_t, ur_t, Q_t,
                                         R_inv, P, w_t, wrap_idx=wrap_idx, n_use=T_max,
@@ -197,17 +244,21 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         t0 = time.perf_counter()
         ric = engine.riccati(lin.A, lin.B, s.X, s.U, xg_t, ur_t, Q_t, R_t, Qf_t, T_star, s.lm,
                              mode=0, wrap_idx=wrap_idx, reg_max_tries=1,
-                             **({} if obs is None else dict(qxx_extra=ex["qxx_extra"],
-                                                            qx_extra=ex["qx_extra"],
-                                                            c_extra=ex["c_extra"])))
+                             **({} if not ex else dict(qxx_extra=ex["qxx_extra"],
+                                                       qx_extra=ex["qx_extra"],
+                                                       c_extra=ex["c_extra"])))
         clock("backward", t0)
         t0 = time.perf_counter()
         # the reference raises out of ilqr_timeopt at the select (FloatingPointError /
         # LinAlgError): such problems become crashed and done; the line search runs
         # the others whose Riccati pass succeeded (one launch for both masks)
         active = engine.ilqr_select_mask(s, sel_status, ric.status)
-        fw = engine.forward_linesearch(sid, s.X, s.U, T_star, ric.K, ric.k, cost, dt,
-                                       alphas=alphas, active=active)
+        if host:
+            fw = _host_linesearch(system, Xh, Uh, T_star, ric.K, ric.k, active, cost_np,
+                                  alphas, extra_stage_cost, tt)
+        else:
+            fw = engine.forward_linesearch(sid, s.X, s.U, T_star, ric.K, ric.k, cost, dt,
+                                           alphas=alphas, active=active)
         engine.ilqr_accept(s, fw.J, fw.accepted, T_star, warm=warm)
         if warm:
             # solver.py:548-553: X, U <- the line search's output, T_bar from the select
@@ -284,6 +335,26 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
                 t_rollout=t_rollout, J_curve=J_curve, select_status=torch.stack(status_log, 1))
 
 
+def _host_linesearch(system, Xh, Uh, T_star, K, k, active, cost_np, alphas, extra, tt):
+    """host_dynamics.linesearch per problem, in the device line search's result form
+    (accepted: the step-size index, -1 none, -2 inactive; inactive rows keep X, U)."""
+    torch = _torch()
+    T = T_star.cpu().numpy()
+    act = active.cpu().numpy()
+    Kh, kh = K.cpu().numpy(), k.cpu().numpy()
+    Xo, Uo = Xh.copy(), Uh.copy()
+    J = np.full(Xh.shape[0], np.nan)
+    J0 = np.full(Xh.shape[0], np.nan)
+    acc = np.full(Xh.shape[0], -2, dtype=np.int32)
+    for b in range(Xh.shape[0]):
+        if not act[b]:
+            continue
+        Xo[b], Uo[b], J[b], J0[b], acc[b] = host_dynamics.linesearch(
+            system, Xh[b], Uh[b], int(T[b]), Kh[b], kh[b], cost_np, alphas, extra)
+    return engine.LineSearchResult(tt(Xo), tt(Uo), tt(J), tt(J0),
+                                   torch.as_tensor(acc, device=T_star.device))
+
+
 # ---------------------------------------------------------------------------
 # reference-shaped single-problem drop-ins (solver.py names and arguments)
 # ---------------------------------------------------------------------------
@@ -294,6 +365,21 @@ def _dyn(F):
         raise TypeError("F must be a time_opt_ilqr_amd.systems.DeviceDynamics "
                         "(use the systems.make_* makers)")
     return F
+
+
+def _on_device(F) -> bool:
+    from .systems import DeviceDynamics
+    if isinstance(F, DeviceDynamics):
+        return True
+    if not callable(F):
+        raise TypeError("F must be a systems.DeviceDynamics or a callable F(x, u) -> x_next")
+    return False
+
+
+def _is_obstacle_cost(extra_stage_cost) -> bool:
+    from . import systems
+    return extra_stage_cost is None or extra_stage_cost is systems.obstacle_stage_cost or \
+        getattr(extra_stage_cost, "obstacles", None) is not None
 
 
 def _dev():
@@ -317,11 +403,13 @@ def _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost):
 
 
 def rollout(F, x0: np.ndarray, U: np.ndarray, *, max_state_norm: float = 1e6) -> np.ndarray:
-    """solver.py:42-62 (GPU)."""
-    F = _dyn(F)
+    """solver.py:42-62 (GPU; a Python callable F: on the host, host_dynamics.rollout)."""
     U = np.asarray(U, dtype=float)
     if U.ndim == 1:
         U = U.reshape(-1, 1)
+    if not _on_device(F):
+        return host_dynamics.rollout(F, x0, U, max_state_norm=max_state_norm)
+    F = _dyn(F)
     X = engine.rollout(F.system_id, _t(np.asarray(x0, dtype=float).reshape(-1)), _t(U)[None],
                        F.dt, max_state_norm=max_state_norm)
     return X[0].cpu().numpy()
@@ -340,6 +428,12 @@ def cost_timeopt_true(X, U, xg, u_ref, Q, R, alpha, w, T_star, wrap_idx=None,
         return float("inf")
     if T > len(U) or T + 1 > len(X):
         raise IndexError("index out of range")
+    if not _is_obstacle_cost(extra_stage_cost):  # a Python stage cost: on the host
+        return host_dynamics.cost_true(X, U, np.asarray(xg, dtype=float).reshape(-1),
+                                       np.atleast_1d(np.asarray(u_ref, dtype=float)).reshape(-1),
+                                       np.asarray(Q, dtype=float), np.atleast_2d(R),
+                                       as_terminal_weight(alpha, X.shape[1]), w, T, wrap_idx,
+                                       extra_stage_cost)
     sid = _system_for(system, X.shape[1], U.shape[1])
     cost = _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost)
     # the reference reads only X[:T+1] and U[:T] (solver.py:80-102)
@@ -358,8 +452,8 @@ def _system_for(system, n, m):
 
 def forward_linesearch_fixedT(F, X, U, xg, u_ref, Q, R, alpha, w, T_star, k_list, K_list, *,
                               alphas=ALPHAS, wrap_idx=None, extra_stage_cost=None):
-    """solver.py:233-286 (GPU) -> (X_new, U_new, J, accepted)."""
-    F = _dyn(F)
+    """solver.py:233-286 (GPU; a Python callable F or stage cost: on the host,
+    host_dynamics.linesearch) -> (X_new, U_new, J, accepted)."""
     X = np.asarray(X, dtype=float)
     U = np.asarray(U, dtype=float)
     if U.ndim == 1:
@@ -373,6 +467,15 @@ def forward_linesearch_fixedT(F, X, U, xg, u_ref, Q, R, alpha, w, T_star, k_list
     for i in range(max(T, 0)):
         K[i] = np.asarray(K_list[i], dtype=float).reshape(m, n)
         k[i] = np.asarray(k_list[i], dtype=float).reshape(-1)
+    if not _on_device(F) or not _is_obstacle_cost(extra_stage_cost):
+        cost_np = (np.asarray(xg, dtype=float).reshape(-1),
+                   np.atleast_1d(np.asarray(u_ref, dtype=float)).reshape(-1),
+                   np.asarray(Q, dtype=float), np.atleast_2d(R), as_terminal_weight(alpha, n),
+                   float(w), wrap_idx)
+        Xn, Un, J, _, acc = host_dynamics.linesearch(F, X, U, T, K, k, cost_np, alphas,
+                                                     extra_stage_cost)
+        return Xn, Un, float(J), acc >= 0
+    F = _dyn(F)
     cost = _cost_params(X, xg, u_ref, Q, R, alpha, w, wrap_idx, extra_stage_cost)
     r = engine.forward_linesearch(F.system_id, _t(X[:N + 1])[None], _t(U)[None], [T],
                                   _t(K)[None], _t(k)[None], cost, F.dt, alphas=alphas)
@@ -394,15 +497,21 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
         raise NotImplementedError("the device outer loop implements method='propagator' "
                                   "(the reference's 'ourmethod') and 'bruteforce' "
                                   "('baseline1')")
-    F = _dyn(F)
-    obs = _obstacle_rows(extra_stage_cost)
-    n = F.n
-    res = ilqr_timeopt_batch(F.system_id, np.asarray(x0, dtype=float).reshape(1, -1), xg, u_ref,
+    x0 = np.asarray(x0, dtype=float).reshape(1, -1)
+    n = x0.shape[1]
+    if _on_device(F) and _is_obstacle_cost(extra_stage_cost):
+        F = _dyn(F)
+        system, kw = F.system_id, dict(dt=F.dt, obstacles=_obstacle_rows(extra_stage_cost))
+    else:  # a Python callable (dynamics or stage cost): evaluated on the host per problem
+        m = np.atleast_2d(np.asarray(R, dtype=float)).shape[0]
+        system = host_dynamics.HostDynamics(F, n, m)
+        kw = dict(extra_stage_cost=extra_stage_cost)
+    res = ilqr_timeopt_batch(system, x0, xg, u_ref,
                              np.asarray(Q, dtype=float), np.atleast_2d(np.asarray(R, dtype=float)),
-                             as_terminal_weight(alpha, n), float(w), N, T_min, T_max, dt=F.dt,
+                             as_terminal_weight(alpha, n), float(w), N, T_min, T_max,
                              U_init=U_init, max_iter=max_iter, lm_init=lm_init,
                              wrap_idx=wrap_idx, use_central_diff=use_central_diff,
-                             obstacles=obs, device=_dev(), method=method)
+                             device=_dev(), method=method, **kw)
     if int(res["crashed"][0].item()):
         raise np.linalg.LinAlgError(
             ("propagator_all_Jt_aug" if method == "propagator" else
