@@ -856,18 +856,23 @@ def test_zero_step_is_rejected_like_the_reference(dev, golden_dir, tag):
     assert torch.equal(r.J, r.J_old)
 
 
+@pytest.mark.parametrize("vectorized", [False, True])
 @pytest.mark.parametrize("tag", TAGS)
-def test_ilqr_outer_loop_host_callables_vs_reference(dev, golden_dir, tag):
+def test_ilqr_outer_loop_host_callables_vs_reference(dev, golden_dir, tag, vectorized):
     """solver.ilqr_timeopt with the dynamics as a plain Python callable F(x, u) (the
     oracle's NumPy dynamics, the reference's bit for bit) and, for the point mass, the
     obstacle cost as a plain callable too: the host evaluates F and the stage cost per
     problem (host_dynamics.py) while the select, Riccati and accept steps run on the
-    device.  Same bars as the device-dynamics run above."""
+    device; ``vectorized``: F declared row-vectorised, so the linearisation is one call.
+    Same bars as the device-dynamics run above."""
     from time_opt_ilqr_amd import solver, systems
     d, sid, wrap, obs = _case(golden_dir, tag)
     mk = list(systems.MAKERS.values())[sid]
     Fd, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap_idx, extra = mk(N=int(d["N"]))
     F = dyn._scalar_F(sid, Fd.dt)
+    if vectorized:  # one F call per iteration for the whole FD linearisation
+        from time_opt_ilqr_amd.host_dynamics import HostDynamics
+        F = HostDynamics(F, len(x0), np.atleast_2d(R).shape[0], vectorized=True)
     cost = None
     if extra:
         cost = lambda x, u: io.obstacle_cost(x, obs)  # noqa: E731

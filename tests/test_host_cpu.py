@@ -1143,3 +1143,53 @@ def test_handover_horizon_of_small_cond_math_vs_oracle_first_nonfinite(small_hos
         assert small_host.small_host_triage_accepts(h - 1, h_poison, h_qt, N) == 0
         checked += 1
     assert checked > 150
+
+
+def test_lu_slot_registers_equal_per_column_solves(small_host):
+    """small_math.hpp's LU slot (lu_sym_solve_regs: one factorisation, the identity's
+    columns carried through the elimination, every index a constant so the arrays
+    stay in registers) against lu_pivot.hpp's per-column lu_sym_solve: bit for bit,
+    for blocks the jitter ladder cannot make positive definite (indefinite, a zero
+    leading entry that needs the row exchange); quad_inverse's one-column slot the same"""
+    inv = small_host.small_host_spd_inverse_s5_f64
+    inv.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+    quad = small_host.small_host_quad_inverse_s5_f64
+    quad.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+    quad.restype = C.c_double
+    col = small_host.small_host_lu_sym_solve_f64
+    col.argtypes = [C.c_void_p, C.c_int, C.c_double, C.c_void_p, C.c_void_p]
+    col.restype = C.c_int
+    rng = np.random.default_rng(11)
+    cases = []
+    for _ in range(40):
+        Qo, _ = np.linalg.qr(rng.standard_normal((5, 5)))
+        ev = rng.uniform(0.5, 3.0, 5)
+        ev[rng.integers(5)] = -rng.uniform(1.0, 5.0)       # beyond the ladder's 0.1
+        cases.append(Qo @ np.diag(ev) @ Qo.T)
+    Z = np.diag([0.0, 1.0, 1.0, 1.0, 1.0]) - 2.0 * np.eye(5)   # zero-pivot-free only with
+    Z[0, 1] = Z[1, 0] = 1.0                                    # the row exchange
+    Z[0, 0] = -0.1
+    cases.append(Z)
+    for M in cases:
+        M = np.ascontiguousarray(M)
+        out = np.zeros((5, 5))
+        st = C.c_uint(0)
+        inv(M.ctypes.data, 8, out.ctypes.data, C.byref(st))
+        assert st.value & 2, st.value  # the LU slot ran
+        eps = 1e-9 * 10.0 ** 8
+        ref = np.zeros((5, 5))
+        for c in range(5):
+            b = np.zeros(5)
+            b[c] = 1.0
+            x = np.zeros(5)
+            assert col(M.ctypes.data, 5, eps, b.ctypes.data, x.ctypes.data) == 0
+            ref[:, c] = x
+        iu = np.triu_indices(5)
+        assert np.array_equal(out[iu], ref[iu])
+        np_ref = np.linalg.solve(M + eps * np.eye(5), np.eye(5))
+        assert np.max(np.abs(out[iu] - np_ref[iu])) <= 1e-12 * np.max(np.abs(np_ref))
+        z = rng.standard_normal(5)
+        q = quad(M.ctypes.data, z.ctypes.data, 8, C.byref(st))
+        x = np.zeros(5)
+        assert col(M.ctypes.data, 5, eps, z.ctypes.data, x.ctypes.data) == 0
+        assert st.value & 2 and q == float(sum(z[i] * x[i] for i in range(5)))

@@ -165,3 +165,28 @@ def test_stage_cost_terms_and_host_dynamics_wrapper():
     # a callable returning the wrong size ends the rollout like a non-finite state
     X1 = hd.rollout(lambda x, u: np.zeros(3), X[0], U)
     assert np.isnan(X1[1:]).all() and _same(X1[0], X[0])
+
+
+@pytest.mark.parametrize("sid", range(5))
+@pytest.mark.parametrize("central", [False, True])
+def test_linearize_batch_vectorized_equals_per_call(sid, central):
+    """HostDynamics(vectorized=True): one F call over every perturbed point of every
+    step and problem gives the per-call quotients -- bit for bit where F's row results
+    do not depend on the stacking (every system but the quadrotor, whose stacked 3x3
+    matmuls may round differently from single ones: 1e-8 absolute on A, B as the
+    device linearisation's bar, the NaN pattern equal)"""
+    n, m = dyn.DIMS[sid]
+    F = dyn._scalar_F(sid, 0.05)
+    X = np.stack([_random_traj(sid, 9, 70 + b)[0] for b in range(3)])
+    U = np.stack([_random_traj(sid, 9, 70 + b)[1] for b in range(3)])
+    X[1, 3, 0] = np.nan
+    per = hd.linearize_batch(hd.HostDynamics(F, n, m), X, U, central=central)
+    vec = hd.linearize_batch(hd.HostDynamics(F, n, m, vectorized=True), X, U, central=central)
+    for g, r in zip(vec, per):
+        assert g.shape == r.shape
+        if sid == 2:
+            assert np.array_equal(np.isnan(g), np.isnan(r))
+            ok = np.isfinite(r)
+            assert np.all(np.abs(g[ok] - r[ok]) <= 1e-8)
+        else:
+            assert _same(g, r)

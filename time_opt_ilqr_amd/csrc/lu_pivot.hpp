@@ -83,6 +83,78 @@ HOP_HD inline bool lu_sym_solve(F at, int n, T eps, T (&x)[S]) {
   return ok;
 }
 
+// The same factorisation and solves with every index a compile-time constant (S is
+// the whole size), for the small-s kernels' per-lane LU slot: the row exchanges are
+// selects, so the arrays stay in registers.  A loop-indexed private array lives in
+// scratch: with the per-column lu_sym_solve (one factorisation per right-hand side)
+// the small-s rerun kernel spent ~60 us per step in scratch round trips on blocks
+// that reach the slot (the point-mass obstacle cost's indefinite Q_k, about half of
+// the inverses).  The right-hand sides ride along the elimination in the order the
+// forward substitution of lu_solve applies them, and the back substitution is
+// lu_solve's, so the values equal lu_sym_solve's bit for bit
+// (tests/test_host_cpu.py::test_lu_slot_registers_equal_per_column_solves).
+// rhs (S x R, row i = right-hand-side row i) <- (sym(M) + eps I)^-1 rhs; false when an
+// exactly zero pivot makes the block singular (gesv's LinAlgError)
+template <class T, int S, int R, class F>
+HOP_HD inline bool lu_sym_solve_regs(F at, T eps, T (&rhs)[S][R]) {
+  T a[S][S];
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) a[i][j] = T(0.5) * (at(i, j) + at(j, i)) + (i == j ? eps : T(0));
+  bool ok = true;
+#pragma unroll
+  for (int p = 0; p < S; ++p) {
+    int piv = p;
+    T big = a[p][p] < T(0) ? -a[p][p] : a[p][p];
+#pragma unroll
+    for (int i = p + 1; i < S; ++i) {
+      const T v = a[i][p] < T(0) ? -a[i][p] : a[i][p];
+      if (v > big) {
+        big = v;
+        piv = i;
+      }
+    }
+#pragma unroll
+    for (int i = p + 1; i < S; ++i) {
+      const bool sw = piv == i;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const T t = a[p][j];
+        a[p][j] = sw ? a[i][j] : t;
+        a[i][j] = sw ? t : a[i][j];
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const T t = rhs[p][j];
+        rhs[p][j] = sw ? rhs[i][j] : t;
+        rhs[i][j] = sw ? t : rhs[i][j];
+      }
+    }
+    const T d = a[p][p];
+    ok = ok && (d != T(0));
+#pragma unroll
+    for (int i = p + 1; i < S; ++i) {
+      const T l = a[i][p] / d;
+      a[i][p] = l;
+#pragma unroll
+      for (int j = p + 1; j < S; ++j) a[i][j] -= l * a[p][j];
+#pragma unroll
+      for (int j = 0; j < R; ++j) rhs[i][j] -= l * rhs[p][j];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < R; ++c)
+#pragma unroll
+    for (int i = S - 1; i >= 0; --i) {
+      T v = rhs[i][c];
+#pragma unroll
+      for (int j = i + 1; j < S; ++j) v -= a[i][j] * rhs[j][c];
+      rhs[i][c] = v / a[i][i];
+    }
+  return ok;
+}
+
 #ifdef __HIPCC__
 // The kernels' LU slot as an out-of-line call (a rare path: inlined, its private
 // arrays raised the register pressure of the sweep loops around it).

@@ -166,6 +166,29 @@ extern "C" int small_host_lu_sym_solve_f64(const double* A, int n, double eps, c
   return ok ? 0 : -1;
 }
 
+// the small-s kernels' chol_inv (small_math.hpp spd_inverse, the ladder and the LU
+// slot solved on registers) and quad_inverse at s = 5; st = the status bits
+extern "C" void small_host_spd_inverse_s5_f64(const double* M, int max_tries, double* out,
+                                              unsigned* st) {
+  hop::small::Sym<double, 5> m;
+  for (int i = 0; i < 5; ++i)
+    for (int j = i; j < 5; ++j) m.at(i, j) = 0.5 * (M[i * 5 + j] + M[j * 5 + i]);
+  *st = 0;
+  hop::small::spd_inverse(m, max_tries, *st);
+  for (int i = 0; i < 5; ++i)
+    for (int j = 0; j < 5; ++j) out[i * 5 + j] = m.at(i, j);
+}
+extern "C" double small_host_quad_inverse_s5_f64(const double* M, const double* z, int max_tries,
+                                                 unsigned* st) {
+  hop::small::Sym<double, 5> m;
+  for (int i = 0; i < 5; ++i)
+    for (int j = i; j < 5; ++j) m.at(i, j) = 0.5 * (M[i * 5 + j] + M[j * 5 + i]);
+  double zz[5];
+  for (int i = 0; i < 5; ++i) zz[i] = z[i];
+  *st = 0;
+  return hop::small::quad_inverse(m, zz, max_tries, *st);
+}
+
 // the hand-over word's field and the triage rule as include/hop.h defines them (the
 // kernels use the same macros; tests/test_host_cpu.py decodes statuses with these)
 extern "C" int small_host_handover_horizon(int32_t status) { return HOP_HANDOVER_HORIZON(status); }

@@ -115,15 +115,15 @@ HOP_HD inline void spd_inverse(Sym<T, S>& m, int max_tries, unsigned& st) {
       if (tries >= max_tries) {
         // the LU slot: np.linalg.solve(A + eps I, I), partial pivoting (lu_pivot.hpp)
         st |= kStLu;
-        T inv[S][S];
-        bool okl = true;
-        for (int c = 0; c < S; ++c) {
-          T x[S];
-          for (int i = 0; i < S; ++i) x[i] = i == c ? T(1) : T(0);
-          okl = okl && lu_sym_solve<T, S>([&](int i, int j) { return in.at(i, j); }, S, eps, x);
-          for (int i = 0; i < S; ++i) inv[i][c] = x[i];
-        }
+        T inv[S][S];  // the identity's columns, solved together (one factorisation)
+#pragma unroll
         for (int i = 0; i < S; ++i)
+#pragma unroll
+          for (int c = 0; c < S; ++c) inv[i][c] = i == c ? T(1) : T(0);
+        const bool okl = lu_sym_solve_regs<T, S, S>([&](int i, int j) { return in.at(i, j); }, eps, inv);
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
           for (int j = i; j < S; ++j) m.at(i, j) = okl ? -inv[i][j] : T(__builtin_nan(""));
         break;
       }
@@ -171,12 +171,14 @@ HOP_HD inline T quad_inverse(const Sym<T, S>& x0, const T (&z)[S], int max_tries
     }
     if (tries >= max_tries) {  // the LU slot: z^T solve(X + eps I, z), partial pivoting
       st |= kStLu;
-      T y[S];
-      for (int i = 0; i < S; ++i) y[i] = z[i];
-      if (!lu_sym_solve<T, S>([&](int i, int j) { return x0.at(i, j); }, S, eps, y))
+      T y[S][1];
+#pragma unroll
+      for (int i = 0; i < S; ++i) y[i][0] = z[i];
+      if (!lu_sym_solve_regs<T, S, 1>([&](int i, int j) { return x0.at(i, j); }, eps, y))
         return T(__builtin_nan(""));
       T q = T(0);
-      for (int i = 0; i < S; ++i) q += z[i] * y[i];
+#pragma unroll
+      for (int i = 0; i < S; ++i) q += z[i] * y[i][0];
       return q;
     }
     eps *= T(10);

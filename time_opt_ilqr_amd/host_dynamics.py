@@ -26,11 +26,17 @@ from .utils import wrap_error
 
 @dataclass
 class HostDynamics:
-    """A user dynamics callable ``F(x, u) -> x_next`` with its state / control sizes."""
+    """A user dynamics callable ``F(x, u) -> x_next`` with its state / control sizes.
+
+    ``vectorized=True`` declares that F maps stacked rows ``x [K, n], u [K, m]`` to
+    ``[K, n]`` row by row (NumPy broadcasting over the leading axis): the FD
+    linearisation then evaluates every perturbed point of every step and problem in one
+    call (``linearize_batch``), with the same quotients as the per-call form."""
     F: Callable
     n: int
     m: int
     name: str = "host"
+    vectorized: bool = False
 
     def __call__(self, x, u):
         return np.asarray(self.F(x, u), dtype=float).reshape(-1)
@@ -107,6 +113,60 @@ def _linearize(F, X, U, central, epsx, epsu, relx, relu):
                 e[j] = h
                 Bm[k, :, j] = (np.asarray(F(x, u + e), dtype=float).reshape(-1) - f0) / h
     return A, Bm, a
+
+
+def linearize_batch(system, X, U, *, central: bool = True, epsx: float = 1e-5,
+                    epsu: float = 1e-5, relx: float = 1e-6, relu: float = 1e-6):
+    """A batch of problems (X [B, N+1, n], U [B, N, m]): A [B, N, n, n], B [B, N, n, m],
+    a [B, N, n].  One call of F over all perturbed points when the system is declared
+    ``vectorized``, else ``linearize`` per problem."""
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float)
+    if not getattr(system, "vectorized", False):
+        parts = [linearize(system, X[b], U[b], central=central, epsx=epsx, epsu=epsu,
+                           relx=relx, relu=relu) for b in range(X.shape[0])]
+        return tuple(np.stack([q[i] for q in parts]) for i in range(3))
+    with np.errstate(all="ignore"):
+        return _linearize_vec(system.F, X, U, central, epsx, epsu, relx, relu)
+
+
+def _linearize_vec(F, X, U, central, epsx, epsu, relx, relu):
+    Bn, N, m = U.shape
+    n = X.shape[-1]
+    x, u = X[:, :N], U
+    # h = max(eps, rel * max(1, |v|)) with Python's max: a NaN |v| gives max(1, NaN) = 1
+    hx = np.fmax(float(epsx), float(relx) * np.fmax(1.0, np.abs(x)))
+    hu = np.fmax(float(epsu), float(relu) * np.fmax(1.0, np.abs(u)))
+    P = 1 + (2 if central else 1) * (n + m)   # points per step: f0, then the perturbations
+    xs = np.repeat(x[:, :, None, :], P, axis=2)
+    us = np.repeat(u[:, :, None, :], P, axis=2)
+    i, j = np.arange(n), np.arange(m)
+    if central:   # x_i + h, x_i - h, u_j + h, u_j - h: the perturbed component alone
+        xs[:, :, 1 + i, i] += hx
+        xs[:, :, 1 + n + i, i] -= hx
+        us[:, :, 1 + 2 * n + j, j] += hu
+        us[:, :, 1 + 2 * n + m + j, j] -= hu
+    else:         # x + h e_i, u + h e_j (the per-call form adds the whole vector)
+        Ex = np.zeros((Bn, N, n, n))
+        Ex[:, :, i, i] = hx
+        Eu = np.zeros((Bn, N, m, m))
+        Eu[:, :, j, j] = hu
+        xs[:, :, 1:1 + n] = x[:, :, None, :] + Ex
+        us[:, :, 1 + n:1 + n + m] = u[:, :, None, :] + Eu
+    fx = np.asarray(F(xs.reshape(-1, n), us.reshape(-1, m)), dtype=float).reshape(Bn, N, P, n)
+    f0 = fx[:, :, 0]
+    if central:
+        A = (fx[:, :, 1:1 + n] - fx[:, :, 1 + n:1 + 2 * n]) / (2.0 * hx)[..., None]
+        Bm = (fx[:, :, 1 + 2 * n:1 + 2 * n + m] - fx[:, :, 1 + 2 * n + m:]) / (2.0 * hu)[..., None]
+    else:
+        A = (fx[:, :, 1:1 + n] - f0[:, :, None]) / hx[..., None]
+        Bm = (fx[:, :, 1 + n:] - f0[:, :, None]) / hu[..., None]
+    A, Bm = A.swapaxes(-1, -2).copy(), Bm.swapaxes(-1, -2).copy()
+    if not central:  # the forward form marks the whole step when F(x_k, u_k) is not finite
+        bad = ~np.isfinite(f0).all(-1)
+        A[bad] = np.nan
+        Bm[bad] = np.nan
+    return A, Bm, f0 - X[:, 1:N + 1]
 
 
 def stage_cost_terms(extra_stage_cost, X, U):

@@ -207,11 +207,8 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
         t0 = time.perf_counter()
         if host:
             Xh, Uh = s.X.cpu().numpy(), s.U.cpu().numpy()
-            parts = [host_dynamics.linearize(system, Xh[b], Uh[b], central=use_central_diff)
-                     for b in range(Xh.shape[0])]
-            lin = SimpleNamespace(A=tt(np.stack([q[0] for q in parts])),
-                                  B=tt(np.stack([q[1] for q in parts])),
-                                  a_res=tt(np.stack([q[2] for q in parts])))
+            A, Bm, a_res = host_dynamics.linearize_batch(system, Xh, Uh, central=use_central_diff)
+            lin = SimpleNamespace(A=tt(A), B=tt(Bm), a_res=tt(a_res))
         else:
             lin = engine.linearize(sid, s.X, s.U, dt, central=use_central_diff)
         clock("linearize", t0)
@@ -504,7 +501,8 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
         system, kw = F.system_id, dict(dt=F.dt, obstacles=_obstacle_rows(extra_stage_cost))
     else:  # a Python callable (dynamics or stage cost): evaluated on the host per problem
         m = np.atleast_2d(np.asarray(R, dtype=float)).shape[0]
-        system = host_dynamics.HostDynamics(F, n, m)
+        system = F if isinstance(F, host_dynamics.HostDynamics) else \
+            host_dynamics.HostDynamics(F, n, m)
         kw = dict(extra_stage_cost=extra_stage_cost)
     res = ilqr_timeopt_batch(system, x0, xg, u_ref,
                              np.asarray(Q, dtype=float), np.atleast_2d(np.asarray(R, dtype=float)),
