@@ -80,6 +80,10 @@ const char* hop_last_error(void);
  *                           the lane-per-problem kernel (lft_small.hip) instead of
  *                           the row-group kernel (lft_sweep_v2.hip SchedCondSmall):
  *                           the A/B and cross-check of the two
+ *   HOP_OPT_RERUN_LANE      the fp64 s <= 5 rerun launch recomputes every hand-over
+ *                           on its own lane (the one-lane LFT kernel) instead of the
+ *                           pipelined rerun (lft_small.hip lft_small_rerun_kernel):
+ *                           the A/B and bitwise cross-check of the two
  * `variant` selects an A/B schedule; only developer builds (HOP_DEV_BUILD=1 at
  * build time, hop_build_flags() & 1) compile them -- product builds return
  * HOP_E_ARG for variant != 0 or HOP_OPT_STAMPS.
@@ -91,6 +95,7 @@ const char* hop_last_error(void);
 #define HOP_OPT_STAMPS 16u
 #define HOP_OPT_NO_RERUN 32u
 #define HOP_OPT_SMALL_LANE 64u
+#define HOP_OPT_RERUN_LANE 128u
 #define HOP_ST_HANDOVER 16 /* status bit, set only under HOP_OPT_NO_RERUN */
 /*
  * The hand-over word: the status a conditioned-prefix kernel leaves for a problem

@@ -131,3 +131,63 @@ def test_rowgroup_genuine_escalation_real_cartpole(dev, golden_dir):
     oth[b] = False
     assert torch.equal(d.J[oth], d0.J[oth]) and torch.equal(d.status[oth], d0.status[oth])
     assert torch.equal(d.t_star[oth], d0.t_star[oth])
+
+
+@pytest.mark.parametrize("s,m", [(5, 2), (5, 1), (4, 2), (3, 1), (2, 1)])
+@pytest.mark.parametrize("N", [1, 63, 64, 65, 150])
+def test_pipelined_small_rerun_bitwise(dev, s, m, N):
+    """The fp64 s <= 5 rerun launch's pipeline (lft_small.hip lft_small_rerun_kernel:
+    stage blocks, compose chain and queries on three waves in beats of 64 steps)
+    against the one-lane LFT kernel (HOP_OPT_RERUN_LANE) and the reference association
+    alone: J, status, T*, J* bitwise.  Hand-overs are chol_inv LU slots (Q_k = -I) at
+    one, two and four problems of a workgroup (the pipeline) and at five (more than
+    kSmallPipeMax: the one-lane body); beats are cut at N = 1, 63, 64, 65, 150."""
+    import torch
+    from time_opt_ilqr_amd import _lib, engine
+    Bn = 600
+    A, Bm, Q, R, Ri, z0, QT = orc.synth_lft_batch(8100 + 7 * s + m, Bn, s, m, N)
+    Q = Q.copy()
+    # problems per workgroup: 192 (s = 5, three waves) or 256 (four)
+    ppb = 192 if s == 5 else 256
+    bad = [3] + [ppb + 10, ppb + 70] + [2 * ppb + i for i in (0, 1, 63, 64)]
+    if 3 * ppb + 5 < Bn:
+        bad += [3 * ppb + i for i in (5, 6, 7, 8, 9)]
+    for j, b in enumerate(bad):
+        Q[b, (7 * j) % N] = -np.eye(s)  # chol_inv's ladder ends in the LU slot
+    args = [_t(x, dev) for x in (A, Bm, Q, Ri, z0[0], QT)]
+    t_min = max(1, N // 3)
+    d = engine.propagate(*args, t_min=t_min, t_max=N)
+    with _lib.options(rerun_lane=True):
+        ln = engine.propagate(*args, t_min=t_min, t_max=N)
+    with _lib.options(reference_assoc=True):
+        r = engine.propagate(*args, t_min=t_min, t_max=N)
+    torch.cuda.synchronize()
+    st = d.status.cpu().numpy()
+    assert all(int(st[b]) & orc.ST_LU for b in bad), st[bad]
+    for o in (ln, r):
+        for b in bad:
+            assert torch.equal(d.J[b].nan_to_num(7.0), o.J[b].nan_to_num(7.0)), b
+        assert torch.equal(d.status[bad], o.status[bad])
+        assert torch.equal(d.t_star[bad], o.t_star[bad])
+        assert torch.equal(d.j_star[bad].nan_to_num(7.0), o.j_star[bad].nan_to_num(7.0))
+    # the problems nobody handed over keep the conditioned kernel's values
+    ok = np.ones(Bn, dtype=bool)
+    ok[bad] = False
+    okt = torch.as_tensor(ok, device=d.J.device)
+    assert torch.equal(d.J[okt], ln.J[okt]) and int(d.status[okt].abs().sum()) == 0
+
+
+def test_pipelined_small_rerun_point_mass_outer_loop(dev):
+    """The point-mass obstacle run (every select hands its problem over: the obstacle
+    Hessian makes Q_k indefinite) through the pipelined rerun and through the
+    one-lane rerun: identical T_hist and J_hist, bit for bit"""
+    from time_opt_ilqr_amd import _lib, solver, systems
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, extra = \
+        systems.make_point_mass_obstacles() if hasattr(systems, "make_point_mass_obstacles") \
+        else list(systems.MAKERS.values())[3]()
+    kw = dict(max_iter=15, wrap_idx=wrap_idx, extra_stage_cost=extra["extra_stage_cost"])
+    a = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, **kw)
+    with _lib.options(rerun_lane=True):
+        b = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, **kw)
+    assert a["T_hist"] == b["T_hist"] and a["J_hist"] == b["J_hist"]
+    assert np.array_equal(a["J_curve"], b["J_curve"], equal_nan=True)

@@ -158,6 +158,7 @@ OPT_TRAJ_UNFUSED = 8
 OPT_STAMPS = 16
 OPT_NO_RERUN = 32
 OPT_SMALL_LANE = 64
+OPT_RERUN_LANE = 128
 ST_HANDOVER = 16  # status bit left by the conditioned kernels under OPT_NO_RERUN
 # the hand-over word (include/hop.h): ST_HANDOVER | first flagged horizon << HANDOVER_SHIFT
 HANDOVER_SHIFT = 13
@@ -177,7 +178,7 @@ def dev_build() -> bool:
 @contextlib.contextmanager
 def options(*, force_generic=None, force_handover=None, reference_assoc=None,
             traj_unfused=None, stamps=None, no_rerun=None, small_lane=None,
-            variant=None):
+            rerun_lane=None, variant=None):
     """Set hop_set_options for the duration of a `with` block (tests, tools).
     Arguments left at None keep the enclosing block's setting; the previous
     controls are restored afterwards.  The library keeps them per host thread
@@ -189,7 +190,8 @@ def options(*, force_generic=None, force_handover=None, reference_assoc=None,
     flags, var = prev
     for on, bit in ((force_generic, OPT_FORCE_GENERIC), (force_handover, OPT_FORCE_HANDOVER),
                     (reference_assoc, OPT_REFERENCE_ASSOC), (traj_unfused, OPT_TRAJ_UNFUSED),
-                    (stamps, OPT_STAMPS), (no_rerun, OPT_NO_RERUN), (small_lane, OPT_SMALL_LANE)):
+                    (stamps, OPT_STAMPS), (no_rerun, OPT_NO_RERUN), (small_lane, OPT_SMALL_LANE),
+                    (rerun_lane, OPT_RERUN_LANE)):
         if on is not None:
             flags = (flags | bit) if on else (flags & ~bit)
     if variant is not None:

@@ -359,7 +359,7 @@ extern "C" {
 int hop_set_options(uint32_t flags, int32_t variant) {
   if (flags & ~(HOP_OPT_FORCE_GENERIC | HOP_OPT_FORCE_HANDOVER | HOP_OPT_REFERENCE_ASSOC |
                 HOP_OPT_TRAJ_UNFUSED | HOP_OPT_STAMPS | HOP_OPT_NO_RERUN |
-                HOP_OPT_SMALL_LANE))
+                HOP_OPT_SMALL_LANE | HOP_OPT_RERUN_LANE))
     return fail(HOP_E_ARG, "unknown option flag");
   if (!hop::kDevBuild && (variant != 0 || (flags & HOP_OPT_STAMPS)))
     return fail(HOP_E_ARG, "A/B schedules and stamps exist only in developer builds "

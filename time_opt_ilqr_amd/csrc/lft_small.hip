@@ -188,7 +188,7 @@ __device__ __forceinline__ void read_block(const unsigned char* wimg, int slot, 
 // 64 scattered 16-B chunks); only with PW = 64
 // LY 2 (timing experiment): the tiled HBM layout [B/64][nalloc][block elements][64]
 template <class T, int S, int MM, bool COND = false, int PW = 64, int EXP = 0, int LY = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 1 : 2))) void lft_small_kernel(LftArgs<T> a) {
+__device__ __forceinline__ void lft_small_body(const LftArgs<T>& a) {
   using G = Geo<T, S, MM, PW>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int tid = threadIdx.x, lane = tid & 63, slot = lane & (PW - 1);
@@ -390,6 +390,241 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
         a.t_star[prob] = ps.tbest;
         a.j_star[prob] = ps.best;
       }
+    }
+  }
+}
+
+template <class T, int S, int MM, bool COND = false, int PW = 64, int EXP = 0, int LY = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 1 : 2))) void lft_small_kernel(LftArgs<T> a) {
+  lft_small_body<T, S, MM, COND, PW, EXP, LY>(a);
+}
+
+// ---------------------------------------------------------------------------
+// The pipelined rerun for s <= 5 (fp64 augmented blocks).  The
+// rerun launch used to recompute every hand-over on its own lane from k = 0: the
+// whole step on one lane, ~12 us per step when the blocks reach chol_inv's ladder
+// (the point-mass obstacle cost: every select hands over).  Only the prefix compose
+// is loop-carried (horizon_selection.py:66-75); the stage blocks (:57-64) and the
+// queries (:77-85) of different steps are independent.  So one workgroup takes one
+// handed-over problem at a time, in beats of 64 steps:
+//   wave 0: the stage blocks E_k, F_k, G_k of beat b, one step per lane;
+//   wave 1: the compose chain of beat b - 1 on lane 0 (W_k and the prefix update);
+//   wave 2: the queries of beat b - 2, one horizon per lane, then the argmin in
+//           horizon order on lane 0.
+// The blocks pass through two LDS rings of two beats.  Every value comes from the
+// same small_math.hpp functions on the same inputs as in lft_small_kernel, so J, the
+// status word and T* / J* are bitwise the one-lane kernel's (HOP_OPT_RERUN_LANE runs
+// that instead; tests/test_gpu_small_rowgroup.py).  A workgroup with more than
+// kSmallPipeMax hand-overs runs the one-lane body on all of them (64 lanes in
+// parallel beat a sequence of pipelines there).
+constexpr int kSmallPipeMax = 4;
+template <class T, int S, int MM>
+struct PipeSmallGeo {
+  static constexpr int NP = S * (S + 1) / 2, SS = S * S;
+  static constexpr int STG = NP + SS + NP;  // E / Ebar, F / Fbar, G / Gbar of one step
+  static constexpr int BS = 64;             // steps per beat (a wave's lanes)
+  static constexpr int RING = 2 * BS * STG; // elements per ring (two beats)
+  static constexpr int OFF_C = RING, OFF_J = 2 * RING;  // chain ring, the beat's J values
+  static constexpr int BYTES = (2 * RING + BS) * (int)sizeof(T) + 16;  // + the status word
+};
+
+template <class T, int S>
+__device__ __forceinline__ void put_step(T* o, const Sym<T, S>& e, const Gen<T, S>& f,
+                                         const Sym<T, S>& g) {
+  constexpr int NP = Sym<T, S>::NP;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) o[i] = e.v[i];
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) o[NP + i * S + j] = f.a[i][j];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) o[NP + S * S + i] = g.v[i];
+}
+template <class T, int S>
+__device__ __forceinline__ void get_step(const T* in, Sym<T, S>& e, Gen<T, S>& f, Sym<T, S>& g) {
+  constexpr int NP = Sym<T, S>::NP;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) e.v[i] = in[i];
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+#pragma unroll
+    for (int j = 0; j < S; ++j) f.a[i][j] = in[NP + i * S + j];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) g.v[i] = in[NP + S * S + i];
+}
+
+template <class T, int S, int MM>
+__device__ __forceinline__ void pipe_small_problem(const LftArgs<T>& a, long long p, int w, int lane,
+                                                   T* ring, unsigned* st_all) {
+  using PG = PipeSmallGeo<T, S, MM>;
+  constexpr int SS = S * S, BS = PG::BS, STG = PG::STG;
+  const int N = a.n, mt = a.max_tries;
+  const long long pstrM = (long long)a.nalloc * SS, pstrB = (long long)a.nalloc * S * MM;
+  if (threadIdx.x == 0) *st_all = 0u;
+  __syncthreads();
+  unsigned st = 0;
+  T rinv[MM][MM];
+  if (w == 0) {  // R^-1 as the one-lane kernel forms it (its status bits included)
+    const T* Rp = a.R + p * a.r_bstride;
+    Gen<T, MM> r;
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+      for (int j = 0; j < MM; ++j) r.a[i][j] = Rp[i * MM + j];
+    Sym<T, MM> rs;
+    sym_of(rs, r);
+    if (!a.r_is_inv) spd_inverse(rs, mt, st);
+#pragma unroll
+    for (int i = 0; i < MM; ++i)
+#pragma unroll
+      for (int j = 0; j < MM; ++j) rinv[i][j] = a.r_is_inv ? r.a[i][j] : rs.at(i, j);
+  }
+  T z[S];
+  if (w == 2) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) z[i] = a.z0[p * a.z_bstride + i];
+  }
+  State<T, S, MM> ch;  // wave 1, lane 0: the prefix
+  ch.st = 0;
+  State<T, S, MM> am;  // wave 2, lane 0: the argmin (take)
+  am.st = 0;
+  am.best = T(0);
+  am.tbest = 0;
+  T* jb = ring + PG::OFF_J;
+  const int nb = (N + BS - 1) / BS;
+#pragma unroll 1
+  for (int beat = 0; beat < nb + 2; ++beat) {
+    if (w == 0) {
+      const int k = beat * BS + lane;
+      if (beat < nb && k < N) {
+        Gen<T, S> Q, A;
+        T Bk[S][MM];
+        const T* q = a.Q + p * pstrM + (long long)k * SS;
+        const T* ap = a.A + p * pstrM + (long long)k * SS;
+        const T* bp = a.B + p * pstrB + (long long)k * S * MM;
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+          for (int j = 0; j < S; ++j) {
+            Q.a[i][j] = q[i * S + j];
+            A.a[i][j] = ap[i * S + j];
+          }
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+#pragma unroll
+          for (int j = 0; j < MM; ++j) Bk[i][j] = bp[i * MM + j];
+        Sym<T, S> E, G;
+        Gen<T, S> F;
+        stage_blocks<T, S, MM>(Q, A, Bk, rinv, mt, st, E, F, G);
+        put_step<T, S>(ring + ((beat & 1) * BS + lane) * STG, E, F, G);
+      }
+    } else if (w == 1) {
+      const int b1 = beat - 1;
+      if (lane == 0 && b1 >= 0 && b1 < nb) {
+#pragma unroll 1
+        for (int j = 0; j < BS; ++j) {
+          const int k = b1 * BS + j;
+          if (k >= N) break;
+          Sym<T, S> E, G;
+          Gen<T, S> F;
+          get_step<T, S>(ring + ((b1 & 1) * BS + j) * STG, E, F, G);
+          compose_step<T, S, MM>(ch, k, E, F, G, mt);
+          put_step<T, S>(ring + PG::OFF_C + ((b1 & 1) * BS + j) * STG, ch.Eb, ch.Fb, ch.Gb);
+        }
+      }
+    } else if (w == 2) {
+      const int b2 = beat - 2;
+      if (b2 >= 0) {  // (b2 < nb: the loop ends at nb + 2)
+        const int k = b2 * BS + lane;
+        if (k < N) {
+          State<T, S, MM> s;
+          s.st = 0;
+          get_step<T, S>(ring + PG::OFF_C + ((b2 & 1) * BS + lane) * STG, s.Eb, s.Fb, s.Gb);
+          Gen<T, S> QT;
+          const T* qt = a.QT + p * pstrM + (long long)k * SS;
+#pragma unroll
+          for (int i = 0; i < S; ++i)
+#pragma unroll
+            for (int j = 0; j < S; ++j) QT.a[i][j] = qt[i * S + j];
+          const T jk = query<T, S, MM>(s, QT, z, mt);
+          st |= s.st;
+          a.J[p * N + k] = jk;
+          jb[lane] = jk;
+        }
+        wave_sync();
+        if (lane == 0) {
+#pragma unroll 1
+          for (int j = 0; j < BS; ++j) {
+            const int kk = b2 * BS + j;
+            if (kk >= N) break;
+            take(am, kk + 1, jb[j], a.t_min, a.t_max);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (w == 1 && lane == 0) st |= ch.st;
+  if (w == 2 && lane == 0) st |= am.st;
+  if (st != 0u) atomicOr(st_all, st);
+  __syncthreads();
+  if (w == 2 && lane == 0) {
+    a.status[p] = (int)*st_all;
+    if (a.t_max > 0 && a.t_star != nullptr) {
+      a.t_star[p] = am.tbest;
+      a.j_star[p] = am.best;
+    }
+  }
+  __syncthreads();  // the next problem reuses the rings and the status word
+}
+
+// The rerun launch after the conditioned small-s kernels (a.cond bit 0): the
+// workgroup's hand-overs (status 16) by the pipeline when there are at most
+// kSmallPipeMax of them, else by the one-lane body
+template <class T, int S, int MM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void lft_small_rerun_kernel(LftArgs<T> a) {
+  using G = Geo<T, S, MM>;
+  using PG = PipeSmallGeo<T, S, MM>;
+  static_assert(G::WPB >= 3, "the pipeline needs three waves per workgroup");
+  static_assert(PG::BYTES <= G::WAVE_BYTES * G::WPB, "the rings must fit the LFT kernel's LDS");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  if (!(a.cond & 1)) {  // not a rerun (HOP_OPT_REFERENCE_ASSOC): every problem, one per lane
+    lft_small_body<T, S, MM, false, 64, 0, 1>(a);
+    return;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const long long prob = (long long)blockIdx.x * G::PPB + w * 64 + lane;
+  const bool need = prob < a.batch && (a.status[prob] & 16);
+  unsigned long long* masks = reinterpret_cast<unsigned long long*>(smem_raw);
+  const unsigned long long bal = __ballot(need);
+  if (lane == 0) masks[w] = bal;
+  __syncthreads();
+  unsigned long long mk[G::WPB];
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < G::WPB; ++i) {
+    mk[i] = masks[i];
+    cnt += __popcll(mk[i]);
+  }
+  if (cnt == 0) return;  // workgroup-uniform
+  if (cnt > kSmallPipeMax) {
+    lft_small_body<T, S, MM, false, 64, 0, 1>(a);
+    return;
+  }
+  __syncthreads();  // the masks live where the rings go
+  T* ring = reinterpret_cast<T*>(smem_raw);
+  unsigned* st_all = reinterpret_cast<unsigned*>(smem_raw + (2 * PG::RING + PG::BS) * sizeof(T));
+#pragma unroll 1
+  for (int i = 0; i < G::WPB; ++i) {
+    unsigned long long m = mk[i];
+#pragma unroll 1
+    while (m != 0ull) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1ull;
+      pipe_small_problem<T, S, MM>(a, (long long)blockIdx.x * G::PPB + i * 64 + l, w, lane, ring,
+                                   st_all);
     }
   }
 }
@@ -692,6 +927,17 @@ constexpr LaunchGeo geo_of() {
   return {G::WAVE_BYTES * G::WPB, G::PPB, G::TPB};
 }
 
+// the rerun launch's kernel for batch-major blocks: the pipelined rerun for fp64
+// (HOP_OPT_RERUN_LANE: the one-lane LFT kernel, its comparator), the one-lane LFT
+// kernel for fp32 (whose conditioned association runs on the lane kernel too)
+template <class T, int S, int MM>
+auto rerun_kernel() {
+  if constexpr (sizeof(T) == 8) {
+    if (!opt(HOP_OPT_RERUN_LANE)) return &lft_small_rerun_kernel<T, S, MM>;
+  }
+  return &lft_small_kernel<T, S, MM, false, 64, 0, 1>;
+}
+
 }  // namespace small
 
 // small-s path: returns hipErrorNotSupported when the shape has no instantiation
@@ -784,7 +1030,7 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
                  small::lft_small_kernel<T, S_, M_, false, 32>,                           \
                  small::geo_of<small::Geo<T, S_, M_, 32>>()); \
     return go2(small::lft_small_kernel<T, S_, M_, true, 64, 0, 1>,                        \
-               small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,                       \
+               small::rerun_kernel<T, S_, M_>(),                                          \
                small::geo_of<small::Geo<T, S_, M_>>());                                   \
   }
 #else
@@ -824,7 +1070,7 @@ hipError_t dispatch_lft_small(const LftArgs<T>& a, hipStream_t stream) {
                              small::lft_small_kernel<T, S_, M_, false, 64, 0, 2>,         \
                              small::geo_of<small::Geo<T, S_, M_>>())                      \
                     : gocond(small::lft_small_kernel<T, S_, M_, true, 64, 0, 1>,          \
-                             small::lft_small_kernel<T, S_, M_, false, 64, 0, 1>,         \
+                             small::rerun_kernel<T, S_, M_>(),                            \
                              small::geo_of<small::Geo<T, S_, M_>>());                     \
   }
 #endif

@@ -262,17 +262,15 @@ struct State {
   unsigned st;
 };
 
-// stage + compose for step k (Q, A, B of step k given); returns nothing
+// the stage blocks of step k (horizon_selection.py:57-64): E = chol_inv(Q_k),
+// F = E A^T, G = _sym(A F + B R^-1 B^T); independent of every other step
 template <class T, int S, int MM>
-HOP_HD inline void stage_compose(State<T, S, MM>& s, int k, const Gen<T, S>& Q,
-                                 const Gen<T, S>& A, const T (&Bk)[S][MM],
-                                 const T (&rinv)[MM][MM], int mt) {
-  Sym<T, S> E;
+HOP_HD inline void stage_blocks(const Gen<T, S>& Q, const Gen<T, S>& A, const T (&Bk)[S][MM],
+                                const T (&rinv)[MM][MM], int mt, unsigned& st, Sym<T, S>& E,
+                                Gen<T, S>& F, Sym<T, S>& G) {
   sym_of(E, Q);
-  spd_inverse(E, mt, s.st);                 // E = chol_inv(Q)
-  Gen<T, S> F;
+  spd_inverse(E, mt, st);                   // E = chol_inv(Q)
   mul_sym_gt(F, E, A);                      // F = E A^T
-  Sym<T, S> G;                              // G = _sym(A F + B R^-1 B^T)
 #pragma unroll
   for (int i = 0; i < Sym<T, S>::NP; ++i) G.v[i] = T(0);
   acc_sym_xy<false>(G, A, F);
@@ -294,6 +292,13 @@ HOP_HD inline void stage_compose(State<T, S, MM>& s, int k, const Gen<T, S>& Q,
       G.at(i, j) += v;
     }
   }
+}
+
+// the prefix compose with step k's stage blocks (horizon_selection.py:66-75): the
+// only loop-carried part of the sweep
+template <class T, int S, int MM>
+HOP_HD inline void compose_step(State<T, S, MM>& s, int k, const Sym<T, S>& E, const Gen<T, S>& F,
+                                const Sym<T, S>& G, int mt) {
   if (k == 0) {
     s.Eb = E;
     s.Fb = F;
@@ -313,6 +318,17 @@ HOP_HD inline void stage_compose(State<T, S, MM>& s, int k, const Gen<T, S>& Q,
   s.Fb = Fn;
   s.Gb = G;
   acc_sym_xty<true>(s.Gb, F, Z);            // Gbar = _sym(G - F^T W F)
+}
+
+// stage + compose for step k (Q, A, B of step k given); returns nothing
+template <class T, int S, int MM>
+HOP_HD inline void stage_compose(State<T, S, MM>& s, int k, const Gen<T, S>& Q,
+                                 const Gen<T, S>& A, const T (&Bk)[S][MM],
+                                 const T (&rinv)[MM][MM], int mt) {
+  Sym<T, S> E, G;
+  Gen<T, S> F;
+  stage_blocks<T, S, MM>(Q, A, Bk, rinv, mt, s.st, E, F, G);
+  compose_step<T, S, MM>(s, k, E, F, G, mt);
 }
 
 // query horizon k+1 from QT_k; returns J
