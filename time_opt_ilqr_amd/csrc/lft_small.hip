@@ -408,7 +408,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
 // queries (:77-85) of different steps are independent.  So one workgroup takes one
 // handed-over problem at a time, in beats of 64 steps:
 //   wave 0: the stage blocks E_k, F_k, G_k of beat b, one step per lane;
-//   wave 1: the compose chain of beat b - 1 on lane 0 (W_k and the prefix update);
+//   wave 1: the compose chain of beat b - 1 (W_k and the prefix update), the same
+//           values on every lane, W_k's jitter-ladder attempts side by side
+//           (spd_inverse_lanes);
 //   wave 2: the queries of beat b - 2, one horizon per lane, then the argmin in
 //           horizon order on lane 0.
 // The blocks pass through two LDS rings of two beats.  Every value comes from the
@@ -452,6 +454,69 @@ __device__ __forceinline__ void get_step(const T* in, Sym<T, S>& e, Gen<T, S>& f
     for (int j = 0; j < S; ++j) f.a[i][j] = in[NP + i * S + j];
 #pragma unroll
   for (int i = 0; i < NP; ++i) g.v[i] = in[NP + S * S + i];
+}
+
+// spd_inverse (small_math.hpp: chol_inv's jitter ladder, then the LU slot) with the
+// ladder's attempts side by side: lane t sweeps sym(M) + eps_t I, eps_t the ladder's
+// t-th jitter (the same repeated x10 from 1e-9, lanes past max_tries repeat the last),
+// and the first attempt that factors is broadcast, or the LU slot runs at the last
+// jitter when none does.  Each attempt is the same sweep on the same values as in
+// the sequential ladder, so the result and the status bits are bitwise its own; the
+// chain wave of the pipelined rerun calls it on all 64 lanes with the same input.
+template <class T, int S>
+__device__ __forceinline__ T bcast_lane(T v, int src) {
+  if constexpr (sizeof(T) == 8) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, src);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), src);
+    return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
+  } else {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(unsigned, v), src));
+  }
+}
+template <class T, int S>
+__device__ __forceinline__ void spd_inverse_lanes(Sym<T, S>& m, int max_tries, unsigned& st, int lane) {
+  if (max_tries >= 63) {  // more attempts than lanes: the sequential ladder
+    spd_inverse(m, max_tries, st);
+    return;
+  }
+  const Sym<T, S> in = m;
+  const int t = lane < max_tries ? lane : max_tries;
+  T eps = T(1e-9);
+#pragma unroll 1
+  for (int i = 0; i < t; ++i) eps *= T(10);
+  Sym<T, S> x = in;
+  const bool ok = sweep_neg_inverse(x, eps);
+  const unsigned long long okm = __ballot(ok);
+  if (!(okm & 1ull)) {
+    if (!all_finite(in)) {  // chol_inv's _assert_finite: no ladder (spd_inverse)
+      st |= kStNonfinite;
+#pragma unroll
+      for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = T(__builtin_nan(""));
+      return;
+    }
+    st |= kStJitter;
+  }
+  if (okm != 0ull) {
+    const int first = __builtin_amdgcn_readfirstlane(__ffsll((long long)okm) - 1);
+#pragma unroll
+    for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = bcast_lane<T, S>(x.v[k], first);
+  } else {  // the LU slot at the last jitter (every lane, the same values)
+    st |= kStLu;
+    const T e = bcast_lane<T, S>(eps, max_tries);
+    T inv[S][S];
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+#pragma unroll
+      for (int c = 0; c < S; ++c) inv[i][c] = i == c ? T(1) : T(0);
+    const bool okl = lu_sym_solve_regs<T, S, S>([&](int i, int j) { return in.at(i, j); }, e, inv);
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+#pragma unroll
+      for (int j = i; j < S; ++j) m.at(i, j) = okl ? -inv[i][j] : T(__builtin_nan(""));
+  }
+#pragma unroll
+  for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = -m.v[k];
 }
 
 template <class T, int S, int MM>
@@ -521,7 +586,7 @@ __device__ __forceinline__ void pipe_small_problem(const LftArgs<T>& a, long lon
       }
     } else if (w == 1) {
       const int b1 = beat - 1;
-      if (lane == 0 && b1 >= 0 && b1 < nb) {
+      if (b1 >= 0 && b1 < nb) {  // every lane carries the same prefix
 #pragma unroll 1
         for (int j = 0; j < BS; ++j) {
           const int k = b1 * BS + j;
@@ -529,8 +594,11 @@ __device__ __forceinline__ void pipe_small_problem(const LftArgs<T>& a, long lon
           Sym<T, S> E, G;
           Gen<T, S> F;
           get_step<T, S>(ring + ((b1 & 1) * BS + j) * STG, E, F, G);
-          compose_step<T, S, MM>(ch, k, E, F, G, mt);
-          put_step<T, S>(ring + PG::OFF_C + ((b1 & 1) * BS + j) * STG, ch.Eb, ch.Fb, ch.Gb);
+          compose_step<T, S, MM>(ch, k, E, F, G, mt, [&](Sym<T, S>& x, int t, unsigned& s_) {
+            spd_inverse_lanes<T, S>(x, t, s_, lane);
+          });
+          if (lane == 0)
+            put_step<T, S>(ring + PG::OFF_C + ((b1 & 1) * BS + j) * STG, ch.Eb, ch.Fb, ch.Gb);
         }
       }
     } else if (w == 2) {

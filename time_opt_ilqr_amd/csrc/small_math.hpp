@@ -296,9 +296,11 @@ HOP_HD inline void stage_blocks(const Gen<T, S>& Q, const Gen<T, S>& A, const T 
 
 // the prefix compose with step k's stage blocks (horizon_selection.py:66-75): the
 // only loop-carried part of the sweep
-template <class T, int S, int MM>
+// (inv: the chol_inv of W = E_k + Gbar, spd_inverse's semantics; the pipelined rerun
+// passes one that runs the jitter ladder's attempts on separate lanes)
+template <class T, int S, int MM, class Inv>
 HOP_HD inline void compose_step(State<T, S, MM>& s, int k, const Sym<T, S>& E, const Gen<T, S>& F,
-                                const Sym<T, S>& G, int mt) {
+                                const Sym<T, S>& G, int mt, Inv&& inv) {
   if (k == 0) {
     s.Eb = E;
     s.Fb = F;
@@ -308,7 +310,7 @@ HOP_HD inline void compose_step(State<T, S, MM>& s, int k, const Sym<T, S>& E, c
   Sym<T, S> W;
 #pragma unroll
   for (int i = 0; i < Sym<T, S>::NP; ++i) W.v[i] = E.v[i] + s.Gb.v[i];
-  spd_inverse(W, mt, s.st);                 // W = (E_k + Gbar)^-1
+  inv(W, mt, s.st);                         // W = (E_k + Gbar)^-1
   Gen<T, S> Z;
   mul_sym_gt(Z, W, s.Fb);                   // W Fbar^T
   acc_sym_xy<true>(s.Eb, s.Fb, Z);          // Ebar = _sym(Ebar - Fbar W Fbar^T)
@@ -318,6 +320,12 @@ HOP_HD inline void compose_step(State<T, S, MM>& s, int k, const Sym<T, S>& E, c
   s.Fb = Fn;
   s.Gb = G;
   acc_sym_xty<true>(s.Gb, F, Z);            // Gbar = _sym(G - F^T W F)
+}
+template <class T, int S, int MM>
+HOP_HD inline void compose_step(State<T, S, MM>& s, int k, const Sym<T, S>& E, const Gen<T, S>& F,
+                                const Sym<T, S>& G, int mt) {
+  compose_step<T, S, MM>(s, k, E, F, G, mt,
+                         [](Sym<T, S>& x, int t, unsigned& st) { spd_inverse(x, t, st); });
 }
 
 // stage + compose for step k (Q, A, B of step k given); returns nothing
