@@ -884,3 +884,42 @@ def test_ilqr_outer_loop_host_callables_vs_reference(dev, golden_dir, tag, vecto
     assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= tol
     assert sol["T_star"] == int(d["T_star"])
     assert _rel(np.nan_to_num(sol["X"]), np.nan_to_num(d["X"])) <= 100 * tol
+
+
+@pytest.mark.parametrize("vectorized", [False, True])
+@pytest.mark.parametrize("tag", ["di", "pointmass"])
+def test_ilqr_batch_host_callables_vs_oracle(dev, tag, vectorized):
+    """ilqr_timeopt_batch with a Python-callable system (host_dynamics.HostDynamics: the
+    host rolls out, linearises and line-searches every problem, the device selects,
+    runs the Riccati pass and accepts): a batch with different x0 -- double integrator,
+    and the point mass with its obstacle cost as a plain callable (every select hands
+    over: the pipelined s <= 5 rerun on two problems) -- per-problem T_hist / J_hist /
+    T* equal to the oracle's scalar runs"""
+    from time_opt_ilqr_amd import host_dynamics, solver, systems
+    sid = dyn.SYSTEMS[tag]
+    mk = list(systems.MAKERS.values())[sid]
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, extra = \
+        mk(N=50) if tag == "di" else mk()
+    T_max = min(T_max, N)
+    n, m = dyn.DIMS[sid]
+    rng = np.random.default_rng(2)
+    Bn = 5 if tag == "di" else 2
+    X0 = x0 + rng.uniform(-1.5 if tag == "di" else -0.05, 1.5 if tag == "di" else 0.05, (Bn, n))
+    Qf = np.asarray(io.orc.terminal_weight(alpha, n))
+    obs, cost = None, None
+    if extra:
+        obs = np.array([[o[0], o[1], r, wt] for o, r, wt in systems.OBSTACLES])
+        cost = lambda x, u: io.obstacle_cost(x, obs)  # noqa: E731
+    iters = 12 if tag == "di" else 6
+    sysh = host_dynamics.HostDynamics(dyn._scalar_F(sid, F.dt), n, m, vectorized=vectorized)
+    res = solver.ilqr_timeopt_batch(sysh, X0, xg, u_ref, Q, np.atleast_2d(R), Qf, w, N, T_min,
+                                    T_max, max_iter=iters, wrap_idx=wrap_idx,
+                                    use_central_diff=tag != "di", extra_stage_cost=cost)
+    nh = _np(res["n_hist"])
+    for b in range(Bn):
+        o = io.ilqr_timeopt(sid, F.dt, X0[b], xg, u_ref, Q, np.atleast_2d(R), Qf, w, N, T_min,
+                            T_max, max_iter=iters, wrap_idx=wrap_idx, central=tag != "di",
+                            obstacles=obs)
+        assert _np(res["T_hist"][b, :nh[b]]).tolist() == o["T_hist"]
+        assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9
+        assert int(res["T_star"][b]) == o["T_star"]

@@ -190,3 +190,67 @@ def test_linearize_batch_vectorized_equals_per_call(sid, central):
             assert np.all(np.abs(g[ok] - r[ok]) <= 1e-8)
         else:
             assert _same(g, r)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_rollout_batch_vectorized_vs_per_call(golden_dir, tag):
+    """rollout_batch: every problem a time step at a time (one F call per step) against
+    rollout per problem: the divergence cut at the same step, the states equal (bit for
+    bit but for the quadrotor's stacked 3 x 3 matmuls: 1e-13 relative)"""
+    d = np.load(os.path.join(golden_dir, f"ilqr_{tag}.npz"))
+    sid, dt, N = dyn.SYSTEMS[tag], float(d["dt"]), int(d["N"])
+    n, m = dyn.DIMS[sid]
+    F = dyn._scalar_F(sid, dt)
+    X0 = np.stack([d["x0"], d["x0"], d["x0"] + 0.1])
+    U = np.stack([d["U_big"], np.tile(d["u_ref"].reshape(1, -1), (N, 1)), d["U"]])
+    per = hd.rollout_batch(hd.HostDynamics(F, n, m), X0, U, max_state_norm=1e3)
+    vec = hd.rollout_batch(hd.HostDynamics(F, n, m, vectorized=True), X0, U, max_state_norm=1e3)
+    assert np.array_equal(np.isnan(per), np.isnan(vec))
+    assert np.array_equal(np.isnan(per[0]), np.isnan(d["X_big"]))
+    if sid == 2:
+        assert _rel(np.nan_to_num(vec), np.nan_to_num(per)) <= 1e-13
+    else:
+        assert _same(vec, per)
+
+
+@pytest.mark.parametrize("tag", ["quadrotor", "pointmass", "cartpole"])
+def test_linesearch_batch_vectorized_vs_per_call(golden_dir, tag):
+    """linesearch_batch: all (problem, step size) rollouts together against the per-call
+    line search per problem, on a batch built from a captured call with the feed-forward
+    scaled per problem (several accepted step sizes, rejections, NaN guards on the
+    quadrotor), one inactive problem, T* = 0 and short horizons: the same accepted index
+    everywhere, J / X' / U' equal to rounding (1e-12)"""
+    d = np.load(os.path.join(golden_dir, f"ilqr_{tag}.npz"))
+    sid, dt, N = dyn.SYSTEMS[tag], float(d["dt"]), int(d["N"])
+    n, m = dyn.DIMS[sid]
+    g = lambda k: d[f"f1_{k}"]  # noqa: E731
+    T0 = int(g("T_star"))
+    F = dyn._scalar_F(sid, dt)
+    _, extra = _obs(tag)
+    wrap = [int(i) for i in d["wrap_idx"]]
+    args = (d["xg"], d["u_ref"], d["Q"], d["R"], d["Qf"], float(d["w"]), wrap)
+    sc = np.array([1, 3, 10, 30, 100, 300, -1, -10, 0.3])
+    Bn = 14
+    X = np.stack([g("X")] * Bn)
+    U = np.stack([g("U")] * Bn)
+    K = np.zeros((Bn, N, m, n))
+    k = np.zeros((Bn, N, m))
+    K[:, :T0] = g("K")
+    k[:, :T0] = g("k").reshape(T0, m)[None] * sc[np.arange(Bn) % len(sc), None, None]
+    T = np.full(Bn, T0)
+    T[9:13] = [0, 1, 5, T0 // 2]
+    active = np.ones(Bn, dtype=bool)
+    active[4] = False
+    per = hd.linesearch_batch(hd.HostDynamics(F, n, m), X, U, T, K, k, active, args, io.ALPHAS,
+                              extra)
+    vec = hd.linesearch_batch(hd.HostDynamics(F, n, m, vectorized=True), X, U, T, K, k, active,
+                              args, io.ALPHAS, extra)
+    assert np.array_equal(per[4], vec[4]) and per[4][4] == -2
+    for b in range(Bn):
+        if not active[b]:
+            assert _same(vec[0][b], X[b]) and np.isnan(vec[2][b])
+            continue
+        Jp, Jv = per[2][b], vec[2][b]
+        assert Jp == Jv or abs(Jp - Jv) <= 1e-12 * abs(Jp) or (np.isinf(Jp) and np.isinf(Jv))
+        assert _rel(vec[0][b], per[0][b]) <= 1e-12 and _rel(vec[1][b], per[1][b]) <= 1e-12
+    assert len(set(per[4].tolist())) >= 3

@@ -21,7 +21,7 @@ from typing import Callable, Optional, Sequence
 
 import numpy as np
 
-from .utils import wrap_error
+from .utils import angle_normalize, wrap_error
 
 
 @dataclass
@@ -31,7 +31,9 @@ class HostDynamics:
     ``vectorized=True`` declares that F maps stacked rows ``x [K, n], u [K, m]`` to
     ``[K, n]`` row by row (NumPy broadcasting over the leading axis): the FD
     linearisation then evaluates every perturbed point of every step and problem in one
-    call (``linearize_batch``), with the same quotients as the per-call form."""
+    call (``linearize_batch``), with the same quotients as the per-call form, and the
+    rollouts of a batch (``rollout_batch``) and of every (problem, step size) pair of a
+    line search (``linesearch_batch``) advance together, one call per time step."""
     F: Callable
     n: int
     m: int
@@ -50,11 +52,37 @@ def rollout(F, x0, U, *, max_state_norm: float = 1e6) -> np.ndarray:
     N, n = U.shape[0], x0.size
     X = np.full((N + 1, n), np.nan)
     X[0] = x0
-    for k in range(N):
-        xn = np.asarray(F(X[k], U[k]), dtype=float).reshape(-1)
-        if xn.size != n or not np.all(np.isfinite(xn)) or float(np.linalg.norm(xn)) > max_state_norm:
-            break
-        X[k + 1] = xn
+    with np.errstate(all="ignore"):  # a diverging rollout ends at its first bad state
+        for k in range(N):
+            xn = np.asarray(F(X[k], U[k]), dtype=float).reshape(-1)
+            if xn.size != n or not np.all(np.isfinite(xn)) or \
+                    float(np.linalg.norm(xn)) > max_state_norm:
+                break
+            X[k + 1] = xn
+    return X
+
+
+def rollout_batch(system, X0, U, *, max_state_norm: float = 1e6) -> np.ndarray:
+    """A batch (X0 [B, n], U [B, N, m]): X [B, N+1, n], ``rollout`` per problem, or all
+    problems a step at a time when the system is declared ``vectorized``."""
+    X0 = np.asarray(X0, dtype=float)
+    U = np.asarray(U, dtype=float)
+    if not getattr(system, "vectorized", False):
+        return np.stack([rollout(system, X0[b], U[b], max_state_norm=max_state_norm)
+                         for b in range(X0.shape[0])])
+    Bn, N = U.shape[:2]
+    n = X0.shape[1]
+    X = np.full((Bn, N + 1, n), np.nan)
+    X[:, 0] = X0
+    live = np.arange(Bn)
+    with np.errstate(all="ignore"):
+        for k in range(N):
+            if live.size == 0:
+                break
+            xn = np.asarray(system.F(X[live, k], U[live, k]), dtype=float).reshape(live.size, n)
+            ok = np.isfinite(xn).all(1) & (np.linalg.norm(xn, axis=1) <= max_state_norm)
+            X[live[ok], k + 1] = xn[ok]
+            live = live[ok]
     return X
 
 
@@ -208,6 +236,84 @@ def cost_true(X, U, xg, u_ref, Q, R, Qf, w, T_star: int, wrap_idx: Optional[Sequ
     if not np.all(np.isfinite(eT)):
         return float("inf")
     return float(c + 0.5 * float(eT @ (Qf @ eT)))
+
+
+def _wrap_rows(e, wrap_idx):
+    """wrap_error on every row of e [R, n] (the same angle_normalize per component)."""
+    if not wrap_idx:
+        return e
+    e = e.copy()
+    for i in wrap_idx:
+        e[:, i] = angle_normalize(e[:, i])
+    return e
+
+
+def linesearch_batch(system, X, U, T_star, K, kff, active, cost_args, alphas,
+                     extra_stage_cost=None):
+    """A batch of line searches (X [B, N+1, n], U [B, N, m], T_star [B], K [B, N, m, n],
+    kff [B, N, m], active [B]): (X', U', J, J_old, accepted) with accepted = the step-size
+    index, -1 when none is accepted, -2 for inactive problems (their X, U kept, J NaN).
+    Per problem ``linesearch``; for a ``vectorized`` system (and four or more active
+    problems) the step sizes are tried in
+    rounds, each round rolling out every problem still without an accepted step size
+    together (one F call per time step), so each problem gets the first step size the
+    per-call form accepts (the K dx products are stacked matmuls: the same values to
+    rounding)."""
+    X = np.asarray(X, dtype=float)
+    U = np.asarray(U, dtype=float)
+    T = np.asarray(T_star).astype(np.int64).reshape(-1)
+    act = np.asarray(active).reshape(-1).astype(bool)
+    Bn = X.shape[0]
+    Xo, Uo = X.copy(), U.copy()
+    J = np.full(Bn, np.nan)
+    J0 = np.full(Bn, np.nan)
+    acc = np.full(Bn, -2, dtype=np.int32)
+    # a handful of problems: the per-call loop (stacking rows costs more than it saves)
+    if not getattr(system, "vectorized", False) or int(act.sum()) < 4:
+        for b in np.nonzero(act)[0]:
+            Xo[b], Uo[b], J[b], J0[b], acc[b] = linesearch(system, X[b], U[b], int(T[b]), K[b],
+                                                           kff[b], cost_args, alphas,
+                                                           extra_stage_cost)
+        return Xo, Uo, J, J0, acc
+    xg, u_ref, Q, R, Qf, w, wrap_idx = cost_args
+    bs = np.nonzero(act)[0]
+    N, n = U.shape[1], X.shape[2]
+    Kf = np.asarray(K, dtype=float)
+    kf = np.asarray(kff, dtype=float).reshape(Bn, N, -1)
+    for b in bs:
+        J0[b] = cost_true(X[b], U[b], xg, u_ref, Q, R, Qf, w, int(T[b]), wrap_idx, extra_stage_cost)
+        J[b], acc[b] = J0[b], -1
+    pending = bs
+    for ai, al in enumerate(alphas):  # one round per step size, over the problems still open
+        if pending.size == 0:
+            break
+        Xn = np.zeros((pending.size, N + 1, n))
+        Xn[:, 0] = X[pending, 0]
+        Un = U[pending].copy()
+        ok = np.ones(pending.size, dtype=bool)
+        with np.errstate(all="ignore"):
+            for k in range(N):
+                on = k < T[pending]
+                if on.any():
+                    r = np.nonzero(on)[0]
+                    pr = pending[r]
+                    dx = _wrap_rows(Xn[r, k] - X[pr, k], wrap_idx)
+                    Un[r, k] = U[pr, k] + ((Kf[pr, k] @ dx[:, :, None])[:, :, 0]
+                                           + float(al) * kf[pr, k])
+                xn = np.asarray(system.F(Xn[:, k], Un[:, k]), dtype=float).reshape(pending.size, n)
+                Xn[:, k + 1] = xn
+                ok &= np.isfinite(xn).all(1)
+        still = []
+        for i, b in enumerate(pending):
+            if ok[i]:
+                Jn = cost_true(Xn[i], Un[i], xg, u_ref, Q, R, Qf, w, int(T[b]), wrap_idx,
+                               extra_stage_cost)
+                if Jn < J0[b]:
+                    Xo[b], Uo[b], J[b], acc[b] = Xn[i], Un[i], Jn, ai
+                    continue
+            still.append(b)
+        pending = np.asarray(still, dtype=np.int64)
+    return Xo, Uo, J, J0, acc
 
 
 def linesearch(F, X, U, T_star: int, K, kff, cost_args, alphas, extra_stage_cost=None):

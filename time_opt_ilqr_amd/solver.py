@@ -174,7 +174,7 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
     if host:
         x0h = x0.reshape(-1, n).expand(Bn, n).cpu().numpy()
         Uh = U.cpu().numpy()
-        X = tt(np.stack([host_dynamics.rollout(system, x0h[b], Uh[b]) for b in range(Bn)]))
+        X = tt(host_dynamics.rollout_batch(system, x0h, Uh))
     else:
         X = engine.rollout(sid, x0, U, dt)
     if stage_timers:
@@ -333,21 +333,12 @@ def ilqr_timeopt_batch(system, x0, xg, u_ref, Q, R, Qf, w, N: int, T_min: int, T
 
 
 def _host_linesearch(system, Xh, Uh, T_star, K, k, active, cost_np, alphas, extra, tt):
-    """host_dynamics.linesearch per problem, in the device line search's result form
+    """host_dynamics.linesearch_batch in the device line search's result form
     (accepted: the step-size index, -1 none, -2 inactive; inactive rows keep X, U)."""
     torch = _torch()
-    T = T_star.cpu().numpy()
-    act = active.cpu().numpy()
-    Kh, kh = K.cpu().numpy(), k.cpu().numpy()
-    Xo, Uo = Xh.copy(), Uh.copy()
-    J = np.full(Xh.shape[0], np.nan)
-    J0 = np.full(Xh.shape[0], np.nan)
-    acc = np.full(Xh.shape[0], -2, dtype=np.int32)
-    for b in range(Xh.shape[0]):
-        if not act[b]:
-            continue
-        Xo[b], Uo[b], J[b], J0[b], acc[b] = host_dynamics.linesearch(
-            system, Xh[b], Uh[b], int(T[b]), Kh[b], kh[b], cost_np, alphas, extra)
+    Xo, Uo, J, J0, acc = host_dynamics.linesearch_batch(
+        system, Xh, Uh, T_star.cpu().numpy(), K.cpu().numpy(), k.cpu().numpy(),
+        active.cpu().numpy(), cost_np, alphas, extra)
     return engine.LineSearchResult(tt(Xo), tt(Uo), tt(J), tt(J0),
                                    torch.as_tensor(acc, device=T_star.device))
 

@@ -35,6 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--systems", default="di,cartpole,quadrotor,pointmass,segway")
     ap.add_argument("--repeat", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="batch of the row-vectorised run")
     a = ap.parse_args()
     for tag in a.systems.split(","):
         sid = dyn.SYSTEMS[tag]
@@ -64,6 +65,26 @@ def main():
                               device_dynamics_s=round(t_dev, 4), host_callable_s=round(t_host, 4),
                               host_vectorized_s=round(t_vec, 4),
                               oracle_1core_s=round(t_orc, 4))), flush=True)
+
+    # a batch of quadrotor problems (x0 jittered by 1e-3): the device dynamics against the
+    # row-vectorised callable through ilqr_timeopt_batch
+    import torch
+    Fd, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, _ = systems.make_quadrotor()
+    X0 = x0 + 1e-3 * np.random.default_rng(0).standard_normal((a.batch, len(x0)))
+    Qf = np.asarray(as_terminal_weight(alpha, len(x0)))
+    Fv = host_dynamics.HostDynamics(dyn._scalar_F(2, Fd.dt), 12, 4, vectorized=True)
+    out = {}
+    for name, sysx, kw in (("device_dynamics_s", 2, dict(dt=Fd.dt)), ("host_vectorized_s", Fv, {})):
+        best = float("inf")
+        for _ in range(2):
+            t0 = time.perf_counter()
+            r = solver.ilqr_timeopt_batch(sysx, X0, xg, u_ref, Q, np.atleast_2d(R), Qf, w, N, T_min,
+                                          T_max, max_iter=15, wrap_idx=wrap_idx, **kw)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        out[name] = round(best, 4)
+        out[name.replace("_s", "_T_star")] = np.asarray(r["T_star"].cpu()).tolist()[:4]
+    print(json.dumps(dict(system="quadrotor", batch=a.batch, **out)), flush=True)
 
 
 if __name__ == "__main__":
