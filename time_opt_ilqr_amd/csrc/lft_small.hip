@@ -460,7 +460,7 @@ __device__ __forceinline__ void get_step(const T* in, Sym<T, S>& e, Gen<T, S>& f
 // ladder's attempts side by side: lane t sweeps sym(M) + eps_t I, eps_t the ladder's
 // t-th jitter (the same repeated x10 from 1e-9, lanes past max_tries repeat the last),
 // and the first attempt that factors is broadcast, or the LU slot runs at the last
-// jitter when none does.  Each attempt is the same sweep on the same values as in
+// jitter when none does, lane c solving the identity's column c.  Each attempt is the same sweep on the same values as in
 // the sequential ladder, so the result and the status bits are bitwise its own; the
 // chain wave of the pipelined rerun calls it on all 64 lanes with the same input.
 template <class T, int S>
@@ -501,19 +501,19 @@ __device__ __forceinline__ void spd_inverse_lanes(Sym<T, S>& m, int max_tries, u
     const int first = __builtin_amdgcn_readfirstlane(__ffsll((long long)okm) - 1);
 #pragma unroll
     for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = bcast_lane<T, S>(x.v[k], first);
-  } else {  // the LU slot at the last jitter (every lane, the same values)
-    st |= kStLu;
-    const T e = bcast_lane<T, S>(eps, max_tries);
-    T inv[S][S];
+  } else {  // the LU slot at the last jitter: lane c solves the identity's column c
+    st |= kStLu;  // (the same factorisation on every lane; a column's operations do not
+    const T e = bcast_lane<T, S>(eps, max_tries);  // depend on the other columns)
+    const int col = lane < S ? lane : S - 1;
+    T x[S][1];
+#pragma unroll
+    for (int i = 0; i < S; ++i) x[i][0] = i == col ? T(1) : T(0);
+    const bool okl = lu_sym_solve_regs<T, S, 1>([&](int i, int j) { return in.at(i, j); }, e, x);
 #pragma unroll
     for (int i = 0; i < S; ++i)
 #pragma unroll
-      for (int c = 0; c < S; ++c) inv[i][c] = i == c ? T(1) : T(0);
-    const bool okl = lu_sym_solve_regs<T, S, S>([&](int i, int j) { return in.at(i, j); }, e, inv);
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-#pragma unroll
-      for (int j = i; j < S; ++j) m.at(i, j) = okl ? -inv[i][j] : T(__builtin_nan(""));
+      for (int j = i; j < S; ++j)
+        m.at(i, j) = okl ? -bcast_lane<T, S>(x[i][0], j) : T(__builtin_nan(""));
   }
 #pragma unroll
   for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = -m.v[k];
