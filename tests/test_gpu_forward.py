@@ -923,3 +923,24 @@ def test_ilqr_batch_host_callables_vs_oracle(dev, tag, vectorized):
         assert _np(res["T_hist"][b, :nh[b]]).tolist() == o["T_hist"]
         assert _rel(_np(res["J_hist"][b, :nh[b]]), o["J_hist"]) <= 1e-9
         assert int(res["T_star"][b]) == o["T_star"]
+
+
+@pytest.mark.parametrize("tag", ["di", "segway", "pointmass"])
+def test_ilqr_bruteforce_outer_loop_host_callables_vs_reference(dev, golden_dir, tag):
+    """method="bruteforce" (baseline1) with the dynamics as a plain Python callable and,
+    for the point mass, the obstacle cost as a plain callable: the host evaluates them
+    (host_dynamics.py), the device runs the brute-force J curve, the Riccati pass and the
+    accept step; the reference's run reproduced to the device-dynamics test's bars"""
+    from time_opt_ilqr_amd import solver, systems
+    d, sid, wrap, obs = _bf_case(golden_dir, tag)
+    mk = list(systems.MAKERS.values())[sid]
+    Fd, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap_idx, extra = mk(N=int(d["N"]))
+    cost = (lambda x, u: io.obstacle_cost(x, obs)) if extra else None  # noqa: E731
+    sol = solver.ilqr_timeopt_baseline1(
+        dyn._scalar_F(sid, Fd.dt), x0, xg, u_ref, Q, R, alpha, w, int(d["N"]), int(d["T_min"]),
+        int(d["T_max"]), max_iter=int(d["max_iter"]), wrap_idx=wrap_idx,
+        use_central_diff=bool(d["central"]), extra_stage_cost=cost)
+    assert sol["T_hist"] == [int(t) for t in d["T_hist"]]
+    assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= 1e-9
+    assert sol["T_star"] == int(d["T_star"])
+    assert np.max(np.abs(sol["J_curve"] - d["J_curve"]) / np.abs(d["J_curve"])) <= 1e-8
