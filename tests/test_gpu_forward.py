@@ -944,3 +944,26 @@ def test_ilqr_bruteforce_outer_loop_host_callables_vs_reference(dev, golden_dir,
     assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= 1e-9
     assert sol["T_star"] == int(d["T_star"])
     assert np.max(np.abs(sol["J_curve"] - d["J_curve"]) / np.abs(d["J_curve"])) <= 1e-8
+
+
+@pytest.mark.parametrize("tag", ["pointmass", "quadrotor"])
+def test_ilqr_device_dynamics_python_cost_vs_reference(dev, golden_dir, tag):
+    """a built-in system's DeviceDynamics with a Python stage cost (the obstacle cost as
+    a plain callable for the point mass; a zero callable cost for the quadrotor): the
+    host takes the cost and F's rows run on the device kernel in one launch per
+    evaluation round (solver._device_rows); the reference's run reproduced"""
+    from time_opt_ilqr_amd import solver, systems
+    d, sid, wrap, obs = _case(golden_dir, tag)
+    mk = list(systems.MAKERS.values())[sid]
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap_idx, extra = mk(N=int(d["N"]))
+    n = len(x0)
+    if extra:
+        cost = lambda x, u: io.obstacle_cost(x, obs)  # noqa: E731
+    else:
+        cost = lambda x, u: (0.0, np.zeros(n), np.zeros((n, n)))  # noqa: E731
+    sol = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, int(d["N"]), int(d["T_min"]),
+                              int(d["T_max"]), max_iter=int(d["max_iter"]), wrap_idx=wrap_idx,
+                              use_central_diff=bool(d["central"]), extra_stage_cost=cost)
+    assert sol["T_hist"] == [int(t) for t in d["T_hist"]]
+    assert _rel(np.array(sol["J_hist"]), d["J_hist"]) <= 1e-9
+    assert sol["T_star"] == int(d["T_star"])

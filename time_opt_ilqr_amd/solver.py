@@ -364,6 +364,20 @@ def _on_device(F) -> bool:
     return False
 
 
+def _device_rows(F):
+    """F's device kernel on stacked rows, NumPy in / out (x [K, n], u [K, m] -> [K, n]):
+    the row-vectorised form host_dynamics uses for a built-in system whose stage cost is
+    a Python callable (one launch per FD linearisation, rollout step or line-search step
+    instead of one per F call)."""
+    def rows(X, U):
+        torch = _torch()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        Xt = torch.as_tensor(np.ascontiguousarray(X, dtype=float), device=dev).reshape(-1, F.n)
+        Ut = torch.as_tensor(np.ascontiguousarray(U, dtype=float), device=dev).reshape(-1, F.m)
+        return F.batch(Xt, Ut).cpu().numpy()
+    return rows
+
+
 def _is_obstacle_cost(extra_stage_cost) -> bool:
     from . import systems
     return extra_stage_cost is None or extra_stage_cost is systems.obstacle_stage_cost or \
@@ -492,8 +506,12 @@ def ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N: int, T_min: int, T_max: in
         system, kw = F.system_id, dict(dt=F.dt, obstacles=_obstacle_rows(extra_stage_cost))
     else:  # a Python callable (dynamics or stage cost): evaluated on the host per problem
         m = np.atleast_2d(np.asarray(R, dtype=float)).shape[0]
-        system = F if isinstance(F, host_dynamics.HostDynamics) else \
-            host_dynamics.HostDynamics(F, n, m)
+        if isinstance(F, host_dynamics.HostDynamics):
+            system = F
+        elif _on_device(F):  # a built-in system with a Python stage cost: F's rows in one launch
+            system = host_dynamics.HostDynamics(_device_rows(F), n, m, name=F.name, vectorized=True)
+        else:
+            system = host_dynamics.HostDynamics(F, n, m)
         kw = dict(extra_stage_cost=extra_stage_cost)
     res = ilqr_timeopt_batch(system, x0, xg, u_ref,
                              np.asarray(Q, dtype=float), np.atleast_2d(np.asarray(R, dtype=float)),

@@ -53,6 +53,10 @@ def main():
         Fv = host_dynamics.HostDynamics(dyn._scalar_F(sid, Fd.dt), len(x0), np.atleast_2d(R).shape[0],
                                         vectorized=True)
         t_vec, s_vec = _solve(Fv, mk, host_cost, a.repeat)
+        t_dpc = None
+        if host_cost is not None:  # the device system with the cost as a Python callable
+            t_dpc, s_dpc = _solve(Fd, mk, host_cost, a.repeat)
+            assert s_dpc["T_hist"] == s_dev["T_hist"]
         t0 = time.perf_counter()
         o = io.ilqr_timeopt(sid, Fd.dt, x0, xg, u_ref, Q, np.atleast_2d(R),
                             np.asarray(as_terminal_weight(alpha, len(x0))), w, N, T_min, T_max,
@@ -64,6 +68,7 @@ def main():
                                           abs(s_dev["J_hist"][-1])),
                               device_dynamics_s=round(t_dev, 4), host_callable_s=round(t_host, 4),
                               host_vectorized_s=round(t_vec, 4),
+                              device_dynamics_python_cost_s=None if t_dpc is None else round(t_dpc, 4),
                               oracle_1core_s=round(t_orc, 4))), flush=True)
 
     # a batch of quadrotor problems (x0 jittered by 1e-3): the device dynamics against the
