@@ -254,3 +254,44 @@ def test_linesearch_batch_vectorized_vs_per_call(golden_dir, tag):
         assert Jp == Jv or abs(Jp - Jv) <= 1e-12 * abs(Jp) or (np.isinf(Jp) and np.isinf(Jv))
         assert _rel(vec[0][b], per[0][b]) <= 1e-12 and _rel(vec[1][b], per[1][b]) <= 1e-12
     assert len(set(per[4].tolist())) >= 3
+
+
+def test_ilqr_timeopt_routes_callables(monkeypatch):
+    """solver.ilqr_timeopt's routing (no GPU: the batched loop is stubbed): a built-in
+    system with its own cost stays on the device; a Python stage cost with a built-in
+    system keeps F on the device kernel as row-vectorised host dynamics; any other
+    callable F is host dynamics (per call); a HostDynamics passes through"""
+    import torch
+    from time_opt_ilqr_amd import solver, systems
+    seen = {}
+
+    def fake_batch(system, x0, *a, **kw):
+        seen["system"], seen["kw"] = system, kw
+        N = a[6]
+        n = x0.shape[1]
+        return {"crashed": torch.zeros(1, dtype=torch.int32), "n_hist": torch.ones(1, dtype=torch.int32),
+                "X": torch.zeros(1, N + 1, n), "U": torch.zeros(1, N, 1), "J_hist": torch.zeros(1, 1),
+                "T_hist": torch.ones(1, 1, dtype=torch.int32), "timers": {},
+                "J_curve": torch.zeros(1, N), "T_star": torch.ones(1, dtype=torch.int32)}
+
+    monkeypatch.setattr(solver, "ilqr_timeopt_batch", fake_batch)
+    monkeypatch.setattr(solver, "_dev", lambda: torch.device("cpu"))
+    F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, wrap_idx, extra = \
+        systems.make_double_integrator(N=20)
+    args = (x0, xg, u_ref, Q, R, alpha, w, 20, 5, 20)
+    solver.ilqr_timeopt(F, *args)
+    assert seen["system"] == F.system_id and "dt" in seen["kw"]
+    cost = lambda x, u: (0.0, np.zeros(2), np.zeros((2, 2)))  # noqa: E731
+    solver.ilqr_timeopt(F, *args, extra_stage_cost=cost)
+    s = seen["system"]
+    assert isinstance(s, hd.HostDynamics) and s.vectorized and (s.n, s.m) == (2, 1)
+    assert seen["kw"]["extra_stage_cost"] is cost
+    Fp = dyn._scalar_F(0, F.dt)
+    solver.ilqr_timeopt(Fp, *args)
+    s = seen["system"]
+    assert isinstance(s, hd.HostDynamics) and not s.vectorized and s.F is Fp
+    Fh = hd.HostDynamics(Fp, 2, 1, vectorized=True)
+    solver.ilqr_timeopt(Fh, *args)
+    assert seen["system"] is Fh
+    with pytest.raises(TypeError):
+        solver.ilqr_timeopt(42, *args)
