@@ -461,6 +461,23 @@ def _s5_aug_side(dev, Bn=4096, N=200, t_min=40):
     torch.cuda.synchronize()
     ok = torch.isfinite(r_a.J).all(dim=1) & torch.isfinite(tr.J).all(dim=1)
     out["t_star_equal_traj_form"] = int(((r_a.t_star == tr.t_star) & ok).sum().item())
+    # s <= 5 hand-overs: one of these problems with the stage block made
+    # indefinite at every other step (chol_inv's ladder ends in the LU slot there, as the
+    # point-mass obstacle cost makes it), so the conditioned kernel hands them over; the
+    # pipelined rerun against the one-lane rerun (HOP_OPT_RERUN_LANE), bitwise compared
+    h = slice(0, 1)
+    Qh = blk.Q[h].clone()
+    Qh[:, 1::2, 0, 0] -= 1.0
+    hargs = (blk.A[h].contiguous(), blk.B[h].contiguous(), Qh, Ri, blk.z0, blk.QT[h].contiguous())
+    r_p, ms_p = timed(lambda: engine.propagate(*hargs, t_min=t_min, t_max=N))
+    r_l, ms_l = timed(lambda: engine.propagate(*hargs, t_min=t_min, t_max=N), {"rerun_lane": True})
+    out["handover_rerun"] = {
+        "ms_pipelined": ms_p, "ms_one_lane": ms_l, "speedup": ms_l / ms_p,
+        "problems_lu_slot": int(((r_p.status & _lib.ST_LU) != 0).sum().item()),
+        "bitwise_equal": bool(torch.equal(r_p.J.nan_to_num(7.0), r_l.J.nan_to_num(7.0)) and
+                              torch.equal(r_p.status, r_l.status) and torch.equal(r_p.t_star, r_l.t_star)),
+        "workload": "one of the batch's problems, Q_aug[k][0][0] - 1 at odd k (ladder + LU slot): "
+                    "select + rerun launch, pipelined against one lane"}
     out["problems_finite_both"] = int(ok.sum().item())
     out["workload"] = (f"fp64 s = 5, m = 1, N = {N}, B = {Bn}: cart-pole augmented blocks "
                        "(rho_reg = 1e-12) through propagator_all_Jt_aug + argmin")

@@ -140,8 +140,8 @@ def test_pipelined_small_rerun_bitwise(dev, s, m, N):
     stage blocks, compose chain and queries on three waves in beats of 64 steps)
     against the one-lane LFT kernel (HOP_OPT_RERUN_LANE) and the reference association
     alone: J, status, T*, J* bitwise.  Hand-overs are chol_inv LU slots (Q_k = -I) at
-    one, two and four problems of a workgroup (the pipeline) and at five (more than
-    kSmallPipeMax: the one-lane body); beats are cut at N = 1, 63, 64, 65, 150."""
+    one and two problems of a workgroup (the pipeline) and at four and five (more than
+    kSmallPipeMax = 3: the one-lane body); beats are cut at N = 1, 63, 64, 65, 150."""
     import torch
     from time_opt_ilqr_amd import _lib, engine
     Bn = 600
@@ -191,3 +191,43 @@ def test_pipelined_small_rerun_point_mass_outer_loop(dev):
         b = solver.ilqr_timeopt(F, x0, xg, u_ref, Q, R, alpha, w, N, T_min, T_max, **kw)
     assert a["T_hist"] == b["T_hist"] and a["J_hist"] == b["J_hist"]
     assert np.array_equal(a["J_curve"], b["J_curve"], equal_nan=True)
+
+
+@pytest.mark.parametrize("nb", [1, 2, 3, 4])
+def test_pipelined_small_rerun_many_lu_steps_bitwise(dev, nb):
+    """Real cart-pole augmented blocks (fp64, s = 5, N = 200) with the stage block made
+    indefinite at every other step, so chol_inv's ladder ends in the LU slot there and
+    the chain's W_k often does too: the pipelined rerun (one to three hand-overs per
+    workgroup; four run the one-lane body) against the one-lane rerun and the reference
+    association alone, J / status / T* bitwise (a side-by-side ladder once differed
+    here in the last bits from step 125 on: tools/dbg_handover.py)"""
+    import torch
+    from time_opt_ilqr_amd import _lib, engine, systems
+    from time_opt_ilqr_amd.utils import as_terminal_weight
+    N, Bn = 200, 8
+    F, x0, xg, u_ref, Q, R, alpha, w, _, _, _, wrap, _ = systems.make_cartpole_swingup(N=N)
+    g = torch.Generator(device=dev)
+    g.manual_seed(29)
+    kw = dict(device=dev, dtype=torch.float64, generator=g)
+    U = torch.as_tensor(u_ref, device=dev) + 2.0 * torch.randn((Bn, N, F.m), **kw)
+    X = engine.rollout(F.system_id, torch.as_tensor(x0, device=dev) +
+                       0.3 * torch.randn((Bn, F.n), **kw), U, F.dt)
+    P = _t(as_terminal_weight(alpha, F.n), dev)
+    Ri = torch.linalg.inv(_t(R, dev)).contiguous()
+    lin = engine.linearize(F.system_id, X, U, F.dt, central=True)
+    blk = engine.augment(lin.A, lin.B, lin.a_res, X, U, _t(xg, dev), _t(u_ref, dev), _t(Q, dev),
+                         P, w, wrap_idx=wrap)
+    h = slice(0, nb)
+    Qh = blk.Q[h].clone()
+    Qh[:, 1::2, 0, 0] -= 1.0
+    args = (blk.A[h].contiguous(), blk.B[h].contiguous(), Qh, Ri, blk.z0, blk.QT[h].contiguous())
+    a = engine.propagate(*args, t_min=50, t_max=N)
+    with _lib.options(rerun_lane=True):
+        b = engine.propagate(*args, t_min=50, t_max=N)
+    with _lib.options(reference_assoc=True):
+        c = engine.propagate(*args, t_min=50, t_max=N)
+    torch.cuda.synchronize()
+    assert all(int(v) & orc.ST_LU for v in a.status.tolist())
+    for o in (b, c):
+        assert torch.equal(a.J.nan_to_num(7.0), o.J.nan_to_num(7.0))
+        assert torch.equal(a.status, o.status) and torch.equal(a.t_star, o.t_star)

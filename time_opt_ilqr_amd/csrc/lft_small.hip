@@ -409,8 +409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
 // handed-over problem at a time, in beats of 64 steps:
 //   wave 0: the stage blocks E_k, F_k, G_k of beat b, one step per lane;
 //   wave 1: the compose chain of beat b - 1 (W_k and the prefix update), the same
-//           values on every lane, W_k's jitter-ladder attempts side by side
-//           (spd_inverse_lanes);
+//           values on every lane, W_k's LU slot column by column (spd_inverse_lanes);
 //   wave 2: the queries of beat b - 2, one horizon per lane, then the argmin in
 //           horizon order on lane 0.
 // The blocks pass through two LDS rings of two beats.  Every value comes from the
@@ -419,7 +418,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PW == 64 ? 
 // that instead; tests/test_gpu_small_rowgroup.py).  A workgroup with more than
 // kSmallPipeMax hand-overs runs the one-lane body on all of them (64 lanes in
 // parallel beat a sequence of pipelines there).
-constexpr int kSmallPipeMax = 4;
+constexpr int kSmallPipeMax = 3;
+// HOP_PIPE_SEQ_INV=1 (A/B): the chain's W_k by spd_inverse itself (no column-parallel LU)
+#ifndef HOP_PIPE_SEQ_INV
+#define HOP_PIPE_SEQ_INV 0
+#endif
 template <class T, int S, int MM>
 struct PipeSmallGeo {
   static constexpr int NP = S * (S + 1) / 2, SS = S * S;
@@ -456,13 +459,15 @@ __device__ __forceinline__ void get_step(const T* in, Sym<T, S>& e, Gen<T, S>& f
   for (int i = 0; i < NP; ++i) g.v[i] = in[NP + S * S + i];
 }
 
-// spd_inverse (small_math.hpp: chol_inv's jitter ladder, then the LU slot) with the
-// ladder's attempts side by side: lane t sweeps sym(M) + eps_t I, eps_t the ladder's
-// t-th jitter (the same repeated x10 from 1e-9, lanes past max_tries repeat the last),
-// and the first attempt that factors is broadcast, or the LU slot runs at the last
-// jitter when none does, lane c solving the identity's column c.  Each attempt is the same sweep on the same values as in
-// the sequential ladder, so the result and the status bits are bitwise its own; the
-// chain wave of the pipelined rerun calls it on all 64 lanes with the same input.
+// spd_inverse (small_math.hpp: chol_inv's jitter ladder, then the LU slot) for the chain
+// wave of the pipelined rerun, which calls it on all 64 lanes with the same input: the
+// ladder runs as in spd_inverse on every lane, and the LU slot's five right-hand sides
+// (the identity's columns) are solved side by side, lane c taking column c of the one
+// factorisation (a column's operations do not depend on the others', so the values are
+// lu_sym_solve_regs<T, S, S>'s bit for bit).  Running the ladder's attempts side by side
+// as well (lane t at jitter t, the first that factors broadcast) was measured 27 %
+// faster on the point-mass select but differs from the sequential ladder in the last
+// bits of some steps (tools/dbg_handover.py), so it is not used.
 template <class T, int S>
 __device__ __forceinline__ T bcast_lane(T v, int src) {
   if constexpr (sizeof(T) == 8) {
@@ -476,44 +481,39 @@ __device__ __forceinline__ T bcast_lane(T v, int src) {
 }
 template <class T, int S>
 __device__ __forceinline__ void spd_inverse_lanes(Sym<T, S>& m, int max_tries, unsigned& st, int lane) {
-  if (max_tries >= 63) {  // more attempts than lanes: the sequential ladder
-    spd_inverse(m, max_tries, st);
+  // the ladder as spd_inverse runs it (every lane the same attempts)
+  const Sym<T, S> in = m;
+  T eps = T(1e-9);
+  bool ok = sweep_neg_inverse(m, eps);
+  if (!ok && !all_finite(in)) {  // chol_inv's _assert_finite: no ladder
+    st |= kStNonfinite;
+#pragma unroll
+    for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = T(__builtin_nan(""));
     return;
   }
-  const Sym<T, S> in = m;
-  const int t = lane < max_tries ? lane : max_tries;
-  T eps = T(1e-9);
-#pragma unroll 1
-  for (int i = 0; i < t; ++i) eps *= T(10);
-  Sym<T, S> x = in;
-  const bool ok = sweep_neg_inverse(x, eps);
-  const unsigned long long okm = __ballot(ok);
-  if (!(okm & 1ull)) {
-    if (!all_finite(in)) {  // chol_inv's _assert_finite: no ladder (spd_inverse)
-      st |= kStNonfinite;
-#pragma unroll
-      for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = T(__builtin_nan(""));
-      return;
-    }
+  if (!ok) {
     st |= kStJitter;
-  }
-  if (okm != 0ull) {
-    const int first = __builtin_amdgcn_readfirstlane(__ffsll((long long)okm) - 1);
+    for (int tries = 1;; ++tries) {
+      eps *= T(10);
+      m = in;
+      ok = sweep_neg_inverse(m, eps);
+      if (ok) break;
+      if (tries >= max_tries) {  // the LU slot: lane c solves the identity's column c
+        st |= kStLu;
+        const int col = lane < S ? lane : S - 1;
+        T x[S][1];
 #pragma unroll
-    for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = bcast_lane<T, S>(x.v[k], first);
-  } else {  // the LU slot at the last jitter: lane c solves the identity's column c
-    st |= kStLu;  // (the same factorisation on every lane; a column's operations do not
-    const T e = bcast_lane<T, S>(eps, max_tries);  // depend on the other columns)
-    const int col = lane < S ? lane : S - 1;
-    T x[S][1];
+        for (int i = 0; i < S; ++i) x[i][0] = i == col ? T(1) : T(0);
+        const bool okl =
+            lu_sym_solve_regs<T, S, 1>([&](int i, int j) { return in.at(i, j); }, eps, x);
 #pragma unroll
-    for (int i = 0; i < S; ++i) x[i][0] = i == col ? T(1) : T(0);
-    const bool okl = lu_sym_solve_regs<T, S, 1>([&](int i, int j) { return in.at(i, j); }, e, x);
+        for (int i = 0; i < S; ++i)
 #pragma unroll
-    for (int i = 0; i < S; ++i)
-#pragma unroll
-      for (int j = i; j < S; ++j)
-        m.at(i, j) = okl ? -bcast_lane<T, S>(x[i][0], j) : T(__builtin_nan(""));
+          for (int j = i; j < S; ++j)
+            m.at(i, j) = okl ? -bcast_lane<T, S>(x[i][0], j) : T(__builtin_nan(""));
+        break;
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < Sym<T, S>::NP; ++k) m.v[k] = -m.v[k];
@@ -594,9 +594,13 @@ __device__ __forceinline__ void pipe_small_problem(const LftArgs<T>& a, long lon
           Sym<T, S> E, G;
           Gen<T, S> F;
           get_step<T, S>(ring + ((b1 & 1) * BS + j) * STG, E, F, G);
+#if HOP_PIPE_SEQ_INV
+          compose_step<T, S, MM>(ch, k, E, F, G, mt);
+#else
           compose_step<T, S, MM>(ch, k, E, F, G, mt, [&](Sym<T, S>& x, int t, unsigned& s_) {
             spd_inverse_lanes<T, S>(x, t, s_, lane);
           });
+#endif
           if (lane == 0)
             put_step<T, S>(ring + PG::OFF_C + ((b1 & 1) * BS + j) * STG, ch.Eb, ch.Fb, ch.Gb);
         }
