@@ -1,3 +1,14 @@
+"""Bitwise check of the s <= 5 rerun paths on blocks with many LU steps: real cart-pole
+augmented blocks (fp64, s = 5, N = 200) with Q_aug[k][0][0] - 1 at every odd k, so
+chol_inv's ladder ends in the LU slot there; one to four hand-overs per workgroup
+through the pipelined rerun (default), the one-lane rerun (HOP_OPT_RERUN_LANE) and the
+reference association alone (HOP_OPT_REFERENCE_ASSOC).  Prints status, T* and the J
+mismatch counts.  The same case is tests/test_gpu_small_rowgroup.py::
+test_pipelined_small_rerun_many_lu_steps_bitwise; this script found that a side-by-side
+jitter ladder differed in the last bits.
+
+    python tools/dbg_handover.py     (HOP_LIB=<path> for another library)
+"""
 import sys, os
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch
