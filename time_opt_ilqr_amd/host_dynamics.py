@@ -329,15 +329,16 @@ def linesearch(F, X, U, T_star: int, K, kff, cost_args, alphas, extra_stage_cost
         Xn = np.zeros_like(X)
         Xn[0] = X[0]
         ok = True
-        for k in range(N):
-            if k < T:
-                dx = wrap_error((Xn[k] - X[k]).reshape(-1), wrap_idx)
-                Un[k] = U[k] + ((np.asarray(K[k]) @ dx).reshape(-1)
-                                + float(al) * np.asarray(kff[k]).reshape(-1))
-            Xn[k + 1] = np.asarray(F(Xn[k], Un[k]), dtype=float).reshape(-1)
-            if not np.all(np.isfinite(Xn[k + 1])):
-                ok = False
-                break
+        with np.errstate(all="ignore"):  # a diverging rollout is rejected, quietly
+            for k in range(N):
+                if k < T:
+                    dx = wrap_error((Xn[k] - X[k]).reshape(-1), wrap_idx)
+                    Un[k] = U[k] + ((np.asarray(K[k]) @ dx).reshape(-1)
+                                    + float(al) * np.asarray(kff[k]).reshape(-1))
+                Xn[k + 1] = np.asarray(F(Xn[k], Un[k]), dtype=float).reshape(-1)
+                if not np.all(np.isfinite(Xn[k + 1])):
+                    ok = False
+                    break
         if not ok:
             continue
         J_new = cost_true(Xn, Un, xg, u_ref, Q, R, Qf, w, T, wrap_idx, extra_stage_cost)
